@@ -1,0 +1,200 @@
+"""Benchmark: stylized frames/s of the MHAdaSTr forward path on MI355X (BASELINE.json).
+
+A "step" is one full style-transfer forward — vit_c(content), vit_s(style),
+adaFormer(fc, fs) (infer_image.py:83-85 / infer_time.py:74-77) — over one synthetic batch
+already resident in HBM.  Headline workload = BASELINE configs[1]: 512x512, batch 8, fp32.
+The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path) under "configs".
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Multi-GPU: inference replicas: the ViT's batch-axis attention couples the
+images of one forward call, so a call's batch is never split; each rank runs its own batch,
+no collective on the data path (barrier + max-over-ranks timing only) -> scaling "weak".
+
+Roofline: the dominant kernel is the fused MHAda attention (mhada_attn, 6 launches/step);
+its algorithmic FLOPs per launch = 6*Nc*Ns*C*B (QK^T, PV, PV^2; 2 FLOP/MAC), timed live with
+HIP events on its launch stream over the timed region.  CPU baseline: the numpy oracle
+(oracle/mhada_oracle.py, a restatement of the reference) on one 512^2 frame on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "mhada-style-transfer_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch
+import torch.distributed as dist
+
+PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense MFMA peaks
+C = 512
+
+
+def flops_per_frame(res: int, style_res: int) -> dict:
+    """SURVEY.md §8(d) algorithmic FLOPs (2 FLOP/MAC)."""
+    nc, ns = (res // 8) ** 2, (style_res // 8) ** 2
+    d = 64
+    vit = lambda n: 72 * n * C * C + 196608 * n  # noqa: E731  (+12*N*B*C batch-attn, negligible)
+    mhada = 6 * (6 * nc * ns * C + 2 * (nc + 2 * ns) * C * d + 2 * nc * C * C)
+    dec = 30892032 * nc
+    return {"total": vit(nc) + vit(ns) + mhada + dec, "attn_per_block": 6 * nc * ns * C}
+
+
+def build_models(dtype):
+    import network
+    from mhada_hip.recipe import load_recipe
+    dev = torch.device("cuda", torch.cuda.current_device())
+    vc = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c").to(dev).eval()
+    vs = load_recipe(network.VisionTransformer(pos_embedding=False), "vit_s").to(dev).eval()
+    ada = load_recipe(network.AdaAttnTransformerMultiHead(), "ada").to(dev).eval()
+    for m in (vc, vs, ada):
+        m.compute_dtype = dtype
+    return vc, vs, ada
+
+
+def run_config(res, batch, dtype, steps, warmup, rank, world):
+    from mhada_hip import engine
+    from mhada_hip.recipe import seeded_image
+    vc, vs, ada = build_models(dtype)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    c = seeded_image(batch, res, res, 11 + 1000 * rank).to(dev)
+    s = seeded_image(batch, res, res, 12 + 1000 * rank).to(dev)
+
+    def step():
+        fc = vc(c)
+        fs = vs(s)
+        return ada(fc, fs)
+
+    with torch.no_grad():
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        log = {}
+        engine.record_kernel_events(log)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        engine.record_kernel_events(None)
+    assert torch.isfinite(out[1]).all()
+    ev = log.get("mhada_attn", [])
+    attn_ms = [a.elapsed_time(b) for a, b in ev]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    frames = batch * steps * world
+    dts = "f32" if dtype == torch.float32 else "bf16"
+    fl = flops_per_frame(res, res)
+    avg_attn_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
+    attn_flops = fl["attn_per_block"] * batch
+    achieved = attn_flops / avg_attn_s / 1e12
+    return {
+        "value": frames / elapsed,
+        "ms_per_step": elapsed / steps * 1e3,
+        "dtype": dts,
+        "frames_per_s_per_gpu": frames / elapsed / world,
+        "tflops_whole_step": fl["total"] * batch * steps / (elapsed) / 1e12,
+        "roofline": {"bound": "mfma", "kernel": "mhada_attn", "achieved": round(achieved, 2),
+                     "peak": PEAK_TFLOPS[dts], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dts], 4),
+                     "traffic": None, "avg_launch_ms": round(avg_attn_s * 1e3, 4),
+                     "flop_per_launch": attn_flops, "launches_timed": len(attn_ms)},
+        "config": {"workload": f"stylize {res}x{res} content+style, batch {batch}", "resolution": res,
+                   "batch_per_gpu": batch, "global_batch": batch * world, "compute_dtype": dts,
+                   "parallelism": f"replicas x{world}"},
+    }
+
+
+def cpu_baseline(seconds_budget=30.0):
+    """numpy oracle (restatement of the reference CPU path) on one 512x512 frame."""
+    import numpy as np
+    from mhada_hip.recipe import recipe_state_dict, seeded_image
+    from oracle import mhada_oracle as O
+    import network
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    shapes = lambda m: {k: tuple(v.shape) for k, v in m.state_dict().items()}  # noqa: E731
+    p_vc = O.to_numpy_params(recipe_state_dict("vit_c", shapes(network.VisionTransformer(pos_embedding=True))))
+    p_vs = O.to_numpy_params(recipe_state_dict("vit_s", shapes(network.VisionTransformer(pos_embedding=False))))
+    p_ada = O.to_numpy_params(recipe_state_dict("ada", shapes(network.AdaAttnTransformerMultiHead())))
+    c = seeded_image(1, 512, 512, 11).numpy()
+    s = seeded_image(1, 512, 512, 12).numpy()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        O.stylize(c, s, p_vc, p_vs, p_ada)
+        n += 1
+        if time.perf_counter() - t0 > seconds_budget / 3 or n >= 3:
+            break
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frame(s) of 512x512 B=1 through oracle/mhada_oracle.py (numpy fp32, "
+                      f"{threads} BLAS threads), same recipe weights; {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the 1024^2 bf16 config")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    main_cfg = run_config(512, 8, torch.float32, args.steps, args.warmup, rank, world)
+    second = None if args.no_secondary else run_config(1024, 4, torch.bfloat16, args.steps, args.warmup, rank, world)
+
+    if rank == 0:
+        line = {
+            "metric": "stylized frames/sec (whole job) at 512x512 batch 8 fp32 [configs[1]]",
+            "value": round(main_cfg["value"], 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(main_cfg["ms_per_step"], 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": main_cfg["dtype"],
+            "data": "synthetic rand*255 images, recipe random-init weights (no checkpoint ships)",
+            "config": main_cfg["config"],
+            "roofline": main_cfg["roofline"],
+            "tflops_whole_step": round(main_cfg["tflops_whole_step"], 2),
+        }
+        if second is not None:
+            line["configs"] = {"1024x1024_b4_bf16": {k: second[k] for k in
+                                                    ("value", "ms_per_step", "frames_per_s_per_gpu", "dtype",
+                                                     "tflops_whole_step", "roofline", "config")}}
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+/*
+ * mhada_hip.h — C-ABI of libmhada_hip.so, the MI355X (gfx950) kernels behind the MHAdaSTr
+ * style-transfer forward path.
+ *
+ * The reference (Maboroshi0327/MHAda-Style-Transfer, MHAdaSTr/) is pure PyTorch: its
+ * "interface" for this path is the Python module API of MHAdaSTr/network/ (SURVEY.md §8b).
+ * Every entry point below replaces the aten op(s) a reference module calls; the file:line of
+ * that call is given per function.  The host side that mirrors the reference module API
+ * (mhada-style-transfer_amd/network/) binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - Plain C: device pointers, sizes, strides (in ELEMENTS), dtype codes, an opaque stream.
+ *   - The caller owns every buffer; the library never allocates device memory.
+ *   - Everything is enqueued on `stream` (a hipStream_t; NULL = default stream); no call
+ *     synchronises, so all entry points are hipGraph-capturable.
+ *   - Return 0 on success; non-zero = bad argument (1) or launch failure (2); the message is
+ *     available from mhada_last_error() (thread-local).
+ *   - Internal activations are token-major ("NHWC": [batch][token][channel]).
+ */
+#ifndef MHADA_HIP_H
+#define MHADA_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mhada_stream_t; /* hipStream_t */
+
+enum { MHADA_OK = 0, MHADA_ERR_ARG = 1, MHADA_ERR_LAUNCH = 2 };
+enum { MHADA_F32 = 0, MHADA_BF16 = 1 };
+enum { MHADA_ACT_SOFTMAX = 0, MHADA_ACT_COSINE = 1 };
+enum {
+  MHADA_A_ROWS = 0,        /* A[m*lda + k], row-major                                     */
+  MHADA_A_PATCH8 = 1,      /* A = im2col of an NCHW fp32 image, 8x8 patches, stride 8     */
+  MHADA_A_CONV3X3 = 2,     /* A = im2col of NHWC input, 3x3 taps, ReflectionPad2d(1)      */
+  MHADA_A_CONV3X3_UP2 = 3  /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
+};
+
+int mhada_abi_version(void);
+const char* mhada_last_error(void);
+
+/*
+ * Batched NT GEMM with fused epilogue:
+ *   C[z][m][n] = act(sum_k A[z][m][k] * W[z][n][k] + bias[z][n]) + R[z][m][n]
+ * z = (z1, z2) in [0,nb1) x [0,nb2); each operand has per-level strides (0 = shared).
+ * A is loaded in `a_mode` (see enum) from dtype a_dtype and converted to `compute`
+ * (MFMA input type: fp32 -> v_mfma_f32_32x32x2_f32, bf16 -> v_mfma_f32_32x32x16_bf16).
+ * ROWS mode may centre A per column on load: A[m][k] - a_mu[z1*smu1 + z2*smu2 + k].
+ * W has dtype `compute`; bias/R are optional (NULL).
+ *
+ * Replaces: PatchEmbedding conv 8x8/8 (vit.py:109,113) [PATCH8 + pos-embed as R];
+ *   MHA in_proj/out_proj addmm + residual (vit.py:59-60); MLP Linear/ReLU/Linear + residual
+ *   (vit.py:49-53,63); the per-head 1x1 convs f/g/h (adaDecoder.py:143-145,173,178,182);
+ *   out_conv (adaDecoder.py:152,205); Decoder ReflectionPad2d+Conv3x3+ReLU(+bilinear x2)
+ *   (conv.py:23-33,36-45,61-72) [CONV3X3 / CONV3X3_UP2].
+ */
+typedef struct mhada_gemm_args {
+  int M, N, K;
+  int nb1, nb2;
+  int compute;  /* MHADA_F32 | MHADA_BF16 */
+  int a_mode;   /* MHADA_A_* */
+  const void* a; int a_dtype; long long lda, sa1, sa2;
+  const float* a_mu; long long smu1, smu2;
+  /* PATCH8: img_c/h/w of the NCHW image (a_dtype must be F32).
+     CONV*: img_c = Cin, img_h/img_w = spatial size of the NHWC INPUT tensor; the output grid
+     is img_h x img_w (CONV3X3) or 2*img_h x 2*img_w (CONV3X3_UP2); M = batch*out_h*out_w. */
+  int img_c, img_h, img_w;
+  const void* w; long long ldw, sw1, sw2;
+  const float* bias; long long sb1, sb2;
+  const void* r; int r_dtype; long long ldr, sr1, sr2;
+  void* c; int c_dtype; long long ldc, sc1, sc2;
+  int relu;
+} mhada_gemm_args;
+
+int mhada_gemm(const mhada_gemm_args* args, mhada_stream_t stream);
+
+/* Row LayerNorm over `cols` (eps 1e-6 in the ViT): y = (x-mean)/sqrt(var+eps)*gamma + beta.
+ * x fp32 [rows][cols]; y dtype y_dtype.  Replaces nn.LayerNorm (vit.py:54-55,58,62). */
+int mhada_layernorm(const float* x, void* y, int y_dtype, const float* gamma, const float* beta,
+                    int rows, int cols, float eps, mhada_stream_t stream);
+
+/* nn.MultiheadAttention(batch_first=False) applied to a (B, N, C) tensor (vit.py:48,59):
+ * the SEQUENCE axis is the batch axis.  For each token n and head h:
+ *   out[i][n][h] = sum_j softmax_j(q[i][n][h] . k[j][n][h] / sqrt(d)) v[j][n][h]
+ * qkv [L][ntok][3C] (packed q|k|v, dtype), out [L][ntok][C] (dtype); L = batch size. */
+int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L, int ntok, int heads,
+                         int head_dim, mhada_stream_t stream);
+
+/* PosEmbedding (vit.py:81-102): bilinear (align_corners=False) resize of pos (C, bh, bw)
+ * fp32 to (oh, ow), written token-major out[oh*ow][C] fp32 (copy when sizes match). */
+int mhada_pos_embed(const float* pos, float* out, int C, int bh, int bw, int oh, int ow,
+                    mhada_stream_t stream);
+
+/* InstanceNorm2d(affine=False) statistics (adaDecoder.py:147-149): per (b, c) mean and
+ * 1/sqrt(biased var + eps) over the N tokens of x [B][N][C] fp32.  `work` holds
+ * splits*B*C*2 doubles (any splits >= 1). */
+int mhada_instnorm_stats(const float* x, float* mu, float* rstd, double* work, int B, int N,
+                         int C, int splits, float eps, mhada_stream_t stream);
+
+/* Fold the InstanceNorm scale into the per-head 1x1-conv weights of one AdaAttnMultiHead
+ * block (adaDecoder.py:173,178,182) and derive the style-side mean of V:
+ *   wq[b][h][o][c]  = Wf[h][o][c] * rstd_c[b][64h+c]            (A is centred on load)
+ *   wkv[b][h][o][c] = o<64 ? Wg[h][o][c] * rstd_s[b][64h+c] : Wh[h][o-64][c]
+ *   bkv[h][o]       = o<64 ? bg[h][o] : 0                        (V' = V - mean_tokens(V))
+ *   v_mu[b][64h+o]  = sum_c Wh[h][o][c] * mu_s[b][64h+c] + bh[h][o]
+ * W* fp32 [H][64][64]; wq/wkv dtype `dtype`. */
+int mhada_fold_block(const float* wf, const float* wg, const float* wh, const float* bg,
+                     const float* bh, const float* rstd_c, const float* mu_s,
+                     const float* rstd_s, void* wq, void* wkv, float* bkv, float* v_mu,
+                     int dtype, int B, int H, mhada_stream_t stream);
+
+/* bf16 path: VT[b][h][o][n] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), from
+ * kv [B][H][Ns][128]; the transposed operand image the attention kernel streams. */
+int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t stream);
+
+/* L2-normalise the 64-wide rows of q [B][H][Nc][64] and the K half of kv [B][H][Ns][128]
+ * in place (CosineSimilarity, adaDecoder.py:30-32). */
+int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns,
+                      mhada_stream_t stream);
+
+/* Fused multi-head adaptive attention (adaDecoder.py:186-198), one launch per block:
+ *   A = softmax(Q K^T) (no 1/sqrt(d); or the cosine form), M = A V, E2 = A V^2,
+ *   S = sqrt(max(E2 - M^2, 1e-6)), out = S * IN(fcs) + M
+ * computed flash-style (A never materialised) with V centred (v_mu added back to M).
+ * q [B][H][Nc][64], kv [B][H][Ns][128] (K | V'), vt (bf16 only) [B][H][128][Ns],
+ * fcs [B][Nc][64H] fp32 with its stats fcs_mu/fcs_rstd [B][64H], v_mu [B][64H];
+ * out [B][Nc][64H] dtype. */
+int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
+               const float* fcs_mu, const float* fcs_rstd, const float* v_mu, void* out,
+               int dtype, int B, int H, int Nc, int Ns, int activation, mhada_stream_t stream);
+
+/* Last decoder layer (conv.py:96, ConvReLU(64, 3)): ReflectionPad2d(1) + conv3x3 Cin->3 +
+ * bias + ReLU on NHWC x [B][H][W][Cin] (dtype), written NCHW fp32 y [B][3][H][W] — the
+ * module's output layout.  clamp255 != 0 also applies the caller's clamp(0,255)
+ * (infer_image.py:86). w fp32 [3][3][3][Cin] (out, ky, kx, cin). */
+int mhada_conv3x3_out3(const void* x, int dtype, const float* w, const float* b, float* y,
+                       int B, int H, int W, int Cin, int clamp255, mhada_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHADA_HIP_H */

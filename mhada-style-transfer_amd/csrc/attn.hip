@@ -1,0 +1,405 @@
+// Fused multi-head adaptive attention (MHAda), flash-style, one launch per block.
+//
+// Reference: AdaAttnMultiHead.forward (MHAdaSTr/network/adaDecoder.py:162-206).  Per head:
+//   A = softmax(Q K^T)  (no 1/sqrt(d)!)     M = A V      E2 = A V^2
+//   S = sqrt(max(E2 - M^2, 1e-6))           out = S * InstanceNorm(fcs) + M
+// The reference materialises A (Nc x Ns fp32 per head).  Here A never leaves registers:
+// each wave owns 32 query rows and streams 64-key tiles, keeping two output accumulators
+// (sum p*v' and sum p*v'^2 over the centred V' = V - mean_tokens(V); the variance is
+// shift-invariant, so the centring only removes E2 - M^2 cancellation) plus the running
+// max / sum of an online softmax.
+//
+// Orientation ("swapped" products, cdna_hip_programming.md §3 accumulator-as-operand):
+//   S^T (keys x queries) = K . Q^T  — the query is on the MFMA lane, so every lane holds
+//       scores of ONE query: the row max/sum are lane-local plus one cross-half shuffle;
+//   O^T (dv x queries)   = V'^T . P^T — P^T is the S^T accumulator itself, used as the B
+//       operand with no lane movement; the dv/key index pairing follows the accumulator's
+//       row permutation.
+// fp32: v_mfma_f32_32x32x2_f32 (exact fp32), K/V' streamed from kv[.][128] into LDS, V'^2
+//       formed in registers.  bf16: v_mfma_f32_32x32x16_bf16, V'^T and V'^2^T streamed from
+//       the pre-transposed vt image (mhada_transpose_v), fp32 accumulation and softmax.
+// Block = 4 waves = 128 queries of one (batch, head); blocks of one (b, h) are remapped onto
+// one XCD so they share K/V in its L2.
+#include "common.h"
+
+namespace mhada {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+struct AttnP {
+  const void* q;    // [B][H][Nc][64]
+  const void* kv;   // [B][H][Ns][128]
+  const void* vt;   // bf16: [B][H][128][ldt]
+  const float* fcs; // [B][Nc][C]
+  const float* fcs_mu;
+  const float* fcs_rstd;
+  const float* v_mu;
+  void* out;        // [B][Nc][C]
+  int B, H, Nc, Ns, ldt, nqb, nblk;
+};
+
+MHADA_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Epilogue shared by both variants.  O[blk] holds O^T[dv][q] for dv = (r&3)+8(r>>2)+4h+32(blk&1);
+// blk 0,1: sum p v'   blk 2,3: sum p v'^2.
+template <typename T>
+MHADA_DEV void attn_epilogue(const AttnP& p, const f32x16 (&O)[4], float l, int b, int hh, int q, int h) {
+  const int C = p.H * 64;
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q >= p.Nc) return;
+  const float inv = 1.0f / lt;
+  const float* fr = p.fcs + ((long long)b * p.Nc + q) * C + hh * 64;
+  const float* mu = p.fcs_mu + (long long)b * C + hh * 64;
+  const float* rs = p.fcs_rstd + (long long)b * C + hh * 64;
+  const float* vm = p.v_mu + (long long)b * C + hh * 64;
+  T* orow = reinterpret_cast<T*>(p.out) + ((long long)b * p.Nc + q) * C + hh * 64;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // 4 contiguous dv per group
+      const int dv0 = 8 * g + 4 * h + 32 * blk;
+      const f32x4 f = *reinterpret_cast<const f32x4*>(fr + dv0);
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(mu + dv0);
+      const f32x4 r4 = *reinterpret_cast<const f32x4*>(rs + dv0);
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(vm + dv0);
+      float res[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[blk][4 * g + e] * inv;
+        const float e2 = O[blk + 2][4 * g + e] * inv;
+        const float sd = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f));
+        res[e] = sd * ((f[e] - m4[e]) * r4[e]) + (m1 + v4[e]);
+      }
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(orow + dv0) = f32x4{res[0], res[1], res[2], res[3]};
+      } else {
+        *reinterpret_cast<bf16x4*>(orow + dv0) = bf16x4{(bf16)res[0], (bf16)res[1], (bf16)res[2], (bf16)res[3]};
+      }
+    }
+  }
+}
+
+// Online-softmax update of one tile (32 scores per lane: S[kb][r], key index
+// kb*32 + (r&3) + 8(r>>2) + 4h); returns the rescale factor for O.  Cosine: p = s (+1 done
+// by caller), no max.
+template <int ACT>
+MHADA_DEV float softmax_tile(f32x16 (&S)[2], float& m, float& l, int key0, int Ns, int h) {
+  const bool partial = key0 + 64 > Ns;
+  if (partial) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (key >= Ns) S[kb][r] = (ACT == MHADA_ACT_SOFTMAX) ? -INFINITY : -1.0f;
+      }
+  }
+  if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+    float mx = S[0][0];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[kb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = fast_exp2((m - mn) * kLog2e);
+    const float mb = mn * kLog2e;
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = fast_exp2(S[kb][r] * kLog2e - mb);
+        S[kb][r] = pv;
+        sum += pv;
+      }
+    l = l * alpha + sum;
+    m = mn;
+    return alpha;
+  } else {
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = S[kb][r] + 1.0f;  // masked keys: -1 + 1 = 0
+        S[kb][r] = pv;
+        sum += pv;
+      }
+    l += sum;
+    return 1.0f;
+  }
+}
+
+MHADA_DEV void decode_block(const AttnP& p, int& b, int& hh, int& qb) {
+  const int t = xcd_remap(blockIdx.x, p.nblk);
+  qb = t % p.nqb;
+  const int bh = t / p.nqb;
+  b = bh / p.H;
+  hh = bh - b * p.H;
+}
+
+// ======================================================================================
+// fp32 variant
+// ======================================================================================
+template <int ACT>
+__global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
+  constexpr int LS = 132;  // LDS row (128 + 4 floats): conflict-free b128 K reads, b32 V reads
+  __shared__ __attribute__((aligned(16))) float sKV[2][64 * LS];
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * 128 + wave * 32 + r32;
+  const long long bh = (long long)b * p.H + hh;
+
+  // Q^T operand: MFMA step s takes d = 32h + s
+  float qreg[32];
+  {
+    const float* qp = reinterpret_cast<const float*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(qp + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qreg[4 * i + e] = (q < p.Nc) ? t[e] : 0.f;
+    }
+  }
+  const float* kvb = reinterpret_cast<const float*>(p.kv) + bh * p.Ns * 128;
+
+  // staging: 64 keys x 128 floats = 2048 16-B chunks, 8 per thread (row = c >> 5, col = c & 31)
+  f32x4 stg[8];
+  auto issue = [&](int key0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 4;
+      const int key = key0 + row;
+      stg[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto commit = [&](float* dst) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 4;
+      *reinterpret_cast<f32x4*>(dst + row * LS + col) = stg[i];
+    }
+  };
+
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int NT = (p.Ns + 63) / 64;
+  issue(0);
+  commit(sKV[0]);
+  __syncthreads();
+  for (int t = 0; t < NT; ++t) {
+    const float* cur = sKV[t & 1];
+    if (t + 1 < NT) issue((t + 1) * 64);
+    // ---- S^T = K . Q^T --------------------------------------------------------------
+    f32x16 S[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[kb][e] = 0.f;
+      const float* krow = cur + (kb * 32 + r32) * LS + 32 * h;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f32x4 kk = *reinterpret_cast<const f32x4*>(krow + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          S[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk[e], qreg[4 * i + e], S[kb], 0, 0, 0);
+      }
+    }
+    // ---- online softmax ---------------------------------------------------------------
+    const float alpha = softmax_tile<ACT>(S, m, l, t * 64, p.Ns, h);
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
+    }
+    // ---- O^T += V'^T . P^T , (V'^2)^T . P^T ----------------------------------------
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float* vrow = cur + key * LS + 64;
+        const float v0 = vrow[r32], v1 = vrow[32 + r32];
+        const float pr = S[kb][r];
+        O[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, pr, O[0], 0, 0, 0);
+        O[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, pr, O[1], 0, 0, 0);
+        O[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0 * v0, pr, O[2], 0, 0, 0);
+        O[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1 * v1, pr, O[3], 0, 0, 0);
+      }
+    }
+    if (t + 1 < NT) commit(sKV[(t + 1) & 1]);
+    __syncthreads();
+  }
+  attn_epilogue<float>(p, O, l, b, hh, q, h);
+}
+
+// ======================================================================================
+// bf16 variant
+// ======================================================================================
+template <int ACT>
+__global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
+  constexpr int LK = 72;   // K tile row: 64 + 8 bf16 (144 B)
+  constexpr int LV = 68;   // VT tile row: 64 + 4 bf16 (136 B): conflict-free b64 reads
+  constexpr int KSZ = 64 * LK, VSZ = 128 * LV;
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][KSZ];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][VSZ];
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * 128 + wave * 32 + r32;
+  const long long bh = (long long)b * p.H + hh;
+
+  // Q^T operand: k-step s takes d = 16s + 8h + j
+  bf16x8 qf[4];
+  {
+    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+      if (q >= p.Nc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
+      }
+    }
+  }
+  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * p.Ns * 128;
+  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
+
+  // staging: K 64 rows x 8 chunks (2/thread), VT 128 rows x 8 chunks (4/thread)
+  bf16x8 sk[2], sv[4];
+  auto issue = [&](int key0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+      const int key = key0 + row;
+      if (key < p.Ns) {
+        sk[i] = *reinterpret_cast<const bf16x8*>(kvb + (long long)key * 128 + col);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sk[i][e] = (bf16)0.0f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+      sv[i] = *reinterpret_cast<const bf16x8*>(vtb + (long long)row * p.ldt + key0 + col);  // zero-padded to ldt
+    }
+  };
+  auto commit = [&](bf16* dk, bf16* dv) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<bf16x8*>(dk + row * LK + col) = sk[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+      // 136-B rows are only 8-B aligned: two b64 writes
+      bf16x4 lo = {sv[i][0], sv[i][1], sv[i][2], sv[i][3]};
+      bf16x4 hi = {sv[i][4], sv[i][5], sv[i][6], sv[i][7]};
+      *reinterpret_cast<bf16x4*>(dv + row * LV + col) = lo;
+      *reinterpret_cast<bf16x4*>(dv + row * LV + col + 4) = hi;
+    }
+  };
+
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int NT = (p.Ns + 63) / 64;
+  issue(0);
+  commit(sK[0], sV[0]);
+  __syncthreads();
+  for (int t = 0; t < NT; ++t) {
+    const bf16* ck = sK[t & 1];
+    const bf16* cv = sV[t & 1];
+    if (t + 1 < NT) issue((t + 1) * 64);
+    f32x16 S[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[kb][e] = 0.f;
+      const bf16* krow = ck + (kb * 32 + r32) * LK + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kk = *reinterpret_cast<const bf16x8*>(krow + 16 * s);
+        S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[s], S[kb], 0, 0, 0);
+      }
+    }
+    const float alpha = softmax_tile<ACT>(S, m, l, t * 64, p.Ns, h);
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        // B = P^T: element j <-> key kb*32 + 16s + 8(j>>2) + 4h + (j&3)  (accumulator regs 8s..8s+7)
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (bf16)S[kb][8 * s + j];
+        const int kofs = kb * 32 + 16 * s + 4 * h;
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+          const bf16* vrow = cv + (32 * blk + r32) * LV + kofs;
+          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow);
+          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + 8);
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < NT) commit(sK[(t + 1) & 1], sV[(t + 1) & 1]);
+    __syncthreads();
+  }
+  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
+}
+
+}  // namespace mhada
+
+using namespace mhada;
+
+extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs, const float* fcs_mu,
+                          const float* fcs_rstd, const float* v_mu, void* out, int dtype, int B, int H, int Nc,
+                          int Ns, int activation, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!q || !kv || !fcs || !fcs_mu || !fcs_rstd || !v_mu || !out || B <= 0 || H <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn: bad args");
+  if (dtype == MHADA_BF16 && !vt) return fail("mhada_attn: bf16 needs the transposed V image");
+  if (activation != MHADA_ACT_SOFTMAX && activation != MHADA_ACT_COSINE) return fail("mhada_attn: bad activation");
+  AttnP p;
+  p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
+  p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
+  p.ldt = (Ns + 63) / 64 * 64;
+  p.nqb = (Nc + 127) / 128;
+  const long long nblk = (long long)B * H * p.nqb;
+  if (nblk > (1LL << 31) - 1) return fail("mhada_attn: grid too large");
+  p.nblk = (int)nblk;
+  const dim3 grid(p.nblk), blk(256);
+  if (dtype == MHADA_F32) {
+    if (activation == MHADA_ACT_SOFTMAX)
+      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX>), grid, blk, 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE>), grid, blk, 0, s, p);
+  } else {
+    if (activation == MHADA_ACT_SOFTMAX)
+      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX>), grid, blk, 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE>), grid, blk, 0, s, p);
+  }
+  return check_launch("mhada_attn");
+}

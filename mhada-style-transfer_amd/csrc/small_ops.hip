@@ -1,0 +1,407 @@
+// Bandwidth-bound kernels of the forward path: LayerNorm, the ViT's batch-axis attention,
+// the positional-embedding resize, InstanceNorm (AdaIN) statistics, the per-block weight
+// fold, the V transpose for the bf16 attention, the cosine row normalisation and the last
+// (Cin -> 3) decoder convolution.  All activations are token-major.
+#include "common.h"
+
+namespace mhada {
+
+// ---------------------------------------------------------------------------------------
+// LayerNorm (vit.py:54-55): one wave per row, VPL = cols/64 values per lane, two-pass in
+// registers (mean, then centred sum of squares) — biased variance as nn.LayerNorm.
+// ---------------------------------------------------------------------------------------
+template <typename TO, int VPL>
+__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, TO* __restrict__ y,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ b, int rows, float eps) {
+  constexpr int COLS = VPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * COLS;
+  float v[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(xr + (i * 64 + lane) * 4);
+    v[4 * i] = t[0]; v[4 * i + 1] = t[1]; v[4 * i + 2] = t[2]; v[4 * i + 3] = t[3];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.0f / COLS);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const float d = v[i] - mean;
+    ss += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / COLS) + eps);
+  TO* yr = y + (long long)row * COLS;
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = (i * 64 + lane) * 4 + e;
+      yr[c] = from_f32<TO>((v[4 * i + e] - mean) * rstd * g[c] + b[c]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Batch-axis multi-head attention of the ViT (vit.py:48,59; batch_first=False on (B,N,C)):
+// one wave per (token, head); lane = feature d (head_dim 64).  L = batch size is small.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) vit_batch_attn_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                             int L, int ntok, int heads) {
+  constexpr int D = 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long pair = (long long)blockIdx.x * 4 + wv;
+  const int C = heads * D;
+  if (pair >= (long long)ntok * heads) return;
+  const int n = (int)(pair / heads), hh = (int)(pair - (long long)n * heads);
+  const float scale = 0.125f;                            // 1/sqrt(64)
+  const long long row_stride = (long long)ntok * 3 * C;  // between sequence (= batch) positions
+  const T* base = qkv + (long long)n * 3 * C + hh * D + lane;
+  for (int i = 0; i < L; ++i) {
+    const float qi = to_f32<T>(base[i * row_stride]) * scale;
+    float m = -INFINITY, l = 0.f, o = 0.f;  // online softmax over the L keys
+    for (int j = 0; j < L; ++j) {
+      const float sj = wave_sum(qi * to_f32<T>(base[j * row_stride + C]));
+      const float mn = fmaxf(m, sj);
+      const float a = __expf(m - mn), p = __expf(sj - mn);
+      l = l * a + p;
+      o = o * a + p * to_f32<T>(base[j * row_stride + 2 * C]);
+      m = mn;
+    }
+    out[((long long)i * ntok + n) * C + hh * D + lane] = from_f32<T>(o / l);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// PosEmbedding resize (vit.py:91-92) to token-major [oh*ow][C]
+// ---------------------------------------------------------------------------------------
+__global__ void pos_embed_kernel(const float* __restrict__ pos, float* __restrict__ out, int C, int bh,
+                                 int bw, int oh, int ow) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)oh * ow * C) return;
+  const int c = (int)(idx % C);
+  const int tkn = (int)(idx / C);
+  const int oy = tkn / ow, ox = tkn - (tkn / ow) * ow;
+  const float* pc = pos + (long long)c * bh * bw;
+  if (oh == bh && ow == bw) {
+    out[idx] = pc[oy * bw + ox];
+    return;
+  }
+  const float shy = (float)bh / (float)oh, shx = (float)bw / (float)ow;
+  const float sy = fmaxf(shy * ((float)oy + 0.5f) - 0.5f, 0.f);
+  const float sx = fmaxf(shx * ((float)ox + 0.5f) - 0.5f, 0.f);
+  const int y0 = min((int)sy, bh - 1), x0 = min((int)sx, bw - 1);
+  const int y1 = y0 + (y0 < bh - 1 ? 1 : 0), x1 = x0 + (x0 < bw - 1 ? 1 : 0);
+  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  out[idx] = ly0 * (lx0 * pc[y0 * bw + x0] + lx1 * pc[y0 * bw + x1]) +
+             ly1 * (lx0 * pc[y1 * bw + x0] + lx1 * pc[y1 * bw + x1]);
+}
+
+// ---------------------------------------------------------------------------------------
+// InstanceNorm statistics: partial sums in fp64 per (split, b, c), then a finalize pass.
+// grid (C/64, B, splits), 256 threads = 64 channels x 4 row phases (coalesced 256-B rows).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) in_partial_kernel(const float* __restrict__ x, double* __restrict__ work,
+                                                         int B, int N, int C, int splits) {
+  __shared__ double red[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  const int b = blockIdx.y, s = blockIdx.z;
+  const int per = (N + splits - 1) / splits;
+  const int r0 = s * per, r1 = min(N, r0 + per);
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    const float* xb = x + (long long)b * N * C + c;
+    for (int r = r0 + ph; r < r1; r += 4) {
+      const double v = (double)xb[(long long)r * C];
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  red[0][ph][threadIdx.x & 63] = s1;
+  red[1][ph][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    const int t = threadIdx.x & 63;
+    const double a = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
+    const double q = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
+    double* w = work + (((long long)s * B + b) * C + c) * 2;
+    w[0] = a;
+    w[1] = q;
+  }
+}
+
+__global__ void in_finalize_kernel(const double* __restrict__ work, float* __restrict__ mu,
+                                   float* __restrict__ rstd, int B, int N, int C, int splits, float eps) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * C) return;
+  double a = 0.0, q = 0.0;
+  for (int s = 0; s < splits; ++s) {
+    a += work[((long long)s * B * C + idx) * 2];
+    q += work[((long long)s * B * C + idx) * 2 + 1];
+  }
+  const double mean = a / N;
+  double var = q / N - mean * mean;
+  if (var < 0.0) var = 0.0;
+  mu[idx] = (float)mean;
+  rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// ---------------------------------------------------------------------------------------
+// Weight fold for one AdaAttnMultiHead block, grid B*H, 256 threads.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf, const float* __restrict__ wg,
+                                                   const float* __restrict__ wh, const float* __restrict__ bg,
+                                                   const float* __restrict__ bh, const float* __restrict__ rstd_c,
+                                                   const float* __restrict__ mu_s, const float* __restrict__ rstd_s,
+                                                   T* __restrict__ wq, T* __restrict__ wkv, float* __restrict__ bkv,
+                                                   float* __restrict__ v_mu, int H) {
+  constexpr int D = 64;
+  const int b = blockIdx.x / H, hh = blockIdx.x - (blockIdx.x / H) * H;
+  const int C = H * D;
+  const float* rc = rstd_c + (long long)b * C + hh * D;
+  const float* rs = rstd_s + (long long)b * C + hh * D;
+  const float* ms = mu_s + (long long)b * C + hh * D;
+  const float* Wf = wf + (long long)hh * D * D;
+  const float* Wg = wg + (long long)hh * D * D;
+  const float* Wh = wh + (long long)hh * D * D;
+  T* oq = wq + (long long)blockIdx.x * D * D;
+  T* okv = wkv + (long long)blockIdx.x * 2 * D * D;
+  for (int i = threadIdx.x; i < D * D; i += 256) {
+    const int c = i & (D - 1);
+    oq[i] = from_f32<T>(Wf[i] * rc[c]);
+    okv[i] = from_f32<T>(Wg[i] * rs[c]);
+    okv[D * D + i] = from_f32<T>(Wh[i]);
+  }
+  if (threadIdx.x < D) {
+    const int o = threadIdx.x;
+    float acc = bh[hh * D + o];
+    for (int c = 0; c < D; ++c) acc += Wh[o * D + c] * ms[c];
+    v_mu[(long long)b * C + hh * D + o] = acc;
+    if (b == 0) {
+      bkv[hh * 2 * D + o] = bg[hh * D + o];
+      bkv[hh * 2 * D + D + o] = 0.f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// V transpose for the bf16 attention: vt[bh][o][n] = V'[n][o], vt[bh][64+o][n] = V'[n][o]^2
+// (row stride ldt = Ns rounded up to 64, padding zero-filled).  64x64 tiles through LDS.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) transpose_v_kernel(const bf16* __restrict__ kv, bf16* __restrict__ vt,
+                                                          int Ns, int ldt) {
+  __shared__ float tile[64][65];
+  const int bh = blockIdx.y, n0 = blockIdx.x * 64;
+  const bf16* src = kv + (long long)bh * Ns * 128 + 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int n = i >> 6, o = i & 63;
+    tile[n][o] = (n0 + n < Ns) ? (float)src[(long long)(n0 + n) * 128 + o] : 0.f;
+  }
+  __syncthreads();
+  bf16* dst = vt + (long long)bh * 128 * ldt + n0;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int o = i >> 6, n = i & 63;
+    const float v = tile[n][o];
+    dst[(long long)o * ldt + n] = (bf16)v;
+    dst[(long long)(64 + o) * ldt + n] = (bf16)(v * v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Cosine activation prep (adaDecoder.py:30-32): L2-normalise 64-wide rows in place.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) rownorm_kernel(T* __restrict__ x, long long rows, int ld) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  T* r = x + row * ld;
+  const float v = to_f32<T>(r[lane]);
+  const float n = sqrtf(wave_sum(v * v));
+  r[lane] = from_f32<T>(v / n);
+}
+
+// ---------------------------------------------------------------------------------------
+// Last decoder layer: ReflectionPad(1) + conv3x3 Cin->3 + bias + ReLU, NHWC in, NCHW fp32 out.
+// One thread per output pixel; the 27*Cin weights live in LDS.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, float* __restrict__ y,
+                                                        int B, int H, int W, int Cin, int clamp255) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sw = reinterpret_cast<float*>(smem);  // [tap][cin][3]
+  for (int i = threadIdx.x; i < 27 * Cin; i += 256) {
+    const int o = i / (9 * Cin), rem = i - o * 9 * Cin;  // w layout [o][tap][cin]
+    sw[rem * 3 + o] = w[i];
+  }
+  __syncthreads();
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (long long)B * H * W) return;
+  const int b = (int)(pix / ((long long)H * W));
+  const int rem = (int)(pix - (long long)b * H * W);
+  const int yy = rem / W, xx = rem - (rem / W) * W;
+  float a0 = bias[0], a1 = bias[1], a2 = bias[2];
+  for (int tap = 0; tap < 9; ++tap) {
+    int Y = yy + tap / 3 - 1, X = xx + tap % 3 - 1;
+    Y = Y < 0 ? -Y : (Y >= H ? 2 * H - 2 - Y : Y);
+    X = X < 0 ? -X : (X >= W ? 2 * W - 2 - X : X);
+    const T* px = x + (((long long)b * H + Y) * W + X) * Cin;
+    const float* wt = sw + tap * Cin * 3;
+    constexpr int EV = 16 / sizeof(T);
+    for (int c = 0; c < Cin; c += EV) {
+      const typename Vec16<T>::type v = *reinterpret_cast<const typename Vec16<T>::type*>(px + c);
+#pragma unroll
+      for (int e = 0; e < EV; ++e) {
+        const float f = (float)v[e];
+        a0 += f * wt[(c + e) * 3 + 0];
+        a1 += f * wt[(c + e) * 3 + 1];
+        a2 += f * wt[(c + e) * 3 + 2];
+      }
+    }
+  }
+  a0 = fmaxf(a0, 0.f); a1 = fmaxf(a1, 0.f); a2 = fmaxf(a2, 0.f);
+  if (clamp255) { a0 = fminf(a0, 255.f); a1 = fminf(a1, 255.f); a2 = fminf(a2, 255.f); }
+  const long long plane = (long long)H * W;
+  float* yb = y + (long long)b * 3 * plane + (long long)yy * W + xx;
+  yb[0] = a0;
+  yb[plane] = a1;
+  yb[2 * plane] = a2;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace mhada
+
+using namespace mhada;
+
+extern "C" int mhada_layernorm(const float* x, void* y, int y_dtype, const float* gamma, const float* beta,
+                               int rows, int cols, float eps, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!x || !y || !gamma || !beta || rows < 0) return fail("mhada_layernorm: bad args");
+  if (rows == 0) return MHADA_OK;
+  if (!aligned16(x)) return fail("mhada_layernorm: x must be 16-byte aligned");
+  const dim3 grid((rows + 3) / 4), blk(256);
+#define LN_CASE(VPL)                                                                                   \
+  case VPL * 64:                                                                                       \
+    if (y_dtype == MHADA_F32)                                                                          \
+      hipLaunchKernelGGL((layernorm_kernel<float, VPL>), grid, blk, 0, s, x, (float*)y, gamma, beta, rows, eps); \
+    else                                                                                               \
+      hipLaunchKernelGGL((layernorm_kernel<bf16, VPL>), grid, blk, 0, s, x, (bf16*)y, gamma, beta, rows, eps); \
+    break;
+  switch (cols) {
+    LN_CASE(4)
+    LN_CASE(8)
+    LN_CASE(16)
+    LN_CASE(32)
+    default:
+      return fail("mhada_layernorm: cols must be 256, 512, 1024 or 2048");
+  }
+#undef LN_CASE
+  return check_launch("mhada_layernorm");
+}
+
+extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L, int ntok, int heads,
+                                    int head_dim, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!qkv || !out || L <= 0 || ntok < 0 || heads <= 0) return fail("mhada_vit_batch_attn: bad args");
+  if (head_dim != 64) return fail("mhada_vit_batch_attn: head_dim must be 64");
+  if (ntok == 0) return MHADA_OK;
+  const long long pairs = (long long)ntok * heads;
+  const size_t lds = 0;
+  const dim3 grid((unsigned)((pairs + 3) / 4));
+  if (dtype == MHADA_F32)
+    hipLaunchKernelGGL((vit_batch_attn_kernel<float>), grid, dim3(256), lds, s, (const float*)qkv, (float*)out, L,
+                       ntok, heads);
+  else
+    hipLaunchKernelGGL((vit_batch_attn_kernel<bf16>), grid, dim3(256), lds, s, (const bf16*)qkv, (bf16*)out, L,
+                       ntok, heads);
+  return check_launch("mhada_vit_batch_attn");
+}
+
+extern "C" int mhada_pos_embed(const float* pos, float* out, int C, int bh, int bw, int oh, int ow,
+                               mhada_stream_t s_) {
+  if (!pos || !out || C <= 0 || bh <= 0 || bw <= 0 || oh <= 0 || ow <= 0) return fail("mhada_pos_embed: bad args");
+  const long long n = (long long)oh * ow * C;
+  hipLaunchKernelGGL(pos_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s_, pos, out,
+                     C, bh, bw, oh, ow);
+  return check_launch("mhada_pos_embed");
+}
+
+extern "C" int mhada_instnorm_stats(const float* x, float* mu, float* rstd, double* work, int B, int N, int C,
+                                    int splits, float eps, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!x || !mu || !rstd || !work || B <= 0 || N <= 0 || C <= 0 || splits <= 0)
+    return fail("mhada_instnorm_stats: bad args");
+  if (splits > 65535) return fail("mhada_instnorm_stats: too many splits");
+  hipLaunchKernelGGL(in_partial_kernel, dim3((C + 63) / 64, B, splits), dim3(256), 0, s, x, work, B, N, C, splits);
+  int rc = check_launch("mhada_instnorm_stats/partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, work, mu, rstd, B, N, C,
+                     splits, eps);
+  return check_launch("mhada_instnorm_stats/finalize");
+}
+
+extern "C" int mhada_fold_block(const float* wf, const float* wg, const float* wh, const float* bg, const float* bh,
+                                const float* rstd_c, const float* mu_s, const float* rstd_s, void* wq, void* wkv,
+                                float* bkv, float* v_mu, int dtype, int B, int H, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!wf || !wg || !wh || !bg || !bh || !rstd_c || !mu_s || !rstd_s || !wq || !wkv || !bkv || !v_mu || B <= 0 ||
+      H <= 0)
+    return fail("mhada_fold_block: bad args");
+  if (dtype == MHADA_F32)
+    hipLaunchKernelGGL((fold_kernel<float>), dim3(B * H), dim3(256), 0, s, wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s,
+                       (float*)wq, (float*)wkv, bkv, v_mu, H);
+  else
+    hipLaunchKernelGGL((fold_kernel<bf16>), dim3(B * H), dim3(256), 0, s, wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s,
+                       (bf16*)wq, (bf16*)wkv, bkv, v_mu, H);
+  return check_launch("mhada_fold_block");
+}
+
+extern "C" int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t s_) {
+  if (!kv || !vt || B <= 0 || H <= 0 || Ns <= 0) return fail("mhada_transpose_v: bad args");
+  const int ldt = (Ns + 63) / 64 * 64;
+  hipLaunchKernelGGL(transpose_v_kernel, dim3(ldt / 64, B * H), dim3(256), 0, (hipStream_t)s_, (const bf16*)kv,
+                     (bf16*)vt, Ns, ldt);
+  return check_launch("mhada_transpose_v");
+}
+
+extern "C" int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns, mhada_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!q || !kv || B <= 0 || H <= 0 || Nc <= 0 || Ns <= 0) return fail("mhada_cosine_prep: bad args");
+  const long long rq = (long long)B * H * Nc, rk = (long long)B * H * Ns;
+  if (dtype == MHADA_F32) {
+    hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (float*)q, rq, 64);
+    hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (float*)kv, rk, 128);
+  } else {
+    hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (bf16*)q, rq, 64);
+    hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (bf16*)kv, rk, 128);
+  }
+  return check_launch("mhada_cosine_prep");
+}
+
+extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, const float* b, float* y, int B, int H,
+                                  int W, int Cin, int clamp255, mhada_stream_t s_) {
+  if (!x || !w || !b || !y || B <= 0 || H < 2 || W < 2 || Cin <= 0) return fail("mhada_conv3x3_out3: bad args");
+  const int ev = dtype == MHADA_F32 ? 4 : 8;
+  if (Cin % ev || !aligned16(x)) return fail("mhada_conv3x3_out3: Cin must fill 16-byte vectors");
+  const long long pix = (long long)B * H * W;
+  const size_t lds = (size_t)27 * Cin * sizeof(float);
+  const dim3 grid((unsigned)((pix + 255) / 256));
+  if (dtype == MHADA_F32)
+    hipLaunchKernelGGL((conv_out3_kernel<float>), grid, dim3(256), lds, (hipStream_t)s_, (const float*)x, w, b, y, B,
+                       H, W, Cin, clamp255);
+  else
+    hipLaunchKernelGGL((conv_out3_kernel<bf16>), grid, dim3(256), lds, (hipStream_t)s_, (const bf16*)x, w, b, y, B,
+                       H, W, Cin, clamp255);
+  return check_launch("mhada_conv3x3_out3");
+}

@@ -1,0 +1,90 @@
+"""ctypes binding of libmhada_hip.so (include/mhada_hip.h).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``).  There is no
+fallback: if the library is missing every op raises, so a GPU run can never silently take
+a CPU or aten path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmhada_hip.so")
+
+F32, BF16 = 0, 1
+ACT_SOFTMAX, ACT_COSINE = 0, 1
+A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2 = 0, 1, 2, 3
+
+_c_ll = ctypes.c_longlong
+_vp = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    """mirror of ``mhada_gemm_args``"""
+    _fields_ = [
+        ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+        ("nb1", ctypes.c_int), ("nb2", ctypes.c_int),
+        ("compute", ctypes.c_int), ("a_mode", ctypes.c_int),
+        ("a", _vp), ("a_dtype", ctypes.c_int), ("lda", _c_ll), ("sa1", _c_ll), ("sa2", _c_ll),
+        ("a_mu", _vp), ("smu1", _c_ll), ("smu2", _c_ll),
+        ("img_c", ctypes.c_int), ("img_h", ctypes.c_int), ("img_w", ctypes.c_int),
+        ("w", _vp), ("ldw", _c_ll), ("sw1", _c_ll), ("sw2", _c_ll),
+        ("bias", _vp), ("sb1", _c_ll), ("sb2", _c_ll),
+        ("r", _vp), ("r_dtype", ctypes.c_int), ("ldr", _c_ll), ("sr1", _c_ll), ("sr2", _c_ll),
+        ("c", _vp), ("c_dtype", ctypes.c_int), ("ldc", _c_ll), ("sc1", _c_ll), ("sc2", _c_ll),
+        ("relu", ctypes.c_int),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/mhada_hip.h
+_I, _F = ctypes.c_int, ctypes.c_float
+SIGNATURES = {
+    "mhada_abi_version": (_I, []),
+    "mhada_last_error": (ctypes.c_char_p, []),
+    "mhada_gemm": (_I, [ctypes.POINTER(GemmArgs), _vp]),
+    "mhada_layernorm": (_I, [_vp, _vp, _I, _vp, _vp, _I, _I, _F, _vp]),
+    "mhada_vit_batch_attn": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_pos_embed": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_instnorm_stats": (_I, [_vp, _vp, _vp, _vp, _I, _I, _I, _I, _F, _vp]),
+    "mhada_fold_block": (_I, [_vp] * 12 + [_I, _I, _I, _vp]),
+    "mhada_transpose_v": (_I, [_vp, _vp, _I, _I, _I, _vp]),
+    "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
+    "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and type the library; raises RuntimeError if it is not built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"MHAda HIP library not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C mhada-style-transfer_amd/csrc)")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().mhada_last_error()
+        msg = msg.decode() if msg else "unknown error"
+        if rc == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg}")

@@ -1,0 +1,289 @@
+"""Forward-path engine: the reference modules' forward passes expressed as sequences of
+HIP launches on token-major ("NHWC") device buffers.
+
+Layout in HBM (per forward call, B images, N = (H/8)(W/8) tokens, C = 512):
+  * ViT residual stream       fp32 [B][N][C]            (LayerNorm inputs / residual adds)
+  * GEMM operands             compute dtype (fp32 | bf16) [B*N][K]
+  * per-layer ViT outputs     fp32 [B][N][C]; handed to callers as NCHW *views*
+                              (x.view(B,h,w,C).permute(0,3,1,2)) — no transpose kernel
+  * MHAda per block           Q [B][H][Nc][64], KV [B][H][Ns][128] (K | V'), bf16 adds
+                              VT [B][H][128][ceil64(Ns)] (V'^T | V'^2^T); out [B][Nc][C]
+  * decoder                   NHWC activations in the compute dtype; the module output is
+                              NCHW fp32 (B,3,8h,8w), written directly by the last conv.
+Weights are repacked once per (dtype, parameter version) and cached on the module.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+from . import ops
+from ._lib import ACT_COSINE, ACT_SOFTMAX
+
+HEAD_DIM = 64
+DECODER_LAYERS: Tuple[Tuple[str, bool], ...] = (
+    # (name, upsample x2 applied to this layer's INPUT) — conv.py:78-94: bilinear x2 follows
+    # conv1.0, conv1.4 and conv2.1, so conv1.1, conv2.0 and conv3.0 read an upsampled input.
+    ("conv1.0", False), ("conv1.1", True), ("conv1.2", False), ("conv1.3", False),
+    ("conv1.4", False), ("conv2.0", True), ("conv2.1", False), ("conv3.0", True),
+)
+LAST_LAYER = "conv3.1"
+
+
+# ---------------------------------------------------------------------------------------
+# optional per-kernel event timing (bench.py): HIP events recorded on the launch stream
+# ---------------------------------------------------------------------------------------
+_event_log = None  # dict name -> list of (start, end) torch.cuda.Event, or None (off)
+
+
+def record_kernel_events(log) -> None:
+    """Enable (pass a dict) or disable (None) event brackets around the named launches."""
+    global _event_log
+    _event_log = log
+
+
+class _timed:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if _event_log is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _event_log is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _event_log.setdefault(self.name, []).append((self.s, e))
+        return False
+
+
+# ---------------------------------------------------------------------------------------
+# compute dtype & weight caches
+# ---------------------------------------------------------------------------------------
+def resolve_compute_dtype(module: torch.nn.Module) -> torch.dtype:
+    """fp32 by default (the reference's arithmetic); bf16 when the module's
+    ``compute_dtype`` says so or a CUDA autocast region asks for a 16-bit dtype (the HIP path
+    has bf16 MFMA kernels only, so float16 autocast also runs bf16)."""
+    explicit = getattr(module, "compute_dtype", None)
+    if explicit is not None:
+        if explicit not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute_dtype must be torch.float32 or torch.bfloat16, got {explicit}")
+        return explicit
+    if torch.is_autocast_enabled("cuda"):
+        if torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16):
+            return torch.bfloat16
+    return torch.float32
+
+
+def _signature(module: torch.nn.Module):
+    return tuple((p.data_ptr(), p._version) for p in module.parameters())
+
+
+def cached_prep(module: torch.nn.Module, dtype: torch.dtype, build):
+    cache: Dict = module.__dict__.setdefault("_mhada_prep", {})
+    key = (dtype, _signature(module))
+    hit = cache.get(dtype)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        prep = build(dtype)
+    cache[dtype] = (key, prep)
+    return prep
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: the MI355X-native network runs on ROCm device tensors only; "
+                           "move the module and inputs with .to('cuda')")
+
+
+def to_tokens(x: torch.Tensor) -> torch.Tensor:
+    """NCHW (any strides) -> contiguous fp32 [B][H][W][C] (zero-copy for this package's own
+    channels-last views)."""
+    t = x.permute(0, 2, 3, 1)
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def tokens_to_nchw(t: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    B, _, C = t.shape
+    return t.view(B, h, w, C).permute(0, 3, 1, 2)
+
+
+# ---------------------------------------------------------------------------------------
+# ViT (network/vit.py)
+# ---------------------------------------------------------------------------------------
+def vit_prep(vit, dtype):
+    def build(dt):
+        pe = vit.patch_embedding.conv_proj
+        layers = []
+        for blk in vit.encoder:
+            att = blk.attention
+            layers.append(dict(
+                ln1_g=blk.ln1.weight.float().contiguous(), ln1_b=blk.ln1.bias.float().contiguous(),
+                ln2_g=blk.ln2.weight.float().contiguous(), ln2_b=blk.ln2.bias.float().contiguous(),
+                w_qkv=att.in_proj_weight.to(dt).contiguous(), b_qkv=att.in_proj_bias.float().contiguous(),
+                w_o=att.out_proj.weight.to(dt).contiguous(), b_o=att.out_proj.bias.float().contiguous(),
+                w1=blk.mlp[0].weight.to(dt).contiguous(), b1=blk.mlp[0].bias.float().contiguous(),
+                w2=blk.mlp[2].weight.to(dt).contiguous(), b2=blk.mlp[2].bias.float().contiguous(),
+                heads=att.num_heads, eps=blk.ln1.eps))
+        return dict(patch_w=pe.weight.reshape(pe.weight.shape[0], -1).to(dt).contiguous(),
+                    patch_b=pe.bias.float().contiguous(), layers=layers, pos={})
+    return cached_prep(vit, dtype, build)
+
+
+def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
+    """VisionTransformer.forward (vit.py:148-169) on the HIP path."""
+    require_device(x, "VisionTransformer")
+    dt = resolve_compute_dtype(vit)
+    prep = vit_prep(vit, dt)
+    if x.dim() != 4 or x.shape[1] != 3:
+        raise ValueError(f"expected an image batch (B, 3, H, W), got {tuple(x.shape)}")
+    img = x.float().contiguous()
+    B, _, H, W = img.shape
+    p = vit.patch_size
+    h, w = H // p, W // p
+    N = h * w
+    C = prep["patch_w"].shape[0]
+    pos = None
+    if vit.pos_embedding is not None:
+        pos = prep["pos"].get((h, w))
+        if pos is None:
+            pos = ops.pos_embed(vit.pos_embedding.pos_embed.detach().float().contiguous(), h, w)
+            prep["pos"][(h, w)] = pos
+    tok = ops.patch_embed(img, prep["patch_w"], prep["patch_b"], pos, p)  # [B][N][C] fp32
+    xs = tok.view(B * N, C)
+    outs = []
+    for L in prep["layers"]:
+        hb = ops.layernorm(xs, L["ln1_g"], L["ln1_b"], dt, L["eps"])
+        qkv = ops.linear(hb, L["w_qkv"], L["b_qkv"], dt)
+        att = ops.vit_batch_attn(qkv.view(B, N, 3 * C), B, N, L["heads"])
+        xs = ops.linear(att.view(B * N, C), L["w_o"], L["b_o"], torch.float32, residual=xs)
+        h2 = ops.layernorm(xs, L["ln2_g"], L["ln2_b"], dt, L["eps"])
+        m1 = ops.linear(h2, L["w1"], L["b1"], dt, relu=True)
+        xs = ops.linear(m1, L["w2"], L["b2"], torch.float32, residual=xs)
+        outs.append(tokens_to_nchw(xs.view(B, N, C), h, w))
+    return outs
+
+
+# ---------------------------------------------------------------------------------------
+# MHAda blocks (network/adaDecoder.py)
+# ---------------------------------------------------------------------------------------
+def block_prep(blk, dtype):
+    def build(dt):
+        H = blk.num_heads
+        d = blk.head_dim
+
+        def stack(lst):
+            return torch.stack([m.weight.reshape(d, d) for m in lst]).float().contiguous()
+
+        def stackb(lst):
+            return torch.stack([m.bias for m in lst]).float().contiguous()
+        C = H * d
+        return dict(wf=stack(blk.f_list), wg=stack(blk.g_list), wh=stack(blk.h_list),
+                    bf=stackb(blk.f_list), bg=stackb(blk.g_list), bh=stackb(blk.h_list),
+                    w_out=blk.out_conv.weight.reshape(C, C).to(dt).contiguous(),
+                    b_out=blk.out_conv.bias.float().contiguous())
+    return cached_prep(blk, dtype, build)
+
+
+class _Feat:
+    """A token-major fp32 feature map with lazily computed InstanceNorm statistics."""
+
+    def __init__(self, t: torch.Tensor, h: int, w: int):
+        self.t, self.h, self.w = t, h, w  # t: [B][N][C]
+        self._stats = None
+
+    @classmethod
+    def from_nchw(cls, x: torch.Tensor):
+        _, _, h, w = x.shape
+        t = to_tokens(x)
+        return cls(t.view(t.shape[0], h * w, t.shape[3]), h, w)
+
+    def stats(self):
+        if self._stats is None:
+            self._stats = ops.instnorm_stats(self.t)
+        return self._stats
+
+
+def block_forward(blk, fc: _Feat, fs: _Feat, fcs: _Feat, dt: torch.dtype) -> _Feat:
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206)."""
+    if blk.head_dim != HEAD_DIM:
+        raise ValueError(f"the HIP MHAda kernels implement head_dim={HEAD_DIM} (qkv_dim/num_heads), "
+                         f"got {blk.head_dim}")
+    prep = block_prep(blk, dt)
+    H = blk.num_heads
+    C = H * HEAD_DIM
+    B, Nc, Cc = fc.t.shape
+    Ns = fs.t.shape[1]
+    if Cc != C or fs.t.shape[2] != C or fcs.t.shape[2] != C:
+        raise ValueError(f"channel mismatch: block expects {C}")
+    mu_c, rstd_c = fc.stats()
+    mu_s, rstd_s = fs.stats()
+    mu_o, rstd_o = fcs.stats()
+    wq, wkv, bkv, v_mu = ops.fold_block(prep["wf"], prep["wg"], prep["wh"], prep["bg"], prep["bh"],
+                                        rstd_c, mu_s, rstd_s, dt)
+    dev = fc.t.device
+    q = torch.empty(B, H, Nc, HEAD_DIM, device=dev, dtype=dt)
+    ops.gemm(a=fc.t, w=wq, c=q, M=Nc, N=HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Nc * C, HEAD_DIM),
+             nb=(B, H), a_mu=mu_c, smu=(C, HEAD_DIM), ldw=HEAD_DIM, sw=(H * HEAD_DIM * HEAD_DIM, HEAD_DIM * HEAD_DIM),
+             bias=prep["bf"], sb=(0, HEAD_DIM), ldc=HEAD_DIM, sc=(H * Nc * HEAD_DIM, Nc * HEAD_DIM))
+    kv = torch.empty(B, H, Ns, 2 * HEAD_DIM, device=dev, dtype=dt)
+    ops.gemm(a=fs.t, w=wkv, c=kv, M=Ns, N=2 * HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Ns * C, HEAD_DIM),
+             nb=(B, H), a_mu=mu_s, smu=(C, HEAD_DIM), ldw=HEAD_DIM,
+             sw=(H * 2 * HEAD_DIM * HEAD_DIM, 2 * HEAD_DIM * HEAD_DIM), bias=bkv, sb=(0, 2 * HEAD_DIM),
+             ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM))
+    act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
+    if act == ACT_COSINE:
+        ops.cosine_prep(q, kv)
+    vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+    with _timed("mhada_attn"):
+        att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
+    out = ops.linear(att.view(B * Nc, C), prep["w_out"], prep["b_out"], torch.float32)
+    return _Feat(out.view(B, Nc, C), fc.h, fc.w)
+
+
+# ---------------------------------------------------------------------------------------
+# Decoder (network/conv.py)
+# ---------------------------------------------------------------------------------------
+def decoder_prep(dec, dtype):
+    def build(dt):
+        mods = dict(dec.named_modules())
+        layers = []
+        for name, up in DECODER_LAYERS:
+            conv = mods[name].conv.conv
+            w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1).to(dt).contiguous()
+            layers.append((w, conv.bias.float().contiguous(), up))
+        last = mods[LAST_LAYER].conv.conv
+        return dict(layers=layers, w_last=last.weight.permute(0, 2, 3, 1).float().contiguous(),
+                    b_last=last.bias.float().contiguous())
+    return cached_prep(dec, dtype, build)
+
+
+def decoder_forward_tokens(dec, x_nhwc: torch.Tensor, dt: torch.dtype, clamp255: bool = False) -> torch.Tensor:
+    """Decoder.forward (conv.py:96-100) on NHWC input; returns NCHW fp32 (B,3,8h,8w)."""
+    prep = decoder_prep(dec, dt)
+    x = x_nhwc
+    for w, b, up in prep["layers"]:
+        x = ops.conv3x3(x, w, b, dt, upsample=up, relu=True)
+    return ops.conv3x3_out3(x, prep["w_last"], prep["b_last"], clamp255=clamp255)
+
+
+def adaformer_forward(ada, fc: Sequence[torch.Tensor], fs: Sequence[torch.Tensor]):
+    """AdaAttnTransformerMultiHead.forward (adaDecoder.py:253-268): returns (fcs, cs)."""
+    require_device(fc[0], "AdaAttnTransformerMultiHead")
+    dt = resolve_compute_dtype(ada)
+    fcf = [_Feat.from_nchw(t) for t in fc[: ada.num_layers]]
+    fsf = [_Feat.from_nchw(t) for t in fs[: ada.num_layers]]
+    fcs = fcf[0]
+    for i in range(ada.num_layers):
+        fcs = block_forward(ada.adaAttnHead[2 * i], fcf[i], fsf[i], fcs, dt)
+        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fsf[i], fcs, dt)
+    B, N, C = fcs.t.shape
+    cs = decoder_forward_tokens(ada.decoder, fcs.t.view(B, fcs.h, fcs.w, C), dt)
+    return tokens_to_nchw(fcs.t, fcs.h, fcs.w), cs

@@ -1,0 +1,211 @@
+"""Tensor-level wrappers over the C-ABI (one function per entry point of include/mhada_hip.h).
+
+Every wrapper takes ROCm device tensors, validates shapes/dtypes on the host, launches on
+``torch.cuda.current_stream()`` and allocates outputs through the torch caching allocator
+(the library itself never allocates).  No wrapper has a CPU or aten fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import A_CONV3X3, A_CONV3X3_UP2, A_PATCH8, A_ROWS, BF16, F32, GemmArgs
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt_code(dtype: torch.dtype) -> int:
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise ValueError(f"unsupported dtype {dtype}; the HIP path computes in float32 or bfloat16")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need_gpu(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("mhada_hip ops need ROCm device tensors (the MI355X path has no CPU fallback)")
+
+
+def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K: int,
+         compute: torch.dtype, a_mode: int = A_ROWS, lda: int = 0, sa=(0, 0), nb=(1, 1),
+         a_mu: Optional[torch.Tensor] = None, smu=(0, 0), img=(0, 0, 0),
+         ldw: int = 0, sw=(0, 0), bias: Optional[torch.Tensor] = None, sb=(0, 0),
+         r: Optional[torch.Tensor] = None, ldr: int = 0, sr=(0, 0),
+         ldc: int = 0, sc=(0, 0), relu: bool = False) -> torch.Tensor:
+    """``mhada_gemm``: C[z] = act(A[z] W[z]^T + bias[z]) + R[z]; strides in elements."""
+    _need_gpu(a, w, c, a_mu, bias, r)
+    if w.dtype != compute:
+        raise ValueError("W must already be in the compute dtype")
+    for t in (a_mu, bias):
+        if t is not None and t.dtype != torch.float32:
+            raise ValueError("a_mu / bias must be float32")
+    if r is not None and r.dtype != c.dtype:
+        raise ValueError("residual dtype must equal the output dtype")
+    args = GemmArgs()
+    args.M, args.N, args.K = M, N, K
+    args.nb1, args.nb2 = nb
+    args.compute = dt_code(compute)
+    args.a_mode = a_mode
+    args.a, args.a_dtype, args.lda = a.data_ptr(), dt_code(a.dtype), lda
+    args.sa1, args.sa2 = sa
+    args.a_mu = _ptr(a_mu)
+    args.smu1, args.smu2 = smu
+    args.img_c, args.img_h, args.img_w = img
+    args.w, args.ldw = w.data_ptr(), ldw
+    args.sw1, args.sw2 = sw
+    args.bias = _ptr(bias)
+    args.sb1, args.sb2 = sb
+    args.r = _ptr(r)
+    args.r_dtype = dt_code(r.dtype) if r is not None else 0
+    args.ldr = ldr
+    args.sr1, args.sr2 = sr
+    args.c, args.c_dtype, args.ldc = c.data_ptr(), dt_code(c.dtype), ldc
+    args.sc1, args.sc2 = sc
+    args.relu = int(relu)
+    _lib.check(_lib.load().mhada_gemm(ctypes.byref(args), _stream()), "mhada_gemm")
+    return c
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
+           residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+    """x [M][K] @ w[N][K]^T + bias (+relu) (+residual) -> [M][N] of out_dtype."""
+    M, K = x.shape
+    N = w.shape[0]
+    c = torch.empty(M, N, device=x.device, dtype=out_dtype)
+    return gemm(a=x, w=w, c=c, M=M, N=N, K=K, compute=w.dtype, lda=x.stride(0), ldw=w.stride(0),
+                bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)
+
+
+def patch_embed(img: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, pos: Optional[torch.Tensor],
+                patch: int = 8) -> torch.Tensor:
+    """img (B,3,H,W) fp32 -> tokens [B][N][C] fp32 (+ pos [N][C] broadcast over B)."""
+    if patch != 8:
+        raise ValueError("the HIP patch embedding implements patch_size=8 (the reference default)")
+    B, Ci, H, W = img.shape
+    h, wd = H // 8, W // 8
+    N, C = h * wd, w.shape[0]
+    out = torch.empty(B, N, C, device=img.device, dtype=torch.float32)
+    return gemm(a=img, w=w, c=out, M=N, N=C, K=Ci * 64, compute=w.dtype, a_mode=A_PATCH8,
+                sa=(Ci * H * W, 0), nb=(B, 1), img=(Ci, H, W), ldw=w.stride(0), bias=bias,
+                r=pos, ldr=C, sr=(0, 0), ldc=C, sc=(N * C, 0))
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out_dtype: torch.dtype,
+            upsample: bool, relu: bool = True) -> torch.Tensor:
+    """NHWC x [B][H][W][Cin] -> NHWC [B][H'][W'][Cout]; ReflectionPad2d(1)+conv3x3(+ReLU),
+    optionally on bilinear-x2(x).  w packed [Cout][9*Cin] in the compute dtype."""
+    B, H, W, Ci = x.shape
+    Co = w.shape[0]
+    Ho, Wo = (2 * H, 2 * W) if upsample else (H, W)
+    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=out_dtype)
+    return gemm(a=x, w=w, c=y, M=B * Ho * Wo, N=Co, K=9 * Ci, compute=w.dtype,
+                a_mode=A_CONV3X3_UP2 if upsample else A_CONV3X3, img=(Ci, H, W), ldw=w.stride(0),
+                bias=bias, ldc=Co, relu=relu)
+
+
+def conv3x3_out3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, clamp255: bool = False) -> torch.Tensor:
+    B, H, W, Ci = x.shape
+    _need_gpu(x, w, bias)
+    y = torch.empty(B, 3, H, W, device=x.device, dtype=torch.float32)
+    rc = _lib.load().mhada_conv3x3_out3(x.data_ptr(), dt_code(x.dtype), w.data_ptr(), bias.data_ptr(),
+                                        y.data_ptr(), B, H, W, Ci, int(clamp255), _stream())
+    _lib.check(rc, "mhada_conv3x3_out3")
+    return y
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, out_dtype: torch.dtype, eps: float) -> torch.Tensor:
+    _need_gpu(x, g, b)
+    rows, cols = x.shape
+    y = torch.empty(rows, cols, device=x.device, dtype=out_dtype)
+    rc = _lib.load().mhada_layernorm(x.data_ptr(), y.data_ptr(), dt_code(out_dtype), g.data_ptr(), b.data_ptr(),
+                                     rows, cols, eps, _stream())
+    _lib.check(rc, "mhada_layernorm")
+    return y
+
+
+def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int) -> torch.Tensor:
+    _need_gpu(qkv)
+    C = qkv.shape[-1] // 3
+    out = torch.empty(L, ntok, C, device=qkv.device, dtype=qkv.dtype)
+    rc = _lib.load().mhada_vit_batch_attn(qkv.data_ptr(), out.data_ptr(), dt_code(qkv.dtype), L, ntok, heads,
+                                          C // heads, _stream())
+    _lib.check(rc, "mhada_vit_batch_attn")
+    return out
+
+
+def pos_embed(pos: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
+    _need_gpu(pos)
+    _, C, bh, bw = pos.shape
+    out = torch.empty(oh * ow, C, device=pos.device, dtype=torch.float32)
+    rc = _lib.load().mhada_pos_embed(pos.data_ptr(), out.data_ptr(), C, bh, bw, oh, ow, _stream())
+    _lib.check(rc, "mhada_pos_embed")
+    return out
+
+
+def instnorm_stats(x: torch.Tensor, eps: float = 1e-5):
+    """x [B][N][C] fp32 -> (mu, rstd) [B][C] fp32."""
+    _need_gpu(x)
+    B, N, C = x.shape
+    splits = max(1, min(N // 32, 2048 // max(1, B * ((C + 63) // 64))))
+    mu = torch.empty(B, C, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(B, C, device=x.device, dtype=torch.float32)
+    work = torch.empty(splits, B, C, 2, device=x.device, dtype=torch.float64)
+    rc = _lib.load().mhada_instnorm_stats(x.data_ptr(), mu.data_ptr(), rstd.data_ptr(), work.data_ptr(), B, N, C,
+                                          splits, eps, _stream())
+    _lib.check(rc, "mhada_instnorm_stats")
+    return mu, rstd
+
+
+def fold_block(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s, dtype: torch.dtype):
+    B, C = rstd_c.shape
+    H = wf.shape[0]
+    dev = wf.device
+    wq = torch.empty(B, H, 64, 64, device=dev, dtype=dtype)
+    wkv = torch.empty(B, H, 128, 64, device=dev, dtype=dtype)
+    bkv = torch.empty(H, 128, device=dev, dtype=torch.float32)
+    v_mu = torch.empty(B, C, device=dev, dtype=torch.float32)
+    rc = _lib.load().mhada_fold_block(wf.data_ptr(), wg.data_ptr(), wh.data_ptr(), bg.data_ptr(), bh.data_ptr(),
+                                      rstd_c.data_ptr(), mu_s.data_ptr(), rstd_s.data_ptr(), wq.data_ptr(),
+                                      wkv.data_ptr(), bkv.data_ptr(), v_mu.data_ptr(), dt_code(dtype), B, H,
+                                      _stream())
+    _lib.check(rc, "mhada_fold_block")
+    return wq, wkv, bkv, v_mu
+
+
+def transpose_v(kv: torch.Tensor) -> torch.Tensor:
+    B, H, Ns, _ = kv.shape
+    ldt = (Ns + 63) // 64 * 64
+    vt = torch.empty(B, H, 128, ldt, device=kv.device, dtype=kv.dtype)
+    rc = _lib.load().mhada_transpose_v(kv.data_ptr(), vt.data_ptr(), B, H, Ns, _stream())
+    _lib.check(rc, "mhada_transpose_v")
+    return vt
+
+
+def cosine_prep(q: torch.Tensor, kv: torch.Tensor) -> None:
+    B, H, Nc, _ = q.shape
+    Ns = kv.shape[2]
+    rc = _lib.load().mhada_cosine_prep(q.data_ptr(), kv.data_ptr(), dt_code(q.dtype), B, H, Nc, Ns, _stream())
+    _lib.check(rc, "mhada_cosine_prep")
+
+
+def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch.Tensor:
+    B, H, Nc, _ = q.shape
+    Ns = kv.shape[2]
+    out = torch.empty(B, Nc, H * 64, device=q.device, dtype=q.dtype)
+    rc = _lib.load().mhada_attn(q.data_ptr(), kv.data_ptr(), _ptr(vt), fcs.data_ptr(), fcs_mu.data_ptr(),
+                                fcs_rstd.data_ptr(), v_mu.data_ptr(), out.data_ptr(), dt_code(q.dtype), B, H, Nc,
+                                Ns, activation, _stream())
+    _lib.check(rc, "mhada_attn")
+    return out

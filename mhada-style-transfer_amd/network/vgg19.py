@@ -1,0 +1,38 @@
+"""Frozen VGG19 loss network — constructor/state_dict parity with ``MHAdaSTr/network/vgg19.py:15-70``.
+
+The reference pulls ImageNet weights from torchvision at construction (a network fetch this
+environment cannot make); here the layers are built with the same indices so a locally
+saved ``slice{1..5}.{idx}.{weight,bias}`` state_dict loads strictly.  Its forward belongs to
+the training path, which is not on the HIP path in this round.
+"""
+import torch.nn as nn
+
+# torchvision vgg19 cfg "E" features[0:30]: (index, in, out) of each 3x3 conv; ReLU follows
+# each conv, MaxPool2d(2) at 4, 9, 18, 27.
+_CONVS = [(0, 3, 64), (2, 64, 64), (5, 64, 128), (7, 128, 128), (10, 128, 256), (12, 256, 256),
+          (14, 256, 256), (16, 256, 256), (19, 256, 512), (21, 512, 512), (23, 512, 512), (25, 512, 512),
+          (28, 512, 512)]
+_POOLS = (4, 9, 18, 27)
+_SLICES = ((0, 2), (2, 7), (7, 12), (12, 21), (21, 30))
+
+
+class VGG19(nn.Module):
+    def __init__(self):
+        super().__init__()
+        convs = {i: (ci, co) for i, ci, co in _CONVS}
+        for s, (a, b) in enumerate(_SLICES, start=1):
+            seq = nn.Sequential()
+            for x in range(a, b):
+                if x in convs:
+                    seq.add_module(str(x), nn.Conv2d(convs[x][0], convs[x][1], 3, padding=1))
+                elif x in _POOLS:
+                    seq.add_module(str(x), nn.MaxPool2d(2, 2))
+                else:
+                    seq.add_module(str(x), nn.ReLU(inplace=True))
+            setattr(self, f"slice{s}", seq)
+        for p in self.parameters():
+            p.requires_grad = False
+
+    def forward(self, x):
+        raise NotImplementedError("VGG19 loss features (training path) are not on the HIP path yet; "
+                                  "see DESIGN.md §scope")

@@ -1,0 +1,279 @@
+"""CPU oracle for the MHAdaSTr style-transfer forward path — numpy restatement.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the *checker* (or the timed CPU
+baseline), never as the thing measured or shipped.  The product path
+(``mhada-style-transfer_amd/network``) runs the HIP kernels and fails loudly without them.
+
+Parity pinning: this restatement is checked against golden vectors produced by running the
+reference modules themselves (``/root/reference/MHAdaSTr/network/{conv,vit,adaDecoder}.py``,
+loaded by path in this container) on seeded inputs with recipe weights —
+``tests/golden/make_goldens.py`` writes them, ``tests/test_oracle_golden.py`` checks them.
+
+Every function cites the reference ``file:line`` (relative to ``MHAdaSTr/``) that it follows.
+Weights are passed as ``{state_dict_key: np.ndarray}``.  Tensors follow the reference's NCHW
+convention at the module boundary.  ``dtype`` selects the arithmetic type (float32 follows
+the reference; float64 gives a high-precision check).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+Params = Dict[str, np.ndarray]
+
+
+# --------------------------------------------------------------------------------------
+# small primitives
+# --------------------------------------------------------------------------------------
+def _src_index(out_size: int, in_size: int, scale: float):
+    """PyTorch ``upsample_bilinear2d`` (align_corners=False) source taps for one axis:
+    src = scale*(dst+0.5)-0.5 clamped at 0; i1 = i0+1 unless at the border."""
+    dst = np.arange(out_size, dtype=np.float64)
+    src = scale * (dst + 0.5) - 0.5
+    src = np.maximum(src, 0.0)
+    i0 = np.floor(src).astype(np.int64)
+    i0 = np.minimum(i0, in_size - 1)
+    i1 = np.where(i0 < in_size - 1, i0 + 1, i0)
+    l1 = src - i0
+    l0 = 1.0 - l1
+    return i0, i1, l0, l1
+
+
+def interp_bilinear(x: np.ndarray, out_h: int, out_w: int, scale_h: float | None = None,
+                    scale_w: float | None = None) -> np.ndarray:
+    """``F.interpolate(mode="bilinear", align_corners=False)`` on NCHW.
+
+    Used with ``size=`` by ``PosEmbedding`` (``network/vit.py:91-92``) and with
+    ``scale_factor=2`` by ``ConvReluInterpolate`` (``network/conv.py:71``); for an exact ×2
+    both give scale = in/out = 1/2."""
+    n, c, h, w = x.shape
+    sh = h / out_h if scale_h is None else scale_h
+    sw = w / out_w if scale_w is None else scale_w
+    y0, y1, ly0, ly1 = _src_index(out_h, h, sh)
+    x0, x1, lx0, lx1 = _src_index(out_w, w, sw)
+    dt = x.dtype
+    ly0 = ly0.astype(dt)[:, None]
+    ly1 = ly1.astype(dt)[:, None]
+    lx0 = lx0.astype(dt)[None, :]
+    lx1 = lx1.astype(dt)[None, :]
+    top = x[:, :, y0, :]
+    bot = x[:, :, y1, :]
+    out = ly0 * (lx0 * top[..., x0] + lx1 * top[..., x1]) + ly1 * (lx0 * bot[..., x0] + lx1 * bot[..., x1])
+    return out.astype(dt)
+
+
+def layer_norm(x: np.ndarray, g: np.ndarray, b: np.ndarray, eps: float = 1e-6) -> np.ndarray:
+    """``nn.LayerNorm(hidden_dim, eps=1e-6)`` (``network/vit.py:54-55``), biased variance."""
+    mu = x.mean(axis=-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=-1, keepdims=True)
+    return ((x - mu) / np.sqrt(var + eps)) * g + b
+
+
+def instance_norm(x: np.ndarray, eps: float = 1e-5) -> np.ndarray:
+    """``nn.InstanceNorm2d(affine=False)`` (``network/adaDecoder.py:147-149``): per (b,c)
+    mean and biased variance over H·W, no running stats."""
+    mu = x.mean(axis=(2, 3), keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=(2, 3), keepdims=True)
+    return (x - mu) / np.sqrt(var + eps)
+
+
+def softmax_last(s: np.ndarray) -> np.ndarray:
+    m = s.max(axis=-1, keepdims=True)
+    e = np.exp(s - m)
+    return e / e.sum(axis=-1, keepdims=True)
+
+
+def conv2d(x: np.ndarray, w: np.ndarray, b: np.ndarray, pad_mode: str | None = None) -> np.ndarray:
+    """Stride-1 3×3 (or k×k) conv on NCHW via im2col.  ``pad_mode="reflect"`` is
+    ``ReflectionPad2d(k//2)`` (``network/conv.py:27-28``), ``"zeros"`` is VGG's padding=1."""
+    co, ci, kh, kw = w.shape
+    ph, pw = kh // 2, kw // 2
+    if pad_mode == "reflect":
+        xp = np.pad(x, ((0, 0), (0, 0), (ph, ph), (pw, pw)), mode="reflect")
+    elif pad_mode == "zeros":
+        xp = np.pad(x, ((0, 0), (0, 0), (ph, ph), (pw, pw)))
+    else:
+        xp = x
+    n, _, hp, wp = xp.shape
+    ho, wo = hp - kh + 1, wp - kw + 1
+    cols = np.empty((n, ho, wo, ci, kh, kw), dtype=x.dtype)
+    for dy in range(kh):
+        for dx in range(kw):
+            cols[:, :, :, :, dy, dx] = xp[:, :, dy:dy + ho, dx:dx + wo].transpose(0, 2, 3, 1)
+    y = cols.reshape(n * ho * wo, ci * kh * kw) @ w.reshape(co, -1).T.astype(x.dtype) + b.astype(x.dtype)
+    return y.reshape(n, ho, wo, co).transpose(0, 3, 1, 2)
+
+
+# --------------------------------------------------------------------------------------
+# ViT encoder (network/vit.py)
+# --------------------------------------------------------------------------------------
+def patch_embed(x: np.ndarray, w: np.ndarray, b: np.ndarray, patch: int = 8) -> np.ndarray:
+    """``PatchEmbedding`` (``network/vit.py:105-117``): conv k=s=8, then (B, N, C)."""
+    n, ci, hh, ww = x.shape
+    h, wd = hh // patch, ww // patch
+    xc = x[:, :, : h * patch, : wd * patch]
+    cols = xc.reshape(n, ci, h, patch, wd, patch).transpose(0, 2, 4, 1, 3, 5).reshape(n * h * wd, -1)
+    y = cols @ w.reshape(w.shape[0], -1).T.astype(x.dtype) + b.astype(x.dtype)
+    return y.reshape(n, h * wd, w.shape[0])
+
+
+def pos_embedding(pos: np.ndarray, h: int, w: int) -> np.ndarray:
+    """``PosEmbedding.forward`` (``network/vit.py:81-102``): bilinear from 32×32 when the
+    token grid differs, returned as (1, N, C)."""
+    if h != pos.shape[2] or w != pos.shape[3]:
+        pos = interp_bilinear(pos, h, w)
+    c = pos.shape[1]
+    return pos.reshape(1, c, h * w).transpose(0, 2, 1)
+
+
+def mha_batch_axis(x: np.ndarray, p: Params, pre: str, heads: int) -> np.ndarray:
+    """``nn.MultiheadAttention`` as called at ``network/vit.py:59`` with the default
+    ``batch_first=False`` on a (B, N, C) tensor: the sequence axis is B and the N tokens
+    are the batch — every token attends over the B images at the same position."""
+    bsz, n, c = x.shape
+    d = c // heads
+    dt = x.dtype
+    qkv = x @ p[pre + "in_proj_weight"].T.astype(dt) + p[pre + "in_proj_bias"].astype(dt)
+    q, k, v = qkv[..., :c], qkv[..., c:2 * c], qkv[..., 2 * c:]
+    # (L=B, N, H, d) -> (N, H, L, d)
+    q = q.reshape(bsz, n, heads, d).transpose(1, 2, 0, 3)
+    k = k.reshape(bsz, n, heads, d).transpose(1, 2, 0, 3)
+    v = v.reshape(bsz, n, heads, d).transpose(1, 2, 0, 3)
+    s = (q @ k.transpose(0, 1, 3, 2)) * dt.type(1.0 / np.sqrt(d))
+    o = softmax_last(s) @ v  # (N, H, L, d)
+    o = o.transpose(2, 0, 1, 3).reshape(bsz, n, c)
+    return o @ p[pre + "out_proj.weight"].T.astype(dt) + p[pre + "out_proj.bias"].astype(dt)
+
+
+def encoder_block(x: np.ndarray, p: Params, pre: str, heads: int) -> np.ndarray:
+    """``EncoderBlock.forward`` (``network/vit.py:57-64``): pre-LN attention + MLP."""
+    dt = x.dtype
+    h = layer_norm(x, p[pre + "ln1.weight"], p[pre + "ln1.bias"])
+    x = mha_batch_axis(h, p, pre + "attention.", heads) + x
+    y = layer_norm(x, p[pre + "ln2.weight"], p[pre + "ln2.bias"])
+    y = np.maximum(y @ p[pre + "mlp.0.weight"].T.astype(dt) + p[pre + "mlp.0.bias"].astype(dt), 0)
+    y = y @ p[pre + "mlp.2.weight"].T.astype(dt) + p[pre + "mlp.2.bias"].astype(dt)
+    return x + y
+
+
+def vit_forward(img: np.ndarray, p: Params, num_layers: int = 3, heads: int = 8,
+                patch: int = 8) -> List[np.ndarray]:
+    """``VisionTransformer.forward`` (``network/vit.py:148-169``).  Returns the per-layer
+    outputs reshaped to (B, C, H/8, W/8)."""
+    dt = img.dtype
+    bsz, _, hh, ww = img.shape
+    h, w = hh // patch, ww // patch
+    x = patch_embed(img, p["patch_embedding.conv_proj.weight"], p["patch_embedding.conv_proj.bias"], patch)
+    if "pos_embedding.pos_embed" in p:
+        x = x + pos_embedding(p["pos_embedding.pos_embed"].astype(dt), h, w)
+    outs = []
+    for i in range(num_layers):
+        x = encoder_block(x, p, f"encoder.{i}.", heads)
+        outs.append(x.transpose(0, 2, 1).reshape(bsz, -1, h, w).copy())
+    return outs
+
+
+# --------------------------------------------------------------------------------------
+# MHAda blocks (network/adaDecoder.py)
+# --------------------------------------------------------------------------------------
+def activation_softmax(q: np.ndarray, k: np.ndarray) -> np.ndarray:
+    """``Softmax.forward`` (``network/adaDecoder.py:16-17``): softmax(bmm(q,k)), no 1/√d."""
+    return softmax_last(q @ k)
+
+
+def activation_cosine(q: np.ndarray, k: np.ndarray) -> np.ndarray:
+    """``CosineSimilarity.forward`` (``network/adaDecoder.py:24-34``)."""
+    qn = np.sqrt((q * q).sum(axis=-1, keepdims=True))
+    kn = np.sqrt((k * k).sum(axis=1, keepdims=True))
+    s = (q @ k) / (qn @ kn) + 1
+    return s / s.sum(axis=-1, keepdims=True)
+
+
+def conv1x1(x: np.ndarray, w: np.ndarray, b: np.ndarray) -> np.ndarray:
+    co = w.shape[0]
+    bsz, ci, h, wd = x.shape
+    dt = x.dtype
+    y = w.reshape(co, ci).astype(dt) @ x.reshape(bsz, ci, h * wd) + b.astype(dt)[:, None]
+    return y.reshape(bsz, co, h, wd)
+
+
+def ada_attn_multihead(fc: np.ndarray, fs: np.ndarray, fcs: np.ndarray, p: Params, pre: str,
+                       heads: int = 8, activation: str = "softmax", trace: dict | None = None) -> np.ndarray:
+    """``AdaAttnMultiHead.forward`` (``network/adaDecoder.py:162-206``): per head
+    Q=f(IN(fc)), K=g(IN(fs)), V=h(fs); A=act(Q,K); M=AV; S=√max(AV²−M²,1e-6);
+    out=S·IN(fcs)+M; concat; out_conv."""
+    act = {"softmax": activation_softmax, "cosine": activation_cosine}[activation]
+    bsz, c, h, w = fc.shape
+    _, _, hs, ws = fs.shape
+    d = c // heads
+    outs = []
+    for i in range(heads):
+        sl = slice(i * d, (i + 1) * d)
+        q = conv1x1(instance_norm(fc[:, sl]), p[f"{pre}f_list.{i}.weight"], p[f"{pre}f_list.{i}.bias"])
+        q = q.reshape(bsz, d, h * w).transpose(0, 2, 1)
+        k = conv1x1(instance_norm(fs[:, sl]), p[f"{pre}g_list.{i}.weight"], p[f"{pre}g_list.{i}.bias"])
+        k = k.reshape(bsz, d, hs * ws)
+        v = conv1x1(fs[:, sl], p[f"{pre}h_list.{i}.weight"], p[f"{pre}h_list.{i}.bias"])
+        v = v.reshape(bsz, d, hs * ws).transpose(0, 2, 1)
+        a = act(q, k)
+        m = a @ v
+        var = a @ (v ** 2) - m ** 2
+        s = np.sqrt(np.maximum(var, 1e-6))
+        m4 = m.reshape(bsz, h, w, d).transpose(0, 3, 1, 2)
+        s4 = s.reshape(bsz, h, w, d).transpose(0, 3, 1, 2)
+        if trace is not None:
+            trace.setdefault("Q", []).append(q)
+            trace.setdefault("K", []).append(k)
+            trace.setdefault("V", []).append(v)
+            trace.setdefault("M", []).append(m)
+            trace.setdefault("S", []).append(s)
+        outs.append(s4 * instance_norm(fcs[:, sl]) + m4)
+    cat = np.concatenate(outs, axis=1)
+    return conv1x1(cat, p[f"{pre}out_conv.weight"], p[f"{pre}out_conv.bias"])
+
+
+def decoder_forward(x: np.ndarray, p: Params, pre: str = "decoder.") -> np.ndarray:
+    """``Decoder.forward`` (``network/conv.py:75-100``): 9 × [ReflectionPad(1) → conv3×3 →
+    ReLU], bilinear ×2 after conv1.0, conv1.4 and conv2.1.  The last layer is ReLU."""
+    layers = [("conv1.0", True), ("conv1.1", False), ("conv1.2", False), ("conv1.3", False),
+              ("conv1.4", True), ("conv2.0", False), ("conv2.1", True), ("conv3.0", False),
+              ("conv3.1", False)]
+    for name, up in layers:
+        w = p[f"{pre}{name}.conv.conv.weight"]
+        b = p[f"{pre}{name}.conv.conv.bias"]
+        x = np.maximum(conv2d(x, w, b, "reflect"), 0)
+        if up:
+            x = interp_bilinear(x, x.shape[2] * 2, x.shape[3] * 2, 0.5, 0.5)
+    return x
+
+
+def adaformer_forward(fc: Sequence[np.ndarray], fs: Sequence[np.ndarray], p: Params,
+                      num_layers: int = 3, heads: int = 8, activation: str = "softmax"):
+    """``AdaAttnTransformerMultiHead.forward`` (``network/adaDecoder.py:253-268``).
+    Returns (fcs, cs)."""
+    fcs = fc[0]
+    for i in range(num_layers):
+        fcs = ada_attn_multihead(fc[i], fs[i], fcs, p, f"adaAttnHead.{2 * i}.", heads, activation)
+        fcs = ada_attn_multihead(fcs, fs[i], fcs, p, f"adaAttnHead.{2 * i + 1}.", heads, activation)
+    return fcs, decoder_forward(fcs, p)
+
+
+def stylize(content: np.ndarray, style: np.ndarray, p_vc: Params, p_vs: Params, p_ada: Params,
+            activation: str = "softmax"):
+    """The inference call sequence of ``infer_image.py:83-86``: fc=vit_c(c), fs=vit_s(s),
+    (fcs, cs)=adaFormer(fc, fs).  Returns (fc, fs, fcs, cs) with cs *unclamped*."""
+    fc = vit_forward(content, p_vc)
+    fs = vit_forward(style, p_vs)
+    fcs, cs = adaformer_forward(fc, fs, p_ada, activation=activation)
+    return fc, fs, fcs, cs
+
+
+def to_numpy_params(sd, dtype=np.float32) -> Params:
+    """state_dict (torch tensors or arrays) -> {key: ndarray of ``dtype``}."""
+    out = {}
+    for k, v in sd.items():
+        arr = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
+        out[k] = arr.astype(dtype)
+    return out

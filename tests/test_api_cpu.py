@@ -1,0 +1,105 @@
+"""Host-side checks of the drop-in network/ API and the C-ABI library (no GPU needed)."""
+import json
+import os
+import re
+
+import pytest
+import torch
+
+import network
+from mhada_hip import _lib
+from mhada_hip.recipe import load_recipe
+from conftest import GOLDEN, REPO
+
+
+def _keys():
+    with open(os.path.join(GOLDEN, "state_dict_keys.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name,ctor", [
+    ("vit_c", lambda: network.VisionTransformer(pos_embedding=True)),
+    ("vit_s", lambda: network.VisionTransformer(pos_embedding=False)),
+    ("ada", lambda: network.AdaAttnTransformerMultiHead()),
+    ("block_512_8", lambda: network.AdaAttnMultiHead(512, 8)),
+    ("decoder", lambda: network.Decoder()),
+])
+def test_state_dict_keys_match_reference(name, ctor):
+    ref = _keys()[name]
+    mine = {k: list(v.shape) for k, v in ctor().state_dict().items()}
+    assert mine == ref
+
+
+def test_reference_checkpoint_roundtrip(tmp_path):
+    """A reference-format checkpoint (torch.save(state_dict)) loads strictly, weights_only."""
+    vit = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c")
+    path = tmp_path / "ViT_C.pth"
+    torch.save(vit.state_dict(), path)
+    vit2 = network.VisionTransformer(pos_embedding=True)
+    vit2.load_state_dict(torch.load(path, weights_only=True), strict=True)
+    for k, v in vit.state_dict().items():
+        assert torch.equal(v, vit2.state_dict()[k])
+
+
+def test_constructor_errors_mirror_reference():
+    with pytest.raises(ValueError):
+        network.AdaAttnMultiHead(512, 7)           # adaDecoder.py:137-138
+    with pytest.raises(ValueError):
+        network.AdaAttnTransformerMultiHead(activation="relu")  # adaDecoder.py:160
+    with pytest.raises(ValueError):
+        network.AdaAttnForLoss(256, 448, activation="tanh")      # adaDecoder.py:50
+    network.AdaAttnTransformerMultiHead(activation="cosine")
+
+
+def test_forward_refuses_cpu_tensors():
+    vit = network.VisionTransformer()
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        vit(torch.rand(1, 3, 64, 64) * 255)
+    ada = network.AdaAttnTransformerMultiHead()
+    f = [torch.rand(1, 512, 8, 8)] * 3
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        ada(f, f)
+
+
+def test_compute_dtype_resolution():
+    from mhada_hip import engine
+    m = network.VisionTransformer()
+    assert engine.resolve_compute_dtype(m) == torch.float32
+    m.compute_dtype = torch.bfloat16
+    assert engine.resolve_compute_dtype(m) == torch.bfloat16
+    m.compute_dtype = torch.float16
+    with pytest.raises(ValueError):
+        engine.resolve_compute_dtype(m)
+
+
+def _header_symbols():
+    with open(os.path.join(REPO, "include", "mhada_hip.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mhada_\w+)\s*\(", src, re.M)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmhada_hip.so not built (run __graft_entry__.build())")
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
+    assert lib.mhada_abi_version() == 1
+
+
+def test_abi_argument_errors_without_gpu():
+    """Argument validation happens on the host before any launch."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmhada_hip.so not built")
+    lib = _lib.load()
+    assert lib.mhada_layernorm(None, None, 0, None, None, 4, 512, 1e-6, None) == 1
+    assert b"bad args" in lib.mhada_last_error()
+    args = _lib.GemmArgs()
+    args.M, args.N, args.K, args.nb1, args.nb2 = 4, 4, 4, 1, 1
+    args.compute = 7
+    assert lib.mhada_gemm(args, None) == 1
+    assert b"compute" in lib.mhada_last_error()
+    assert lib.mhada_attn(*([None] * 8), 0, 1, 8, 64, 64, 0, None) == 1

@@ -1,0 +1,227 @@
+"""Per-kernel numerics on the GPU: every C-ABI entry point against a plain-PyTorch fp64/fp32
+computation of the same op (tolerances stated per test).  Runs through libmhada_hip.so."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from mhada_hip import _lib, ops
+    DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def rnd(*shape, scale=1.0, seed=0, dtype=torch.float32):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV, dtype)
+
+
+# fp32 compute: exact-fp32 MFMA, only summation order differs -> 1e-5; bf16 operands -> 1e-2
+TOL = {torch.float32: 2e-5, torch.bfloat16: 1e-2}
+
+
+def test_library_is_the_native_one():
+    lib = _lib.load()
+    assert lib.mhada_abi_version() == 1
+    assert _lib.LIB_PATH.endswith("libmhada_hip.so")
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(100, 96, 64), (1024, 1536, 512), (333, 512, 2048), (4096, 64, 64), (17, 2048, 512)])
+def test_linear(cdt, M, N, K):
+    x = rnd(M, K, seed=1, dtype=cdt)
+    w = rnd(N, K, scale=K ** -0.5, seed=2, dtype=cdt)
+    b = rnd(N, seed=3)
+    r = rnd(M, N, seed=4)
+    y = ops.linear(x, w, b, torch.float32, residual=r, relu=False)
+    ref = x.double() @ w.double().T + b.double() + r.double()
+    assert rel(y, ref) < TOL[cdt]
+    y2 = ops.linear(x, w, b, cdt, relu=True)
+    ref2 = torch.relu(x.double() @ w.double().T + b.double())
+    assert rel(y2, ref2) < TOL[cdt] + (4e-3 if cdt == torch.bfloat16 else 0)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_linear_fp32_input_converted_on_load(cdt):
+    x = rnd(300, 512, seed=5)
+    w = rnd(512, 512, scale=512 ** -0.5, seed=6, dtype=cdt)
+    y = ops.linear(x, w, None, torch.float32)
+    ref = x.to(cdt).double() @ w.double().T
+    assert rel(y, ref) < TOL[cdt]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_grouped_centred_projection(cdt):
+    """The MHAda per-head projection pattern: z = (batch, head), A centred per column."""
+    B, H, N, C = 2, 8, 200, 512
+    x = rnd(B, N, C, seed=7) * 3 + 1.5
+    mu = x.mean(dim=1)  # [B][C]
+    w = rnd(B, H, 64, 64, scale=0.125, seed=8, dtype=cdt)
+    bias = rnd(H, 64, seed=9)
+    q = torch.empty(B, H, N, 64, device=DEV, dtype=cdt)
+    ops.gemm(a=x, w=w, c=q, M=N, N=64, K=64, compute=cdt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
+             smu=(C, 64), ldw=64, sw=(H * 4096, 4096), bias=bias, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
+    xc = (x - mu[:, None, :]).view(B, N, H, 64).permute(0, 2, 1, 3).to(cdt).double()
+    ref = xc @ w.double().transpose(-1, -2) + bias.double()[None, :, None, :]
+    assert rel(q, ref) < TOL[cdt]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H,W", [(64, 64), (72, 128), (16, 24)])
+def test_patch_embed(cdt, H, W):
+    B = 2
+    img = torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(3)).to(DEV) * 255
+    w = rnd(512, 3, 8, 8, scale=0.05, seed=4)
+    b = rnd(512, seed=5)
+    pos = rnd((H // 8) * (W // 8), 512, seed=6)
+    y = ops.patch_embed(img, w.reshape(512, -1).to(cdt).contiguous(), b, pos)
+    ref = F.conv2d(img.to(cdt).double(), w.to(cdt).double(), b.double(), stride=8)
+    ref = ref.flatten(2).transpose(1, 2) + pos.double()
+    assert rel(y, ref) < TOL[cdt]
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("up", [False, True])
+@pytest.mark.parametrize("Ci,Co,H,W", [(64, 64, 9, 13), (128, 64, 16, 16), (512, 256, 8, 8), (256, 128, 5, 3)])
+def test_conv3x3(cdt, up, Ci, Co, H, W):
+    B = 2
+    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(Ci + H)).to(DEV)
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, seed=2)
+    b = rnd(Co, seed=3)
+    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).to(cdt).contiguous()
+    y = ops.conv3x3(x.to(cdt) if cdt == torch.bfloat16 and not up else x, wp, b, torch.float32, upsample=up)
+    xn = x.permute(0, 3, 1, 2).double()
+    if cdt == torch.bfloat16 and not up:
+        xn = x.to(cdt).permute(0, 3, 1, 2).double()
+    if up:
+        xn = F.interpolate(xn, scale_factor=2, mode="bilinear", align_corners=False)
+    ref = torch.relu(F.conv2d(F.pad(xn, (1, 1, 1, 1), mode="reflect"), w.to(cdt).double(), b.double()))
+    assert rel(y.permute(0, 3, 1, 2), ref) < TOL[cdt]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("clamp", [False, True])
+def test_conv_out3(dt, clamp):
+    B, H, W, Ci = 2, 20, 33, 64
+    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(9)).to(DEV).to(dt)
+    w = rnd(3, Ci, 3, 3, scale=0.5, seed=2)
+    b = rnd(3, seed=3) * 30
+    y = ops.conv3x3_out3(x, w.permute(0, 2, 3, 1).contiguous(), b, clamp255=clamp)
+    ref = torch.relu(F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
+                              w.double(), b.double()))
+    if clamp:
+        ref = ref.clamp(max=255)
+    assert rel(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm(dt):
+    x = rnd(1000, 512, seed=1) * 4 + 2
+    g, b = rnd(512, seed=2), rnd(512, seed=3)
+    y = ops.layernorm(x, g, b, dt, 1e-6)
+    ref = F.layer_norm(x.double(), (512,), g.double(), b.double(), 1e-6)
+    assert rel(y, ref) < (1e-6 if dt == torch.float32 else 5e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("L", [1, 2, 3, 8])
+def test_vit_batch_attention_matches_nn_mha(dt, L):
+    N, C, heads = 300, 512, 8
+    mha = torch.nn.MultiheadAttention(C, heads).to(DEV).double()
+    x = rnd(L, N, C, seed=L).double()
+    with torch.no_grad():
+        ref, _ = mha(x, x, x, need_weights=False)  # batch_first=False on (B, N, C): attends over B
+        qkv = F.linear(x, mha.in_proj_weight, mha.in_proj_bias).to(dt)
+        att = ops.vit_batch_attn(qkv.contiguous(), L, N, heads)
+        y = F.linear(att.double(), mha.out_proj.weight, mha.out_proj.bias)
+    assert rel(y, ref) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("oh,ow", [(8, 8), (64, 64), (135, 240), (32, 32), (9, 16)])
+def test_pos_embed(oh, ow):
+    pos = rnd(1, 512, 32, 32, scale=0.02, seed=1)
+    y = ops.pos_embed(pos, oh, ow)
+    ref = pos if (oh, ow) == (32, 32) else F.interpolate(pos, size=(oh, ow), mode="bilinear", align_corners=False)
+    ref = ref.reshape(512, -1).T
+    assert rel(y, ref) < 1e-6
+
+
+def test_instnorm_stats():
+    x = rnd(3, 4097, 512, seed=2) * 5 + 10
+    mu, rstd = ops.instnorm_stats(x)
+    xd = x.double()
+    ref_mu = xd.mean(1)
+    ref_rstd = 1 / torch.sqrt(xd.var(1, unbiased=False) + 1e-5)
+    assert rel(mu, ref_mu) < 1e-7
+    assert rel(rstd, ref_rstd) < 1e-6
+
+
+# ---- the fused MHAda attention, through the AdaAttnMultiHead module --------------------------
+def _block(act, dt):
+    import network
+    from mhada_hip.recipe import load_recipe
+    blk = load_recipe(network.AdaAttnMultiHead(512, 8, act), "blk").to(DEV)
+    blk.compute_dtype = dt
+    return blk
+
+
+def _ref_block(blk, fc, fs, fcs, act):
+    import torch_ref
+    sd = {k: v.double() for k, v in blk.state_dict().items()}
+    with torch.no_grad():
+        return torch_ref.block(fc.double(), fs.double(), fcs.double(), sd, "", activation=act)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["softmax", "cosine"])
+@pytest.mark.parametrize("B,hc,wc,hs,ws", [(1, 8, 8, 8, 8), (2, 10, 13, 3, 5), (1, 16, 17, 20, 11), (2, 64, 64, 32, 32)])
+def test_mhada_block(dt, act, B, hc, wc, hs, ws):
+    blk = _block(act, dt)
+    fc = rnd(B, 512, hc, wc, seed=1) * 2 + 0.5
+    fs = rnd(B, 512, hs, ws, seed=2) * 1.5 - 0.25
+    fcs = rnd(B, 512, hc, wc, seed=3)
+    with torch.no_grad():
+        y = blk(fc, fs, fcs)
+    ref = _ref_block(blk, fc, fs, fcs, act)
+    assert rel(y, ref) < (1e-5 if dt == torch.float32 else 1.5e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mhada_online_softmax_rescale_branch(dt):
+    """Force the running max to jump in a LATE key tile (cdna_hip_programming.md rule 26):
+    one style token far out along the content direction dominates every query."""
+    blk = _block("softmax", dt)
+    B, hc, wc, hs, ws = 1, 16, 16, 16, 16
+    fc = rnd(B, 512, hc, wc, seed=4)
+    fs = rnd(B, 512, hs, ws, seed=5)
+    fs[:, :, 15, 10] = 12.0  # token 250 of 256: in the last 64-key tile
+    fcs = rnd(B, 512, hc, wc, seed=6)
+    with torch.no_grad():
+        y = blk(fc, fs, fcs)
+    ref = _ref_block(blk, fc, fs, fcs, "softmax")
+    assert torch.isfinite(y).all()
+    # logits reach +-58 here: the fp32 PyTorch computation itself is 3.7e-5 off fp64, and bf16
+    # Q/K carry ~0.2 absolute logit error; a wrong rescale at the jump would be O(1) off.
+    import torch_ref
+    sd32 = {k: v.float() for k, v in blk.state_dict().items()}
+    with torch.no_grad():
+        err32 = rel(torch_ref.block(fc, fs, fcs, sd32, ""), ref)
+    assert rel(y, ref) < (max(1e-5, 2 * err32) if dt == torch.float32 else 5e-2)
+
+
+def test_mhada_is_per_sample_independent():
+    """Unlike the ViT (batch-axis attention), MHAda blocks are per-sample."""
+    blk = _block("softmax", torch.float32)
+    fc = rnd(3, 512, 12, 12, seed=7)
+    fs = rnd(3, 512, 9, 9, seed=8)
+    with torch.no_grad():
+        y = blk(fc, fs, fc)
+        y1 = blk(fc[1:2], fs[1:2], fc[1:2])
+    assert rel(y[1:2], y1) < 1e-6
