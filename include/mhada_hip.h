@@ -132,9 +132,15 @@ int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
 /* Last decoder layer (conv.py:96, ConvReLU(64, 3)): ReflectionPad2d(1) + conv3x3 Cin->3 +
  * bias + ReLU on NHWC x [B][H][W][Cin] (dtype), written NCHW fp32 y [B][3][H][W] — the
  * module's output layout.  clamp255 != 0 also applies the caller's clamp(0,255)
- * (infer_image.py:86). w fp32 [3][3][3][Cin] (out, ky, kx, cin). */
+ * (infer_image.py:86). w fp32 [9][Cin][3] (tap = 3*ky+kx, cin, out); Cin in {32, 64, 128}. */
 int mhada_conv3x3_out3(const void* x, int dtype, const float* w, const float* b, float* y,
                        int B, int H, int W, int Cin, int clamp255, mhada_stream_t stream);
+
+/* Bilinear x2 upsample, align_corners=False (ConvReluInterpolate, conv.py:71) on NHWC:
+ * x [B][H][W][C] -> y [B][2H][2W][C], dtype fp32|bf16, C % 8 == 0.  Used where the decoder's
+ * upsample is not fused into the next conv's operand gather (the bf16 path). */
+int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int C,
+                     mhada_stream_t stream);
 
 #ifdef __cplusplus
 }

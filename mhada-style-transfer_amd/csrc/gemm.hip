@@ -176,13 +176,13 @@ MHADA_DEV void issue_a(AStage<TA, TC, AMODE, A_CH>& st, const GemmP& p, const TA
   }
 }
 
-template <typename TA, typename TC, int AMODE, int A_CH>
+template <int RS, typename TA, typename TC, int AMODE, int A_CH>
 MHADA_DEV void commit_a(const AStage<TA, TC, AMODE, A_CH>& st, TC* sA, int tid) {
   constexpr int E = Cfg<TC>::E, LS = Cfg<TC>::LS;
   const int kc = tid & 7;
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    const int row = (tid >> 3) + 32 * i;
+    const int row = (tid >> 3) + RS * i;
     float f[E];
     if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {
       const float ly0 = st.wt[i][0], ly1 = st.wt[i][1], lx0 = st.wt[i][2], lx1 = st.wt[i][3];
@@ -199,11 +199,16 @@ MHADA_DEV void commit_a(const AStage<TA, TC, AMODE, A_CH>& st, TC* sA, int tid) 
 }
 
 // ------------------------------------------------------------------------------------
-template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN>
-__global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
+// BM x BN block tile, WM x WN waves (NT = 64*WM*WN threads); each wave owns a
+// (BM/WM) x (BN/WN) sub-tile of TM x TN 32x32 MFMA blocks.
+// ------------------------------------------------------------------------------------
+template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
+  constexpr int NT = 64 * WM * WN, RS = NT / 8;  // RS: rows staged per pass
   constexpr int E = Cfg<TC>::E, BK = Cfg<TC>::BK, LS = Cfg<TC>::LS;
-  constexpr int WN = BN / 64;
-  constexpr int A_CH = BM * 8 / 256, B_CH = BN * 8 / 256;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int A_CH = BM / RS, B_CH = BN / RS;
+  static_assert(A_CH >= 1 && B_CH >= 1 && TM >= 1 && TN >= 1, "tile config");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TC* sA = reinterpret_cast<TC*>(smem);  // [2][BM][LS]
   TC* sB = sA + 2 * BM * LS;             // [2][BN][LS]
@@ -224,7 +229,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
   RowInfo ri[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
+    const int m = m0 + (tid >> 3) + RS * i;
     ri[i].valid = m < p.M;
     const int mm = m < p.M ? m : 0;
     if constexpr (AMODE == MHADA_A_ROWS) {
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
   bool bval[B_CH];
 #pragma unroll
   for (int i = 0; i < B_CH; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
+    const int n = n0 + (tid >> 3) + RS * i;
     bval[i] = n < p.N;
     brow[i] = n < p.N ? n : 0;
   }
@@ -264,25 +269,26 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
   auto commit_b = [&](TC* dst) {
 #pragma unroll
     for (int i = 0; i < B_CH; ++i)
-      *reinterpret_cast<typename Vec16<TC>::type*>(dst + ((tid >> 3) + 32 * i) * LS + kc * E) = bst[i];
+      *reinterpret_cast<typename Vec16<TC>::type*>(dst + ((tid >> 3) + RS * i) * LS + kc * E) = bst[i];
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
   const int KT = (p.K + BK - 1) / BK;
   issue_a<TA, TC, AMODE, A_CH>(ast, pz, abase, ri, 0, kc);
   issue_b(0);
-  commit_a<TA, TC, AMODE, A_CH>(ast, sA, tid);
+  commit_a<RS>(ast, sA, tid);
   commit_b(sB);
   __syncthreads();
 
   const int h = lane >> 5, r32 = lane & 31;
+  const int arow0 = wm * (BM / WM) + r32, brow0 = wn * (BN / WN) + r32;
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < KT) {
@@ -294,43 +300,46 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
     if constexpr (sizeof(TC) == 2) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8 af[2], bfr[2];
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-          af[mi] = *reinterpret_cast<const bf16x8*>(cA + (wm * 64 + mi * 32 + r32) * LS + ks * 16 + 8 * h);
+        for (int mi = 0; mi < TM; ++mi)
+          af[mi] = *reinterpret_cast<const bf16x8*>(cA + (arow0 + mi * 32) * LS + ks * 16 + 8 * h);
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(cB + (wn * 64 + ni * 32 + r32) * LS + ks * 16 + 8 * h);
+        for (int ni = 0; ni < TN; ++ni)
+          bfr[ni] = *reinterpret_cast<const bf16x8*>(cB + (brow0 + ni * 32) * LS + ks * 16 + 8 * h);
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
+          for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
       }
     } else {
       // fp32: lane half h supplies k = 16h + s at MFMA step s (both operands agree)
-      f32x4 av[2][4], bv[2][4];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int half = 0; half < 2; ++half) {
+        f32x4 av[TM][2], bv[TN][2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          av[mi][q] = *reinterpret_cast<const f32x4*>(cA + (wm * 64 + mi * 32 + r32) * LS + 16 * h + 4 * q);
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+          for (int q = 0; q < 2; ++q)
+            av[mi][q] = *reinterpret_cast<const f32x4*>(cA + (arow0 + mi * 32) * LS + 16 * h + 8 * half + 4 * q);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          bv[ni][q] = *reinterpret_cast<const f32x4*>(cB + (wn * 64 + ni * 32 + r32) * LS + 16 * h + 4 * q);
+        for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
+          for (int q = 0; q < 2; ++q)
+            bv[ni][q] = *reinterpret_cast<const f32x4*>(cB + (brow0 + ni * 32) * LS + 16 * h + 8 * half + 4 * q);
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int s = 0; s < 8; ++s)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s >> 2][s & 3], bv[ni][s >> 2][s & 3],
-                                                               acc[mi][ni], 0, 0, 0);
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s >> 2][s & 3], bv[ni][s >> 2][s & 3],
+                                                                 acc[mi][ni], 0, 0, 0);
+      }
     }
     if (kt + 1 < KT) {
-      commit_a<TA, TC, AMODE, A_CH>(ast, sA + (buf ^ 1) * BM * LS, tid);
+      commit_a<RS>(ast, sA + (buf ^ 1) * BM * LS, tid);
       commit_b(sB + (buf ^ 1) * BN * LS);
     }
     __syncthreads();
@@ -341,15 +350,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
   const TO* rbase = p.r ? reinterpret_cast<const TO*>(p.r) + z1 * p.sr1 + z2 * p.sr2 : nullptr;
   const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int n = n0 + wn * 64 + ni * 32 + r32;
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = n0 + brow0 + ni * 32;
     if (n >= p.N) continue;
     const float bias = bbase ? bbase[n] : 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
+    for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int m = m0 + arow0 - r32 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (m < p.M) {
           float v = acc[mi][ni][e] + bias;
           if (p.relu) v = fmaxf(v, 0.f);
@@ -361,7 +370,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmP p) {
   }
 }
 
-template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN>
+template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN, int WM, int WN>
 static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -370,17 +379,32 @@ static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
   const size_t lds = (size_t)2 * (BM + BN) * Cfg<TC>::LS * sizeof(TC);
   static std::once_flag attr_once;  // per instantiation: allow > 64 KiB dynamic LDS
   std::call_once(attr_once, [&] {
-    (void)hipFuncSetAttribute((const void*)gemm_kernel<TC, TA, TO, AMODE, BM, BN>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<TC, TA, TO, AMODE, BM, BN, WM, WN>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   });
-  hipLaunchKernelGGL((gemm_kernel<TC, TA, TO, AMODE, BM, BN>), dim3(p.ntiles, nz), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((gemm_kernel<TC, TA, TO, AMODE, BM, BN, WM, WN>), dim3(p.ntiles, nz), dim3(64 * WM * WN),
+                     lds, stream, p);
   return check_launch("mhada_gemm");
 }
 
+// Tile choice.  fp32 MFMA runs 1/16 of the bf16 rate, so 128x128 tiles (64 FLOP per staged
+// byte) are far from L2-bound; bf16 needs 256-row tiles (up to 128 FLOP/B at 256x256) to stay
+// under the ~34 TB/s L2 ceiling at MFMA rate.
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
-  if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64>(p, nz, s);
-  return launch_gemm<TC, TA, TO, AMODE, 128, 128>(p, nz, s);
+  if constexpr (sizeof(TC) == 4) {
+    if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
+    return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
+  } else {
+    if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {  // 4 bilinear taps staged per chunk: keep the tile small
+      if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
+      return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
+    } else {
+      if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
+      if (p.N <= 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
+      return launch_gemm<TC, TA, TO, AMODE, 256, 256, 2, 4>(p, nz, s);
+    }
+  }
 }
 
 template <typename TC, typename TA, typename TO>

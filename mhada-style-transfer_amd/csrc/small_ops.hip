@@ -232,40 +232,38 @@ __global__ void __launch_bounds__(256) rownorm_kernel(T* __restrict__ x, long lo
 
 // ---------------------------------------------------------------------------------------
 // Last decoder layer: ReflectionPad(1) + conv3x3 Cin->3 + bias + ReLU, NHWC in, NCHW fp32 out.
-// One thread per output pixel; the 27*Cin weights live in LDS.
+// One thread per output pixel (adjacent lanes = adjacent pixels, each reading its own
+// contiguous Cin-vector).  Weights are indexed only by loop counters and kernel arguments,
+// so they are wave-uniform: the compiler fetches them with scalar loads into SGPRs and the
+// FMAs take them as scalar operands (no LDS broadcast traffic).
 // ---------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int CIN>
 __global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                        int B, int H, int W, int Cin, int clamp255) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sw = reinterpret_cast<float*>(smem);  // [tap][cin][3]
-  for (int i = threadIdx.x; i < 27 * Cin; i += 256) {
-    const int o = i / (9 * Cin), rem = i - o * 9 * Cin;  // w layout [o][tap][cin]
-    sw[rem * 3 + o] = w[i];
-  }
-  __syncthreads();
+                                                        int B, int H, int W, int clamp255) {
   const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
   if (pix >= (long long)B * H * W) return;
   const int b = (int)(pix / ((long long)H * W));
   const int rem = (int)(pix - (long long)b * H * W);
   const int yy = rem / W, xx = rem - (rem / W) * W;
   float a0 = bias[0], a1 = bias[1], a2 = bias[2];
+  constexpr int EV = 16 / sizeof(T);
+#pragma unroll 1
   for (int tap = 0; tap < 9; ++tap) {
     int Y = yy + tap / 3 - 1, X = xx + tap % 3 - 1;
     Y = Y < 0 ? -Y : (Y >= H ? 2 * H - 2 - Y : Y);
     X = X < 0 ? -X : (X >= W ? 2 * W - 2 - X : X);
-    const T* px = x + (((long long)b * H + Y) * W + X) * Cin;
-    const float* wt = sw + tap * Cin * 3;
-    constexpr int EV = 16 / sizeof(T);
-    for (int c = 0; c < Cin; c += EV) {
+    const T* px = x + (((long long)b * H + Y) * W + X) * CIN;
+    const float* wt = w + tap * CIN * 3;  // [tap][cin][out]
+#pragma unroll
+    for (int c = 0; c < CIN; c += EV) {
       const typename Vec16<T>::type v = *reinterpret_cast<const typename Vec16<T>::type*>(px + c);
 #pragma unroll
       for (int e = 0; e < EV; ++e) {
         const float f = (float)v[e];
-        a0 += f * wt[(c + e) * 3 + 0];
-        a1 += f * wt[(c + e) * 3 + 1];
-        a2 += f * wt[(c + e) * 3 + 2];
+        a0 = fmaf(f, wt[(c + e) * 3 + 0], a0);
+        a1 = fmaf(f, wt[(c + e) * 3 + 1], a1);
+        a2 = fmaf(f, wt[(c + e) * 3 + 2], a2);
       }
     }
   }
@@ -276,6 +274,44 @@ __global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x,
   yb[0] = a0;
   yb[plane] = a1;
   yb[2 * plane] = a2;
+}
+
+// ---------------------------------------------------------------------------------------
+// Bilinear x2 upsample on NHWC (F.interpolate(scale_factor=2, bilinear, align_corners=False),
+// conv.py:71): one thread per (output pixel, 8-channel group), fp32 blend in PyTorch's order.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
+                                                         int W, int C) {
+  const int G = C / 8;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)B * 4 * H * W * G;
+  if (idx >= total) return;
+  const int g = (int)(idx % G);
+  long long pix = idx / G;
+  const int Wo = 2 * W, Ho = 2 * H;
+  const int X = (int)(pix % Wo);
+  pix /= Wo;
+  const int Y = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
+  const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.f);
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const T* base = x + (long long)b * H * W * C + g * 8;
+  const T* p00 = base + ((long long)y0 * W + x0) * C;
+  const T* p01 = base + ((long long)y0 * W + x1) * C;
+  const T* p10 = base + ((long long)y1 * W + x0) * C;
+  const T* p11 = base + ((long long)y1 * W + x1) * C;
+  T* out = y + (((long long)b * Ho + Y) * Wo + X) * C + g * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = ly0 * (lx0 * to_f32<T>(p00[e]) + lx1 * to_f32<T>(p01[e])) +
+                    ly1 * (lx0 * to_f32<T>(p10[e]) + lx1 * to_f32<T>(p11[e]));
+    out[e] = from_f32<T>(v);
+  }
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -391,17 +427,40 @@ extern "C" int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int
 
 extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, const float* b, float* y, int B, int H,
                                   int W, int Cin, int clamp255, mhada_stream_t s_) {
-  if (!x || !w || !b || !y || B <= 0 || H < 2 || W < 2 || Cin <= 0) return fail("mhada_conv3x3_out3: bad args");
-  const int ev = dtype == MHADA_F32 ? 4 : 8;
-  if (Cin % ev || !aligned16(x)) return fail("mhada_conv3x3_out3: Cin must fill 16-byte vectors");
+  if (!x || !w || !b || !y || B <= 0 || H < 2 || W < 2) return fail("mhada_conv3x3_out3: bad args");
+  if (!aligned16(x)) return fail("mhada_conv3x3_out3: x must be 16-byte aligned");
   const long long pix = (long long)B * H * W;
-  const size_t lds = (size_t)27 * Cin * sizeof(float);
   const dim3 grid((unsigned)((pix + 255) / 256));
-  if (dtype == MHADA_F32)
-    hipLaunchKernelGGL((conv_out3_kernel<float>), grid, dim3(256), lds, (hipStream_t)s_, (const float*)x, w, b, y, B,
-                       H, W, Cin, clamp255);
-  else
-    hipLaunchKernelGGL((conv_out3_kernel<bf16>), grid, dim3(256), lds, (hipStream_t)s_, (const bf16*)x, w, b, y, B,
-                       H, W, Cin, clamp255);
+  hipStream_t s = (hipStream_t)s_;
+#define OUT3_CASE(CI)                                                                                          \
+  case CI:                                                                                                     \
+    if (dtype == MHADA_F32)                                                                                    \
+      hipLaunchKernelGGL((conv_out3_kernel<float, CI>), grid, dim3(256), 0, s, (const float*)x, w, b, y, B, H, W, \
+                         clamp255);                                                                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((conv_out3_kernel<bf16, CI>), grid, dim3(256), 0, s, (const bf16*)x, w, b, y, B, H, W,   \
+                         clamp255);                                                                            \
+    break;
+  switch (Cin) {
+    OUT3_CASE(64)
+    OUT3_CASE(32)
+    OUT3_CASE(128)
+    default:
+      return fail("mhada_conv3x3_out3: Cin must be 32, 64 or 128");
+  }
+#undef OUT3_CASE
   return check_launch("mhada_conv3x3_out3");
+}
+
+extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int C, mhada_stream_t s_) {
+  if (!x || !y || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return fail("mhada_upsample2x: bad args");
+  const long long total = (long long)B * 4 * H * W * (C / 8);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == MHADA_F32)
+    hipLaunchKernelGGL((upsample2x_kernel<float>), grid, dim3(256), 0, (hipStream_t)s_, (const float*)x, (float*)y, B,
+                       H, W, C);
+  else
+    hipLaunchKernelGGL((upsample2x_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)x, (bf16*)y, B,
+                       H, W, C);
+  return check_launch("mhada_upsample2x");
 }

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_upsample2x": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
 }
 
 _lib = None

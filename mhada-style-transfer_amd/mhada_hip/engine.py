@@ -29,6 +29,11 @@ DECODER_LAYERS: Tuple[Tuple[str, bool], ...] = (
     ("conv1.4", False), ("conv2.0", True), ("conv2.1", False), ("conv3.0", True),
 )
 LAST_LAYER = "conv3.1"
+# Where the decoder's bilinear x2 runs: fused into the next conv's operand gather (no extra
+# HBM round trip; fp32, where the MFMA is slow enough to hide the 4-tap gather), or as a
+# standalone NHWC upsample kernel followed by a plain conv (bf16, which keeps the conv's
+# tile large; the upsampled tensor costs one extra write+read).
+FUSE_UPSAMPLE = {torch.float32: True, torch.bfloat16: False}
 
 
 # ---------------------------------------------------------------------------------------
@@ -260,7 +265,8 @@ def decoder_prep(dec, dtype):
             w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1).to(dt).contiguous()
             layers.append((w, conv.bias.float().contiguous(), up))
         last = mods[LAST_LAYER].conv.conv
-        return dict(layers=layers, w_last=last.weight.permute(0, 2, 3, 1).float().contiguous(),
+        # [out][cin][ky][kx] -> [ky*3+kx][cin][out]
+        return dict(layers=layers, w_last=last.weight.permute(2, 3, 1, 0).float().contiguous(),
                     b_last=last.bias.float().contiguous())
     return cached_prep(dec, dtype, build)
 
@@ -270,6 +276,9 @@ def decoder_forward_tokens(dec, x_nhwc: torch.Tensor, dt: torch.dtype, clamp255:
     prep = decoder_prep(dec, dt)
     x = x_nhwc
     for w, b, up in prep["layers"]:
+        if up and not FUSE_UPSAMPLE[dt]:
+            x = ops.upsample2x(x)
+            up = False
         x = ops.conv3x3(x, w, b, dt, upsample=up, relu=True)
     return ops.conv3x3_out3(x, prep["w_last"], prep["b_last"], clamp255=clamp255)
 

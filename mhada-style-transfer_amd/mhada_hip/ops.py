@@ -115,6 +115,16 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out_dtype: tor
                 bias=bias, ldc=Co, relu=relu)
 
 
+def upsample2x(x: torch.Tensor) -> torch.Tensor:
+    """NHWC bilinear x2 (align_corners=False)."""
+    _need_gpu(x)
+    B, H, W, C = x.shape
+    y = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=x.dtype)
+    rc = _lib.load().mhada_upsample2x(x.data_ptr(), y.data_ptr(), dt_code(x.dtype), B, H, W, C, _stream())
+    _lib.check(rc, "mhada_upsample2x")
+    return y
+
+
 def conv3x3_out3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, clamp255: bool = False) -> torch.Tensor:
     B, H, W, Ci = x.shape
     _need_gpu(x, w, bias)

@@ -107,13 +107,22 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128)])
+def test_upsample2x(dt, H, W, C):
+    x = rnd(2, H, W, C, seed=H).to(dt)
+    y = ops.upsample2x(x)
+    ref = F.interpolate(x.permute(0, 3, 1, 2).double(), scale_factor=2, mode="bilinear", align_corners=False)
+    assert rel(y.permute(0, 3, 1, 2), ref) < (1e-6 if dt == torch.float32 else 5e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("clamp", [False, True])
 def test_conv_out3(dt, clamp):
     B, H, W, Ci = 2, 20, 33, 64
     x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(9)).to(DEV).to(dt)
     w = rnd(3, Ci, 3, 3, scale=0.5, seed=2)
     b = rnd(3, seed=3) * 30
-    y = ops.conv3x3_out3(x, w.permute(0, 2, 3, 1).contiguous(), b, clamp255=clamp)
+    y = ops.conv3x3_out3(x, w.permute(2, 3, 1, 0).contiguous(), b, clamp255=clamp)
     ref = torch.relu(F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
                               w.double(), b.double()))
     if clamp:
