@@ -154,6 +154,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the 1024^2 bf16 config")
+    ap.add_argument("--only-secondary", action="store_true", help="run only the 1024^2 bf16 config (profiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,6 +164,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.only_secondary:
+        r = run_config(1024, 4, torch.bfloat16, args.steps, args.warmup, rank, world)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        return
     main_cfg = run_config(512, 8, torch.float32, args.steps, args.warmup, rank, world)
     second = None if args.no_secondary else run_config(1024, 4, torch.bfloat16, args.steps, args.warmup, rank, world)
 

@@ -109,8 +109,10 @@ int mhada_fold_block(const float* wf, const float* wg, const float* wh, const fl
                      const float* rstd_s, void* wq, void* wkv, float* bkv, float* v_mu,
                      int dtype, int B, int H, mhada_stream_t stream);
 
-/* bf16 path: VT[b][h][o][n] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), from
- * kv [B][H][Ns][128]; the transposed operand image the attention kernel streams. */
+/* bf16 path: the transposed operand image the attention kernel streams, from kv [B][H][Ns][128]:
+ * VT[b][h][o][pos(n)] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), row stride
+ * ceil64(Ns) (zero padded); pos() swaps bits 2 and 3 of n (keys permuted inside groups of 16
+ * to match the MFMA accumulator's row order). */
 int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t stream);
 
 /* L2-normalise the 64-wide rows of q [B][H][Nc][64] and the K half of kv [B][H][Ns][128]

@@ -15,21 +15,30 @@
 //   O^T (dv x queries)   = V'^T . P^T — P^T is the S^T accumulator itself, used as the B
 //       operand with no lane movement; the dv/key index pairing follows the accumulator's
 //       row permutation.
+// Online softmax with a deferred rescale (cdna_hip_programming.md T13): the running max m
+// only moves when a tile's max exceeds it by more than 2^8 (log2 units), so after the first
+// tiles the O accumulators are never touched by VALU (no AGPR<->VGPR traffic); P <= 2^8.
+// Only the last, partial key tile runs the masking code.
 // fp32: v_mfma_f32_32x32x2_f32 (exact fp32), K/V' streamed from kv[.][128] into LDS, V'^2
 //       formed in registers.  bf16: v_mfma_f32_32x32x16_bf16, V'^T and V'^2^T streamed from
-//       the pre-transposed vt image (mhada_transpose_v), fp32 accumulation and softmax.
-// Block = 4 waves = 128 queries of one (batch, head); blocks of one (b, h) are remapped onto
-// one XCD so they share K/V in its L2.
+//       the pre-transposed, key-permuted vt image (mhada_transpose_v) so every operand read
+//       is one 16-byte ds_read; fp32 accumulation and softmax.
+// Block = NW waves = 32*NW queries of one (batch, head); blocks of one (b, h) are remapped
+// onto one XCD so they share K/V in its L2.
 #include "common.h"
+
+#include <stdlib.h>
+#include <type_traits>
 
 namespace mhada {
 
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kRescaleThr = 32.0f;  // log2 units: P <= 2^32, sums stay far below fp32 overflow
 
 struct AttnP {
   const void* q;    // [B][H][Nc][64]
   const void* kv;   // [B][H][Ns][128]
-  const void* vt;   // bf16: [B][H][128][ldt]
+  const void* vt;   // bf16: [B][H][128][ldt], keys permuted within groups of 16
   const float* fcs; // [B][Nc][C]
   const float* fcs_mu;
   const float* fcs_rstd;
@@ -79,56 +88,93 @@ MHADA_DEV void attn_epilogue(const AttnP& p, const f32x16 (&O)[4], float l, int 
   }
 }
 
-// Online-softmax update of one tile (32 scores per lane: S[kb][r], key index
-// kb*32 + (r&3) + 8(r>>2) + 4h); returns the rescale factor for O.  Cosine: p = s (+1 done
-// by caller), no max.
+// Scores of keys >= Ns: -inf (softmax) / -1 (cosine: p = s + 1 = 0).
 template <int ACT>
-MHADA_DEV float softmax_tile(f32x16 (&S)[2], float& m, float& l, int key0, int Ns, int h) {
-  const bool partial = key0 + 64 > Ns;
-  if (partial) {
+MHADA_DEV void mask_tile(f32x16 (&S)[2], int key0, int Ns, int h) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (key >= Ns) S[kb][r] = (ACT == MHADA_ACT_SOFTMAX) ? -INFINITY : -1.0f;
-      }
-  }
+    for (int r = 0; r < 16; ++r) {
+      const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (key >= Ns) S[kb][r] = (ACT == MHADA_ACT_SOFTMAX) ? -INFINITY : -1.0f;
+    }
+}
+
+// Online-softmax update of one tile: S becomes P (in place); returns true (wave-uniform)
+// when the O accumulators must be multiplied by `alpha`.  m2 is the running max in log2 units.
+template <int ACT>
+MHADA_DEV bool softmax_tile(f32x16 (&S)[2], float& m2, float& l, float& alpha) {
+  float sum = 0.f;
   if constexpr (ACT == MHADA_ACT_SOFTMAX) {
     float mx = S[0][0];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[kb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = fast_exp2((m - mn) * kLog2e);
-    const float mb = mn * kLog2e;
-    float sum = 0.f;
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * kLog2e;
+    const bool resc = __any(mx > m2 + kRescaleThr);
+    alpha = 1.f;
+    if (resc) {
+      const float mn = fmaxf(m2, mx);
+      alpha = fast_exp2(m2 - mn);
+      l *= alpha;
+      m2 = mn;
+    }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = fast_exp2(S[kb][r] * kLog2e - mb);
-        S[kb][r] = pv;
-        sum += pv;
-      }
-    l = l * alpha + sum;
-    m = mn;
-    return alpha;
-  } else {
-    float sum = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = S[kb][r] + 1.0f;  // masked keys: -1 + 1 = 0
+        const float pv = fast_exp2(fmaf(S[kb][r], kLog2e, -m2));
         S[kb][r] = pv;
         sum += pv;
       }
     l += sum;
-    return 1.0f;
+    return resc;
+  } else {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = S[kb][r] + 1.0f;
+        S[kb][r] = pv;
+        sum += pv;
+      }
+    l += sum;
+    alpha = 1.f;
+    return false;
   }
+}
+
+// Tile max of the scores in log2 units, combined over the two lane halves (same query).
+MHADA_DEV float tile_max_log2(const f32x16 (&S)[2]) {
+  float mx = S[0][0];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[kb][r]);
+  return fmaxf(mx, __shfl_xor(mx, 32, 64)) * kLog2e;
+}
+
+// S -> P against the current running max (no rescale); accumulates the row sum.
+template <int ACT>
+MHADA_DEV void softmax_apply(f32x16 (&S)[2], float m2, float& l) {
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = (ACT == MHADA_ACT_SOFTMAX) ? fast_exp2(fmaf(S[kb][r], kLog2e, -m2)) : S[kb][r] + 1.0f;
+      S[kb][r] = pv;
+      sum += pv;
+    }
+  l += sum;
+}
+
+MHADA_DEV void scale_acc(f32x16 (&O)[4], float alpha) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
 }
 
 MHADA_DEV void decode_block(const AttnP& p, int& b, int& hh, int& qb) {
@@ -142,14 +188,16 @@ MHADA_DEV void decode_block(const AttnP& p, int& b, int& hh, int& qb) {
 // ======================================================================================
 // fp32 variant
 // ======================================================================================
-template <int ACT>
-__global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
+template <int ACT, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_f32_kernel(const AttnP p) {
+  constexpr int NT = 64 * NW;
   constexpr int LS = 132;  // LDS row (128 + 4 floats): conflict-free b128 K reads, b32 V reads
+  constexpr int CH = 2048 / NT;  // 16-B chunks per thread per tile (64 keys x 128 floats)
   __shared__ __attribute__((aligned(16))) float sKV[2][64 * LS];
   int b, hh, qb;
   decode_block(p, b, hh, qb);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
-  const int q = qb * 128 + wave * 32 + r32;
+  const int q = qb * (32 * NW) + wave * 32 + r32;
   const long long bh = (long long)b * p.H + hh;
 
   // Q^T operand: MFMA step s takes d = 32h + s
@@ -165,20 +213,19 @@ __global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
   }
   const float* kvb = reinterpret_cast<const float*>(p.kv) + bh * p.Ns * 128;
 
-  // staging: 64 keys x 128 floats = 2048 16-B chunks, 8 per thread (row = c >> 5, col = c & 31)
-  f32x4 stg[8];
+  f32x4 stg[CH];
   auto issue = [&](int key0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 4;
+    for (int i = 0; i < CH; ++i) {
+      const int c = tid + NT * i, row = c >> 5, col = (c & 31) * 4;
       const int key = key0 + row;
       stg[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto commit = [&](float* dst) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 4;
+    for (int i = 0; i < CH; ++i) {
+      const int c = tid + NT * i, row = c >> 5, col = (c & 31) * 4;
       *reinterpret_cast<f32x4*>(dst + row * LS + col) = stg[i];
     }
   };
@@ -188,17 +235,9 @@ __global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  float m2 = -INFINITY, l = 0.f;
 
-  const int NT = (p.Ns + 63) / 64;
-  issue(0);
-  commit(sKV[0]);
-  __syncthreads();
-  for (int t = 0; t < NT; ++t) {
-    const float* cur = sKV[t & 1];
-    if (t + 1 < NT) issue((t + 1) * 64);
-    // ---- S^T = K . Q^T --------------------------------------------------------------
-    f32x16 S[2];
+  auto qk = [&](const float* cur, f32x16 (&S)[2]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -212,15 +251,8 @@ __global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
           S[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk[e], qreg[4 * i + e], S[kb], 0, 0, 0);
       }
     }
-    // ---- online softmax ---------------------------------------------------------------
-    const float alpha = softmax_tile<ACT>(S, m, l, t * 64, p.Ns, h);
-    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
-    }
-    // ---- O^T += V'^T . P^T , (V'^2)^T . P^T ----------------------------------------
+  };
+  auto pv = [&](const float* cur, const f32x16 (&P)[2]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -228,15 +260,56 @@ __global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
         const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float* vrow = cur + key * LS + 64;
         const float v0 = vrow[r32], v1 = vrow[32 + r32];
-        const float pr = S[kb][r];
+        const float pr = P[kb][r];
         O[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, pr, O[0], 0, 0, 0);
         O[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, pr, O[1], 0, 0, 0);
         O[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0 * v0, pr, O[2], 0, 0, 0);
         O[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1 * v1, pr, O[3], 0, 0, 0);
       }
     }
-    if (t + 1 < NT) commit(sKV[(t + 1) & 1]);
-    __syncthreads();
+  };
+
+  const int NTILE = (p.Ns + 63) / 64, NFULL = p.Ns / 64;
+  issue(0);
+  commit(sKV[0]);
+  __syncthreads();
+  // Full tiles.  The hot loop never touches O outside the MFMAs: when a tile's max would
+  // push P past 2^kRescaleThr (always on the first tile) the wave leaves the loop, rescales
+  // O once and re-enters at the same tile (its K/V are still resident).
+  int t = 0;
+  while (t < NFULL) {
+    float mx = 0.f;
+    for (; t < NFULL; ++t) {
+      const float* cur = sKV[t & 1];
+      const bool nxt = t + 1 < NTILE;
+      if (nxt) issue((t + 1) * 64);
+      f32x16 S[2];
+      qk(cur, S);
+      if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+        mx = tile_max_log2(S);
+        if (__any(mx > m2 + kRescaleThr)) break;
+      }
+      softmax_apply<ACT>(S, m2, l);
+      pv(cur, S);
+      if (nxt) commit(sKV[(t + 1) & 1]);
+      __syncthreads();
+    }
+    if (t < NFULL) {
+      const float mn = fmaxf(m2, mx);
+      const float alpha = fast_exp2(m2 - mn);
+      l *= alpha;
+      scale_acc(O, alpha);
+      m2 = mn;
+    }
+  }
+  if (NFULL < NTILE) {  // ragged last tile: masked, full online-softmax update
+    const float* cur = sKV[NFULL & 1];
+    f32x16 S[2];
+    qk(cur, S);
+    mask_tile<ACT>(S, NFULL * 64, p.Ns, h);
+    float alpha;
+    if (softmax_tile<ACT>(S, m2, l, alpha)) scale_acc(O, alpha);
+    pv(cur, S);
   }
   attn_epilogue<float>(p, O, l, b, hh, q, h);
 }
@@ -244,17 +317,18 @@ __global__ void __launch_bounds__(256) attn_f32_kernel(const AttnP p) {
 // ======================================================================================
 // bf16 variant
 // ======================================================================================
-template <int ACT>
-__global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
-  constexpr int LK = 72;   // K tile row: 64 + 8 bf16 (144 B)
-  constexpr int LV = 68;   // VT tile row: 64 + 4 bf16 (136 B): conflict-free b64 reads
-  constexpr int KSZ = 64 * LK, VSZ = 128 * LV;
+template <int ACT, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
+  constexpr int NT = 64 * NW;
+  constexpr int LK = 72;  // 64 + 8 bf16 (144-B rows): conflict-free 16-B row reads
+  constexpr int KSZ = 64 * LK, VSZ = 128 * LK;
+  constexpr int KCH = 512 / NT, VCH = 1024 / NT;  // 16-B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) bf16 sK[2][KSZ];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][VSZ];
   int b, hh, qb;
   decode_block(p, b, hh, qb);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
-  const int q = qb * 128 + wave * 32 + r32;
+  const int q = qb * (32 * NW) + wave * 32 + r32;
   const long long bh = (long long)b * p.H + hh;
 
   // Q^T operand: k-step s takes d = 16s + 8h + j
@@ -273,12 +347,11 @@ __global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
   const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * p.Ns * 128;
   const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
 
-  // staging: K 64 rows x 8 chunks (2/thread), VT 128 rows x 8 chunks (4/thread)
-  bf16x8 sk[2], sv[4];
+  bf16x8 sk[KCH], sv[VCH];
   auto issue = [&](int key0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    for (int i = 0; i < KCH; ++i) {
+      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
       const int key = key0 + row;
       if (key < p.Ns) {
         sk[i] = *reinterpret_cast<const bf16x8*>(kvb + (long long)key * 128 + col);
@@ -288,25 +361,21 @@ __global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
       sv[i] = *reinterpret_cast<const bf16x8*>(vtb + (long long)row * p.ldt + key0 + col);  // zero-padded to ldt
     }
   };
   auto commit = [&](bf16* dk, bf16* dv) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    for (int i = 0; i < KCH; ++i) {
+      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
       *reinterpret_cast<bf16x8*>(dk + row * LK + col) = sk[i];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
-      // 136-B rows are only 8-B aligned: two b64 writes
-      bf16x4 lo = {sv[i][0], sv[i][1], sv[i][2], sv[i][3]};
-      bf16x4 hi = {sv[i][4], sv[i][5], sv[i][6], sv[i][7]};
-      *reinterpret_cast<bf16x4*>(dv + row * LV + col) = lo;
-      *reinterpret_cast<bf16x4*>(dv + row * LV + col + 4) = hi;
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<bf16x8*>(dv + row * LK + col) = sv[i];
     }
   };
 
@@ -315,17 +384,9 @@ __global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  float m2 = -INFINITY, l = 0.f;
 
-  const int NT = (p.Ns + 63) / 64;
-  issue(0);
-  commit(sK[0], sV[0]);
-  __syncthreads();
-  for (int t = 0; t < NT; ++t) {
-    const bf16* ck = sK[t & 1];
-    const bf16* cv = sV[t & 1];
-    if (t + 1 < NT) issue((t + 1) * 64);
-    f32x16 S[2];
+  auto qk = [&](const bf16* ck, f32x16 (&S)[2]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -337,36 +398,92 @@ __global__ void __launch_bounds__(256) attn_bf16_kernel(const AttnP p) {
         S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[s], S[kb], 0, 0, 0);
       }
     }
-    const float alpha = softmax_tile<ACT>(S, m, l, t * 64, p.Ns, h);
-    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
-    }
+  };
+  auto pv = [&](const bf16* cv, const f32x16 (&P)[2]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        // B = P^T: element j <-> key kb*32 + 16s + 8(j>>2) + 4h + (j&3)  (accumulator regs 8s..8s+7)
+        // B = P^T: element j <-> key kb*32 + 16s + 8(j>>2) + 4h + (j&3) (accumulator regs 8s..8s+7);
+        // the vt image stores those 8 keys contiguously at key position 16s + 8h.
         bf16x8 pf;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (bf16)S[kb][8 * s + j];
-        const int kofs = kb * 32 + 16 * s + 4 * h;
+        for (int j = 0; j < 8; ++j) pf[j] = (bf16)P[kb][8 * s + j];
+        const bf16* vcol = cv + r32 * LK + kb * 32 + 16 * s + 8 * h;
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
-          const bf16* vrow = cv + (32 * blk + r32) * LV + kofs;
-          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow);
-          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + 8);
-          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vcol + 32 * blk * LK);
           O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
         }
       }
     }
-    if (t + 1 < NT) commit(sK[(t + 1) & 1], sV[(t + 1) & 1]);
-    __syncthreads();
+  };
+
+  const int NTILE = (p.Ns + 63) / 64, NFULL = p.Ns / 64;
+  issue(0);
+  commit(sK[0], sV[0]);
+  __syncthreads();
+  // Full tiles; see the fp32 kernel for the leave-rescale-reenter structure.
+  int t = 0;
+  while (t < NFULL) {
+    float mx = 0.f;
+    for (; t < NFULL; ++t) {
+      const int cb = t & 1;
+      const bool nxt = t + 1 < NTILE;
+      if (nxt) issue((t + 1) * 64);
+      f32x16 S[2];
+      qk(sK[cb], S);
+      if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+        mx = tile_max_log2(S);
+        if (__any(mx > m2 + kRescaleThr)) break;
+      }
+      softmax_apply<ACT>(S, m2, l);
+      pv(sV[cb], S);
+      if (nxt) commit(sK[cb ^ 1], sV[cb ^ 1]);
+      __syncthreads();
+    }
+    if (t < NFULL) {
+      const float mn = fmaxf(m2, mx);
+      const float alpha = fast_exp2(m2 - mn);
+      l *= alpha;
+      scale_acc(O, alpha);
+      m2 = mn;
+    }
+  }
+  if (NFULL < NTILE) {
+    const int cb = NFULL & 1;
+    f32x16 S[2];
+    qk(sK[cb], S);
+    mask_tile<ACT>(S, NFULL * 64, p.Ns, h);
+    float alpha;
+    if (softmax_tile<ACT>(S, m2, l, alpha)) scale_acc(O, alpha);
+    pv(sV[cb], S);
   }
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
+}
+
+// Waves per workgroup (32 queries each).  Default per dtype; MHADA_ATTN_WAVES=4|8 overrides
+// (read per call, for in-process A/B measurements).
+static int attn_waves(int dtype) {
+  const char* e = getenv("MHADA_ATTN_WAVES");
+  if (e && (atoi(e) == 4 || atoi(e) == 8)) return atoi(e);
+  return 8;
+}
+
+template <int NW>
+static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s) {
+  const dim3 grid(p.nblk), blk(64 * NW);
+  if (dtype == MHADA_F32) {
+    if (activation == MHADA_ACT_SOFTMAX)
+      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX, NW>), grid, blk, 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
+  } else {
+    if (activation == MHADA_ACT_SOFTMAX)
+      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW>), grid, blk, 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
+  }
 }
 
 }  // namespace mhada
@@ -385,21 +502,15 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
   p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
   p.ldt = (Ns + 63) / 64 * 64;
-  p.nqb = (Nc + 127) / 128;
+  const int nw = attn_waves(dtype);
+  p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
   const long long nblk = (long long)B * H * p.nqb;
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn: grid too large");
   p.nblk = (int)nblk;
-  const dim3 grid(p.nblk), blk(256);
-  if (dtype == MHADA_F32) {
-    if (activation == MHADA_ACT_SOFTMAX)
-      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX>), grid, blk, 0, s, p);
-    else
-      hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE>), grid, blk, 0, s, p);
+  if (nw == 8) {
+    launch_attn<8>(p, dtype, activation, s);
   } else {
-    if (activation == MHADA_ACT_SOFTMAX)
-      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX>), grid, blk, 0, s, p);
-    else
-      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE>), grid, blk, 0, s, p);
+    launch_attn<4>(p, dtype, activation, s);
   }
   return check_launch("mhada_attn");
 }

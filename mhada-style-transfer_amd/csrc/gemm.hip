@@ -87,6 +87,10 @@ MHADA_DEV void store_chunk(TC* dst, const float (&f)[Cfg<TC>::E]) {
 
 MHADA_DEV int reflect1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
+// Internal A mode: ROWS with per-column centring (a_mu != NULL), a separate instantiation so
+// the plain ROWS path stages raw chunks with no per-element work.
+constexpr int kRowsCentred = 100;
+
 // ------------------------------------------------------------------------------------
 // A-operand staging for one K step.  Each thread owns A_CH chunks: rows (tid>>3)+32*i,
 // 16-byte column kc = tid&7.
@@ -110,19 +114,16 @@ MHADA_DEV void issue_a(AStage<TA, TC, AMODE, A_CH>& st, const GemmP& p, const TA
   constexpr int E = Cfg<TC>::E;
   const int k = k0 + kc * E;
   const bool kvalid = k < p.K;
-  if constexpr (AMODE == MHADA_A_ROWS) {
+  if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const long long m = (long long)ri[i].b;  // row index within the z problem
       st.raw[i][0] = (ri[i].valid && kvalid) ? load_raw<TA, TC>(abase + m * p.lda + k) : zero_raw<TA, TC>();
       st.wt[i][0] = 1.f;
     }
-    if (p.a_mu) {
+    if constexpr (AMODE == kRowsCentred) {
 #pragma unroll
       for (int e = 0; e < E; ++e) st.mu[e] = kvalid ? p.a_mu[k + e] : 0.f;
-    } else {
-#pragma unroll
-      for (int e = 0; e < E; ++e) st.mu[e] = 0.f;
     }
   } else if constexpr (AMODE == MHADA_A_PATCH8) {
     // k = c*64 + py*8 + px ; E | 8 so a chunk stays inside one image row
@@ -134,8 +135,6 @@ MHADA_DEV void issue_a(AStage<TA, TC, AMODE, A_CH>& st, const GemmP& p, const TA
       st.raw[i][0] = (ri[i].valid && kvalid) ? load_raw<TA, TC>(src) : zero_raw<TA, TC>();
       st.wt[i][0] = 1.f;
     }
-#pragma unroll
-    for (int e = 0; e < E; ++e) st.mu[e] = 0.f;
   } else {
     // implicit GEMM 3x3: k = tap*Cin + cin; a K step never straddles a tap (Cin % BK == 0)
     const int cin_n = p.img_c;
@@ -171,8 +170,6 @@ MHADA_DEV void issue_a(AStage<TA, TC, AMODE, A_CH>& st, const GemmP& p, const TA
         st.wt[i][0] = ly0; st.wt[i][1] = ly1; st.wt[i][2] = lx0; st.wt[i][3] = lx1;
       }
     }
-#pragma unroll
-    for (int e = 0; e < E; ++e) st.mu[e] = 0.f;
   }
 }
 
@@ -190,9 +187,13 @@ MHADA_DEV void commit_a(const AStage<TA, TC, AMODE, A_CH>& st, TC* sA, int tid) 
       for (int e = 0; e < E; ++e)
         f[e] = ly0 * (lx0 * raw_get(st.raw[i][0], e) + lx1 * raw_get(st.raw[i][1], e)) +
                ly1 * (lx0 * raw_get(st.raw[i][2], e) + lx1 * raw_get(st.raw[i][3], e));
-    } else {
+    } else if constexpr (AMODE == kRowsCentred || sizeof(TA) != sizeof(TC)) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) f[e] = raw_get(st.raw[i][0], e) - st.mu[e];
+      for (int e = 0; e < E; ++e) f[e] = raw_get(st.raw[i][0], e) - (AMODE == kRowsCentred ? st.mu[e] : 0.f);
+    } else {
+      // same type, no centring: the raw 16-byte chunk goes to LDS untouched
+      *reinterpret_cast<typename Vec16<TC>::type*>(sA + row * LS + kc * E) = st.raw[i][0].v;
+      continue;
     }
     store_chunk<TC>(sA + row * LS + kc * E, f);
   }
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
     const int m = m0 + (tid >> 3) + RS * i;
     ri[i].valid = m < p.M;
     const int mm = m < p.M ? m : 0;
-    if constexpr (AMODE == MHADA_A_ROWS) {
+    if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred) {
       ri[i].b = mm; ri[i].y = 0; ri[i].x = 0;
     } else if constexpr (AMODE == MHADA_A_PATCH8) {
       const int wt = p.out_w;
@@ -311,7 +312,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
       }
     } else {
       // fp32: lane half h supplies k = 16h + s at MFMA step s (both operands agree)
@@ -334,7 +335,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
           for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s >> 2][s & 3], bv[ni][s >> 2][s & 3],
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[ni][s >> 2][s & 3], av[mi][s >> 2][s & 3],
                                                                  acc[mi][ni], 0, 0, 0);
       }
     }
@@ -345,25 +346,62 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
     __syncthreads();
   }
 
-  // epilogue: C/D layout col = lane&31, row = (r&3) + 8(r>>2) + 4h
+  // epilogue.  The MFMAs above take W as the A operand, so each accumulator holds C^T: the
+  // lane owns ONE output row m (= lane&31 within the block) and registers 4g..4g+3 hold the 4
+  // consecutive columns 8g + 4h + 0..3 — every store below moves 4 elements (8-16 B) instead of
+  // one (a row-per-lane scalar-store tail is store-issue bound).
   TO* cbase = reinterpret_cast<TO*>(p.c) + z1 * p.sc1 + z2 * p.sc2;
   const TO* rbase = p.r ? reinterpret_cast<const TO*>(p.r) + z1 * p.sr1 + z2 * p.sr2 : nullptr;
   const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
 #pragma unroll
-  for (int ni = 0; ni < TN; ++ni) {
-    const int n = n0 + brow0 + ni * 32;
-    if (n >= p.N) continue;
-    const float bias = bbase ? bbase[n] : 0.f;
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = m0 + arow0 + mi * 32;
+    if (m >= p.M) continue;
+    TO* crow = cbase + (long long)m * p.ldc;
+    const TO* rrow = rbase ? rbase + (long long)m * p.ldr : nullptr;
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
+    for (int ni = 0; ni < TN; ++ni) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + arow0 - r32 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (m < p.M) {
-          float v = acc[mi][ni][e] + bias;
-          if (p.relu) v = fmaxf(v, 0.f);
-          if (rbase) v += to_f32<TO>(rbase[(long long)m * p.ldr + n]);
-          cbase[(long long)m * p.ldc + n] = from_f32<TO>(v);
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + brow0 - r32 + ni * 32 + 8 * g + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][4 * g + e];
+        if (n + 3 < p.N) {
+          if (bbase) {
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bbase + n);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bb[e];
+          }
+          if (p.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if constexpr (sizeof(TO) == 4) {
+            if (rrow) {
+              const f32x4 rr = *reinterpret_cast<const f32x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += rr[e];
+            }
+            *reinterpret_cast<f32x4*>(crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            if (rrow) {
+              const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += (float)rr[e];
+            }
+            *reinterpret_cast<bf16x4*>(crow + n) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e < p.N) {
+              float x = v[e] + (bbase ? bbase[n + e] : 0.f);
+              if (p.relu) x = fmaxf(x, 0.f);
+              if (rrow) x += to_f32<TO>(rrow[n + e]);
+              crow[n + e] = from_f32<TO>(x);
+            }
+          }
         }
       }
     }
@@ -392,15 +430,14 @@ static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
 // under the ~34 TB/s L2 ceiling at MFMA rate.
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
+  // N <= 64: 8 waves of 32x64 (one 256x64 tile keeps 8 waves per CU at 92 KiB of LDS)
+  if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
   if constexpr (sizeof(TC) == 4) {
-    if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
   } else {
     if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {  // 4 bilinear taps staged per chunk: keep the tile small
-      if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
       return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
     } else {
-      if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 4, 1>(p, nz, s);
       if (p.N <= 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
       return launch_gemm<TC, TA, TO, AMODE, 256, 256, 2, 4>(p, nz, s);
     }
@@ -410,7 +447,9 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
 template <typename TC, typename TA, typename TO>
 static int dispatch_mode(int mode, const GemmP& p, int nz, hipStream_t s) {
   switch (mode) {
-    case MHADA_A_ROWS: return dispatch_tile<TC, TA, TO, MHADA_A_ROWS>(p, nz, s);
+    case MHADA_A_ROWS:
+      if (p.a_mu) return dispatch_tile<TC, TA, TO, kRowsCentred>(p, nz, s);
+      return dispatch_tile<TC, TA, TO, MHADA_A_ROWS>(p, nz, s);
     case MHADA_A_CONV3X3: return dispatch_tile<TC, TA, TO, MHADA_A_CONV3X3>(p, nz, s);
     case MHADA_A_CONV3X3_UP2: return dispatch_tile<TC, TA, TO, MHADA_A_CONV3X3_UP2>(p, nz, s);
     case MHADA_A_PATCH8:
@@ -446,6 +485,13 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   if (!aligned16(a->w) || a->ldw % ec || a->sw1 % ec || a->sw2 % ec)
     return fail("mhada_gemm: W must be 16-byte aligned with aligned strides");
   if (!aligned16(a->a) || a->sa1 % ea || a->sa2 % ea) return fail("mhada_gemm: A must be 16-byte aligned");
+  // the epilogue moves 4 consecutive output columns per access
+  if (((uintptr_t)a->c & 7) || a->ldc % 4 || a->sc1 % 4 || a->sc2 % 4)
+    return fail("mhada_gemm: C must be 8-byte aligned with strides that are multiples of 4");
+  if (a->r && (((uintptr_t)a->r & 7) || a->ldr % 4 || a->sr1 % 4 || a->sr2 % 4))
+    return fail("mhada_gemm: R must be 8-byte aligned with strides that are multiples of 4");
+  if (a->bias && (!aligned16(a->bias) || a->sb1 % 4 || a->sb2 % 4))
+    return fail("mhada_gemm: bias must be 16-byte aligned with strides that are multiples of 4");
   GemmP p{};
   p.M = a->M; p.N = a->N; p.K = a->K; p.nb2 = a->nb2;
   p.a = a->a; p.lda = a->lda; p.sa1 = a->sa1; p.sa2 = a->sa2;

@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf,
 }
 
 // ---------------------------------------------------------------------------------------
-// V transpose for the bf16 attention: vt[bh][o][n] = V'[n][o], vt[bh][64+o][n] = V'[n][o]^2
+// V transpose for the bf16 attention: vt[bh][o][pos(n)] = V'[n][o], vt[bh][64+o][pos(n)] = V'[n][o]^2
 // (row stride ldt = Ns rounded up to 64, padding zero-filled).  64x64 tiles through LDS.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) transpose_v_kernel(const bf16* __restrict__ kv, bf16* __restrict__ vt,
@@ -209,10 +209,13 @@ __global__ void __launch_bounds__(256) transpose_v_kernel(const bf16* __restrict
   __syncthreads();
   bf16* dst = vt + (long long)bh * 128 * ldt + n0;
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-    const int o = i >> 6, n = i & 63;
+    const int o = i >> 6, pos = i & 63;
+    // key stored at position pos: swap bits 2 and 3 inside each group of 16 (an involution),
+    // so the 8 keys {4h..4h+3, 8+4h..8+4h+3} one MFMA lane half needs are contiguous.
+    const int n = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1);
     const float v = tile[n][o];
-    dst[(long long)o * ldt + n] = (bf16)v;
-    dst[(long long)(64 + o) * ldt + n] = (bf16)(v * v);
+    dst[(long long)o * ldt + pos] = (bf16)v;
+    dst[(long long)(64 + o) * ldt + pos] = (bf16)(v * v);
   }
 }
 

@@ -1,0 +1,118 @@
+"""Per-op microbenchmarks on the GPU (interleaved rounds in one process, median of rounds).
+
+    python tools/opbench.py [gemm|conv|attn|all]
+
+GEMM shapes are the forward path's (1024^2 batch 4 -> M = 65536 tokens); hipBLASLt via
+torch.matmul is timed beside ours on the same operands as a calibration point.
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd")]
+
+import torch
+
+from mhada_hip import ops
+
+
+def bench(fns, rounds=7, iters=10):
+    """fns: {name: callable}; returns {name: median ms per call}."""
+    times = {k: [] for k in fns}
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, f in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                f()
+            e.record()
+            torch.cuda.synchronize()
+            times[k].append(s.elapsed_time(e) / iters)
+    return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+
+
+def gemm_suite():
+    dev = "cuda"
+    for dt in (torch.bfloat16, torch.float32):
+        M = 65536 if dt == torch.bfloat16 else 32768
+        for (N, K, out, res, relu) in [(1536, 512, dt, False, False), (2048, 512, dt, False, True),
+                                       (512, 2048, torch.float32, True, False), (512, 512, torch.float32, True, False)]:
+            x = torch.randn(M, K, device=dev).to(dt)
+            w = (torch.randn(N, K, device=dev) / K ** 0.5).to(dt)
+            b = torch.randn(N, device=dev)
+            r = torch.randn(M, N, device=dev) if res else None
+            fns = {"ours": lambda: ops.linear(x, w, b, out, residual=r, relu=relu),
+                   "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
+            t = bench(fns)
+            fl = 2 * M * N * K
+            print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
+                  + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
+
+
+def conv_suite():
+    dev = "cuda"
+    for dt, B, res in ((torch.bfloat16, 4, 1024), (torch.float32, 8, 512)):
+        h = res // 8
+        for (Ci, Co, H, up) in [(512, 256, h, False), (256, 256, 2 * h, True), (256, 256, 2 * h, False),
+                                (256, 128, 2 * h, False), (128, 128, 4 * h, True), (128, 64, 4 * h, False),
+                                (64, 64, 8 * h, True)]:
+            Hin = H // 2 if up else H
+            x = torch.rand(B, Hin, Hin, Ci, device=dev).to(dt)
+            w = (torch.randn(Co, 9 * Ci, device=dev) / (9 * Ci) ** 0.5).to(dt)
+            bias = torch.randn(Co, device=dev)
+            fns = {"fused": lambda: ops.conv3x3(x, w, bias, dt, upsample=up)}
+            if up:
+                fns["sep"] = lambda: ops.conv3x3(ops.upsample2x(x), w, bias, dt, upsample=False)
+                fns["upsample_only"] = lambda: ops.upsample2x(x)
+            t = bench(fns)
+            fl = 2 * B * H * H * Co * 9 * Ci
+            print(f"conv {str(dt)[6:]:8s} {Ci:3d}->{Co:3d} @{H:4d} up={up:d}: "
+                  + "  ".join(f"{k} {v * 1e3:8.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
+
+
+def attn_suite():
+    import network
+    from mhada_hip import engine
+    from mhada_hip.recipe import load_recipe
+    dev = "cuda"
+    for dt, B, n in ((torch.bfloat16, 4, 16384), (torch.float32, 8, 4096)):
+        H = 8
+        q = torch.randn(B, H, n, 64, device=dev).to(dt)
+        kv = torch.randn(B, H, n, 128, device=dev).to(dt)
+        vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+        fcs = torch.randn(B, n, 512, device=dev)
+        mu, rs = ops.instnorm_stats(fcs)
+        vmu = torch.zeros(B, 512, device=dev)
+        def run(nw, var=""):
+            def f():
+                os.environ["MHADA_ATTN_WAVES"] = str(nw)
+                os.environ["MHADA_ATTN_VARIANT"] = var
+                ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+            return f
+        fns = {"attn_w4": run(4), "attn_w8": run(8)}
+        t = bench(fns, rounds=5, iters=3)
+        # the variants must agree
+        outs = {k: (f(), ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0))[1] for k, f in fns.items()}
+        ref = next(iter(outs.values())).float()
+        for k, o in outs.items():
+            err = ((o.float() - ref).norm() / ref.norm()).item()
+            print(f"   variant {k}: rel diff vs first {err:.2e}")
+        os.environ.pop("MHADA_ATTN_WAVES", None)
+        os.environ.pop("MHADA_ATTN_VARIANT", None)
+        fl = 6 * n * n * 512 * B
+        print(f"attn {str(dt)[6:]:8s} B={B} N={n}: " + "  ".join(f"{k} {v:7.3f} ms {fl / v / 1e9:7.1f} TF"
+                                                               for k, v in t.items()))
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    torch.manual_seed(0)
+    if what in ("gemm", "all"):
+        gemm_suite()
+    if what in ("conv", "all"):
+        conv_suite()
+    if what in ("attn", "all"):
+        attn_suite()
