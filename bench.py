@@ -45,6 +45,22 @@ def flops_per_frame(res: int, style_res: int) -> dict:
     return {"total": vit(nc) + vit(ns) + mhada + dec, "attn_per_block": 6 * nc * ns * C}
 
 
+def pmc_traffic(cfg_key):
+    """HBM bytes per mhada_attn launch from the latest committed rocprofv3 PMC pass
+    (profiles/rNN_pmc_traffic.json, produced by tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE
+    per the gfx950 corrections).  PMC counters need their own profiler run, so the bench reads
+    the measured value rather than collecting it live."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f).get(cfg_key)
+    if not d:
+        return None, None
+    return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+
+
 def build_models(dtype):
     import network
     from mhada_hip.recipe import load_recipe
@@ -101,6 +117,7 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
     avg_attn_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
     attn_flops = fl["attn_per_block"] * batch
     achieved = attn_flops / avg_attn_s / 1e12
+    traffic, tsrc = pmc_traffic(f"{res}x{res}_b{batch}_{dts}")
     return {
         "value": frames / elapsed,
         "ms_per_step": elapsed / steps * 1e3,
@@ -109,7 +126,8 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
         "tflops_whole_step": fl["total"] * batch * steps / (elapsed) / 1e12,
         "roofline": {"bound": "mfma", "kernel": "mhada_attn", "achieved": round(achieved, 2),
                      "peak": PEAK_TFLOPS[dts], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dts], 4),
-                     "traffic": None, "avg_launch_ms": round(avg_attn_s * 1e3, 4),
+                     "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
+                     "avg_launch_ms": round(avg_attn_s * 1e3, 4),
                      "flop_per_launch": attn_flops, "launches_timed": len(attn_ms)},
         "config": {"workload": f"stylize {res}x{res} content+style, batch {batch}", "resolution": res,
                    "batch_per_gpu": batch, "global_batch": batch * world, "compute_dtype": dts,

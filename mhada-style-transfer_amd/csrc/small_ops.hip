@@ -78,6 +78,61 @@ __global__ void __launch_bounds__(256) vit_batch_attn_kernel(const T* __restrict
   }
 }
 
+// Small-batch form (L <= 8, every bench/training config): each (token, head) reads q, k, v
+// once — q/k staged in LDS, v in registers — and the L x L scores are computed in parallel with
+// lane = (i, j); the softmax over j is an 8-lane group reduction.
+template <typename T>
+__global__ void __launch_bounds__(256) vit_batch_attn_small_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                   int L, int ntok, int heads) {
+  constexpr int D = 64;
+  __shared__ float sq[4][8][D + 1];
+  __shared__ float sk[4][8][D + 1];
+  __shared__ float sp[4][8][8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long pair = (long long)blockIdx.x * 4 + wv;
+  const bool valid = pair < (long long)ntok * heads;
+  const int C = heads * D;
+  const long long pp = valid ? pair : 0;
+  const int n = (int)(pp / heads), hh = (int)(pp - (long long)n * heads);
+  const long long row_stride = (long long)ntok * 3 * C;
+  const T* base = qkv + (long long)n * 3 * C + hh * D + lane;
+  float vr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < L) {
+      sq[wv][i][lane] = to_f32<T>(base[i * row_stride]) * 0.125f;  // 1/sqrt(64)
+      sk[wv][i][lane] = to_f32<T>(base[i * row_stride + C]);
+      vr[i] = to_f32<T>(base[i * row_stride + 2 * C]);
+    } else {
+      vr[i] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int i = lane >> 3, j = lane & 7;
+  float s = -INFINITY;
+  if (i < L && j < L) {
+    s = 0.f;
+#pragma unroll 16
+    for (int d = 0; d < D; ++d) s = fmaf(sq[wv][i][d], sk[wv][j][d], s);
+  }
+  float m = s;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const float e = (i < L && j < L) ? __expf(s - m) : 0.f;
+  float sum = e;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
+  sp[wv][i][j] = e / sum;
+  __syncthreads();
+  if (!valid) return;
+  for (int r = 0; r < L; ++r) {
+    float o = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o = fmaf(sp[wv][r][c], vr[c], o);
+    out[((long long)r * ntok + n) * C + hh * D + lane] = from_f32<T>(o);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // PosEmbedding resize (vit.py:91-92) to token-major [oh*ow][C]
 // ---------------------------------------------------------------------------------------
@@ -358,12 +413,20 @@ extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L
   const long long pairs = (long long)ntok * heads;
   const size_t lds = 0;
   const dim3 grid((unsigned)((pairs + 3) / 4));
-  if (dtype == MHADA_F32)
+  if (L <= 8) {
+    if (dtype == MHADA_F32)
+      hipLaunchKernelGGL((vit_batch_attn_small_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv, (float*)out,
+                         L, ntok, heads);
+    else
+      hipLaunchKernelGGL((vit_batch_attn_small_kernel<bf16>), grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out,
+                         L, ntok, heads);
+  } else if (dtype == MHADA_F32) {
     hipLaunchKernelGGL((vit_batch_attn_kernel<float>), grid, dim3(256), lds, s, (const float*)qkv, (float*)out, L,
                        ntok, heads);
-  else
+  } else {
     hipLaunchKernelGGL((vit_batch_attn_kernel<bf16>), grid, dim3(256), lds, s, (const bf16*)qkv, (bf16*)out, L,
                        ntok, heads);
+  }
   return check_launch("mhada_vit_batch_attn");
 }
 

@@ -140,7 +140,7 @@ def test_layernorm(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("L", [1, 2, 3, 8])
+@pytest.mark.parametrize("L", [1, 2, 3, 8, 11])
 def test_vit_batch_attention_matches_nn_mha(dt, L):
     N, C, heads = 300, 512, 8
     mha = torch.nn.MultiheadAttention(C, heads).to(DEV).double()
