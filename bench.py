@@ -135,6 +135,48 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
     }
 
 
+def run_train(steps, warmup, rank, world):
+    """BASELINE configs[3]: train_image.py step at 512^2, 8 images per GPU, DP over RCCL."""
+    import network
+    from mhada_hip.recipe import load_recipe, seeded_image
+    from mhada_hip.train import Trainer
+    dev = torch.device("cuda", torch.cuda.current_device())
+    vc = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c").to(dev).train()
+    vs = load_recipe(network.VisionTransformer(pos_embedding=False), "vit_s").to(dev).train()
+    ada = load_recipe(network.AdaAttnTransformerMultiHead(), "ada").to(dev).train()
+    vgg = load_recipe(network.VGG19(), "vgg").to(dev)
+    tr = Trainer(vc, vs, ada, vgg)
+    batch = 8
+    for i in range(warmup):
+        tr.step(seeded_image(batch, 512, 512, 100 + rank * 1000 + i).to(dev),
+                seeded_image(batch, 512, 512, 500 + rank * 1000 + i).to(dev))
+    data = [(seeded_image(batch, 512, 512, 100 + rank * 1000 + warmup + i).to(dev),
+             seeded_image(batch, 512, 512, 500 + rank * 1000 + warmup + i).to(dev)) for i in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for c, s in data:
+        last = tr.step(c, s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"metric": "train_image.py step throughput at 512x512, 8 images/GPU [configs[3]]",
+            "value": round(batch * steps * world / el, 3), "unit": "images/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic rand*255 images, recipe random-init weights",
+            "config": {"workload": "train step (4 ViT + 3 AdaFormer + 5 VGG19 fwd, 4 losses, bwd, Adam)",
+                       "global_batch": batch * world, "resolution": 512,
+                       "parallelism": f"dp{world} (RCCL grad all-reduce)" if world > 1 else "single GPU",
+                       "engine": "PyTorch-ROCm autograd (training v1, DESIGN.md §6)"},
+            "last_losses": last}
+
+
 def cpu_baseline(seconds_budget=30.0):
     """numpy oracle (restatement of the reference CPU path) on one 512x512 frame."""
     import numpy as np
@@ -173,6 +215,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the 1024^2 bf16 config")
     ap.add_argument("--only-secondary", action="store_true", help="run only the 1024^2 bf16 config (profiling)")
+    ap.add_argument("--train", action="store_true", help="BASELINE configs[3]: DP training step at 512^2")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,6 +225,14 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.train:
+        r = run_train(args.steps, args.warmup, rank, world)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     if args.only_secondary:
         r = run_config(1024, 4, torch.bfloat16, args.steps, args.warmup, rank, world)
         if rank == 0:

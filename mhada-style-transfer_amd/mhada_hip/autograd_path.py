@@ -1,0 +1,135 @@
+"""Differentiable forward passes for the training path (v1: PyTorch-ROCm autograd).
+
+When a forward needs gradients (``torch.is_grad_enabled()`` and a parameter or input requires
+grad — ``train_image.py:93-144``, feature-inversion scripts), the ``network`` modules route
+here instead of to the inference HIP kernels, which have no backward yet.
+Each function evaluates the reference algorithm on the module's own parameter containers
+(the same ``nn.Conv2d`` / ``nn.MultiheadAttention`` / ``nn.Linear`` / ``nn.LayerNorm`` objects
+whose state_dict keys match the reference), so autograd reaches exactly those parameters.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import torch
+import torch.nn.functional as F
+
+# decoder layers and whether bilinear x2 follows them (conv.py:78-94)
+DECODER_ORDER = (("conv1", 0, True), ("conv1", 1, False), ("conv1", 2, False), ("conv1", 3, False),
+                 ("conv1", 4, True), ("conv2", 0, False), ("conv2", 1, True), ("conv3", 0, False),
+                 ("conv3", 1, False))
+
+
+def needs_grad(module: torch.nn.Module, *xs) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    if any(isinstance(x, torch.Tensor) and x.requires_grad for x in xs):
+        return True
+    return any(p.requires_grad for p in module.parameters())
+
+
+def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
+    """VisionTransformer.forward (vit.py:148-169); the MHA keeps batch_first=False on a
+    (B, N, C) tensor, i.e. attends over the batch axis exactly as the reference."""
+    B, _, H, W = x.shape
+    p = vit.patch_size
+    h, w = H // p, W // p
+    t = vit.patch_embedding.conv_proj(x)
+    C = t.shape[1]
+    t = t.reshape(B, C, h * w).permute(0, 2, 1)
+    if vit.pos_embedding is not None:
+        pe = vit.pos_embedding.pos_embed
+        if (h, w) != tuple(pe.shape[2:]):
+            pe = F.interpolate(pe, size=(h, w), mode="bilinear", align_corners=False)
+        t = t + pe.expand(B, -1, -1, -1).reshape(B, C, h * w).permute(0, 2, 1)
+    outs = []
+    for blk in vit.encoder:
+        y = blk.ln1(t)
+        y, _ = blk.attention(y, y, y, need_weights=False)
+        t = y + t
+        t = t + blk.mlp(blk.ln2(t))
+        outs.append(t.permute(0, 2, 1).reshape(B, C, h, w))
+    return outs
+
+
+def _softmax_or_cosine(q, k, activation: str):
+    if activation == "softmax":
+        return torch.softmax(torch.bmm(q, k), dim=-1)  # adaDecoder.py:16-17, no 1/sqrt(d)
+    s = torch.bmm(q, k) / torch.bmm(q.norm(dim=-1, keepdim=True), k.norm(dim=1, keepdim=True)) + 1
+    return s / s.sum(dim=-1, keepdim=True)  # adaDecoder.py:24-34
+
+
+def block_forward(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206)."""
+    B, _, h, w = fc.shape
+    d = blk.head_dim
+    outs = []
+    for i in range(blk.num_heads):
+        sl = slice(i * d, (i + 1) * d)
+        q = blk.f_list[i](F.instance_norm(fc[:, sl])).reshape(B, d, h * w).permute(0, 2, 1)
+        k = blk.g_list[i](F.instance_norm(fs[:, sl]))
+        k = k.reshape(B, d, -1)
+        v = blk.h_list[i](fs[:, sl]).reshape(B, d, -1).permute(0, 2, 1)
+        a = _softmax_or_cosine(q, k, blk.activation_name)
+        m = torch.bmm(a, v)
+        s = torch.sqrt((torch.bmm(a, v * v) - m * m).clamp(min=1e-6))
+        m = m.reshape(B, h, w, d).permute(0, 3, 1, 2)
+        s = s.reshape(B, h, w, d).permute(0, 3, 1, 2)
+        outs.append(s * F.instance_norm(fcs[:, sl]) + m)
+    return blk.out_conv(torch.cat(outs, dim=1))
+
+
+def decoder_forward(dec, x: torch.Tensor) -> torch.Tensor:
+    """Decoder.forward (conv.py:96-100)."""
+    for seq, idx, up in DECODER_ORDER:
+        conv = getattr(dec, seq)[idx].conv.conv
+        x = F.relu(conv(F.pad(x, (1, 1, 1, 1), mode="reflect")))
+        if up:
+            x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    return x
+
+
+def adaformer_forward(ada, fc: Sequence[torch.Tensor], fs: Sequence[torch.Tensor]):
+    """AdaAttnTransformerMultiHead.forward (adaDecoder.py:253-268)."""
+    fcs = fc[0]
+    for i in range(ada.num_layers):
+        fcs = block_forward(ada.adaAttnHead[2 * i], fc[i], fs[i], fcs)
+        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fs[i], fcs)
+    return fcs, decoder_forward(ada.decoder, fcs)
+
+
+def imagenet_normalize(x: torch.Tensor) -> torch.Tensor:
+    """imageNet1k_normalize (vgg19.py:6-12)."""
+    x = x.float()
+    mean = x.new_tensor([0.485, 0.456, 0.406]).view(-1, 1, 1)
+    std = x.new_tensor([0.229, 0.224, 0.225]).view(-1, 1, 1)
+    return (x / 255.0 - mean) / std
+
+
+def vgg19_forward(vgg, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """VGG19.forward (vgg19.py:42-70): relu1_1 .. relu5_1."""
+    x = imagenet_normalize(x)
+    feats = {}
+    for i in range(1, 6):
+        x = getattr(vgg, f"slice{i}")(x)
+        feats[f"relu{i}_1"] = x
+    return feats
+
+
+def ada_attn_for_loss(c_x, s_x, c_1x, s_1x, activation: str = "softmax", chunk: int = 4096) -> torch.Tensor:
+    """AdaAttnForLoss.forward (adaDecoder.py:52-81), query-chunked so the Nc x Ns attention
+    matrix is never whole (relu3_1 at 512^2 is 16384 x 16384 per image)."""
+    b, _, h, w = c_1x.shape
+    q = F.instance_norm(c_1x).reshape(b, -1, h * w).permute(0, 2, 1)
+    k = F.instance_norm(s_1x).reshape(b, s_1x.shape[1], -1)
+    v = s_x.reshape(b, s_x.shape[1], -1).permute(0, 2, 1)
+    ms, ss = [], []
+    for q0 in range(0, q.shape[1], chunk):
+        a = _softmax_or_cosine(q[:, q0:q0 + chunk], k, activation)
+        m = torch.bmm(a, v)
+        ms.append(m)
+        ss.append(torch.sqrt((torch.bmm(a, v * v) - m * m).clamp(min=1e-6)))
+    bc, _, hc, wc = c_x.shape
+    m = torch.cat(ms, 1).reshape(bc, hc, wc, -1).permute(0, 3, 1, 2)
+    s = torch.cat(ss, 1).reshape(bc, hc, wc, -1).permute(0, 3, 1, 2)
+    return s * F.instance_norm(c_x) + m

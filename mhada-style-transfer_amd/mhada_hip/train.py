@@ -1,0 +1,108 @@
+"""One training iteration of ``train_image.py:93-144`` on the drop-in modules, optionally data
+parallel (one process per GPU, gradient all-reduce over RCCL — mhada_hip.parallel).
+
+    trainer = Trainer(vit_c, vit_s, ada, vgg)            # 3 Adam optimisers, lr 1e-4
+    losses = trainer.step(content, style)               # dict of the 4 weighted losses + total
+
+The step: 4 ViT forwards, 3 AdaFormer forwards, 5 VGG19 forwards, global-style / local-feature
+/ identity losses weighted 70 / 15 / 0.05 / 0.1, backward, (all-reduce), 3 Adam steps.
+Checkpoints use the reference's dict layout (train_image.py:172-186).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import losses as L
+
+LAMBDA_GS, LAMBDA_LF, LAMBDA_ID1, LAMBDA_ID2 = 70.0, 15.0, 5e-2, 1e-1  # train_image.py:19-22
+
+
+class Trainer:
+    def __init__(self, vit_c: nn.Module, vit_s: nn.Module, ada: nn.Module, vgg: nn.Module, lr: float = 1e-4,
+                 activation: str = "softmax", distributed: Optional[bool] = None, bucket_mb: int = 25):
+        import network
+        self.vit_c, self.vit_s, self.ada, self.vgg = vit_c, vit_s, ada, vgg
+        dev = next(vit_c.parameters()).device
+        self.no_learn = nn.ModuleList([  # train_image.py:52-58
+            network.AdaAttnForLoss(256, 64 + 128 + 256, activation),
+            network.AdaAttnForLoss(512, 64 + 128 + 256 + 512, activation),
+            network.AdaAttnForLoss(512, 64 + 128 + 256 + 512 + 512, activation),
+        ]).to(dev).eval()
+        self.vgg.eval()
+        for p in self.vgg.parameters():
+            p.requires_grad_(False)
+        self.mse = nn.MSELoss(reduction="mean")
+        self.opt_vit_c = torch.optim.Adam(vit_c.parameters(), lr=lr)
+        self.opt_vit_s = torch.optim.Adam(vit_s.parameters(), lr=lr)
+        self.opt_ada = torch.optim.Adam(ada.parameters(), lr=lr)
+        if distributed is None:
+            distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.reducer = None
+        if distributed:
+            from .parallel import GradAllReducer
+            params = list(vit_c.parameters()) + list(vit_s.parameters()) + list(ada.parameters())
+            self.reducer = GradAllReducer(params, bucket_bytes=bucket_mb << 20)
+
+    def losses(self, content: torch.Tensor, style: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Forward + weighted losses (train_image.py:103-136)."""
+        fc_vc = self.vit_c(content)
+        fs_vs = self.vit_s(style)
+        _, cs = self.ada(fc_vc, fs_vs)
+        fc_vs = self.vit_s(content)
+        fs_vc = self.vit_c(style)
+        _, cc = self.ada(fc_vc, fc_vs)
+        _, ss = self.ada(fs_vc, fs_vs)
+        vgg_fs = self.vgg(style)
+        vgg_fc = self.vgg(content)
+        vgg_fcs = self.vgg(cs)
+        vgg_fcc = self.vgg(cc)
+        vgg_fss = self.vgg(ss)
+        gs = L.global_style_loss(vgg_fcs, vgg_fs, self.mse) * LAMBDA_GS
+        lf = L.local_feature_loss(vgg_fc, vgg_fs, vgg_fcs, self.no_learn, self.mse) * LAMBDA_LF
+        id1 = L.identity_loss_1(cc, content, ss, style, self.mse) * LAMBDA_ID1
+        id2 = L.identity_loss_2(vgg_fcc, vgg_fc, vgg_fss, vgg_fs, self.mse) * LAMBDA_ID2
+        return {"loss_gs": gs, "loss_lf": lf, "loss_id1": id1, "loss_id2": id2, "loss": gs + lf + id1 + id2}
+
+    def zero_grad(self) -> None:
+        for o in (self.opt_vit_c, self.opt_vit_s, self.opt_ada):
+            o.zero_grad()
+
+    def backward(self, content: torch.Tensor, style: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """zero_grad + forward + backward + (all-reduce); no optimizer step."""
+        self.zero_grad()
+        out = self.losses(content, style)
+        out["loss"].backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        return out
+
+    def step(self, content: torch.Tensor, style: torch.Tensor) -> Dict[str, float]:
+        out = self.backward(content, style)
+        self.opt_vit_c.step()
+        self.opt_vit_s.step()
+        self.opt_ada.step()
+        return {k: float(v.detach()) for k, v in out.items()}
+
+    def checkpoint(self, epoch: int, batch_size: int) -> dict:
+        """The reference's checkpoint dict (train_image.py:172-186)."""
+        return {
+            "epoch": epoch,
+            "batch_size": batch_size,
+            "model_state": {"adaFormer": self.ada.state_dict(), "vit_c": self.vit_c.state_dict(),
+                            "vit_s": self.vit_s.state_dict()},
+            "optim_state": {"adaFormer": self.opt_ada.state_dict(), "vit_c": self.opt_vit_c.state_dict(),
+                            "vit_s": self.opt_vit_s.state_dict()},
+        }
+
+    def load_checkpoint(self, ckpt: dict) -> None:
+        """Resume (train_image.py:75-84)."""
+        self.ada.load_state_dict(ckpt["model_state"]["adaFormer"])
+        self.vit_c.load_state_dict(ckpt["model_state"]["vit_c"])
+        self.vit_s.load_state_dict(ckpt["model_state"]["vit_s"])
+        self.opt_ada.load_state_dict(ckpt["optim_state"]["adaFormer"])
+        self.opt_vit_c.load_state_dict(ckpt["optim_state"]["vit_c"])
+        self.opt_vit_s.load_state_dict(ckpt["optim_state"]["vit_s"])

@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 
 from . import _path  # noqa: F401
-from mhada_hip import engine
+from mhada_hip import autograd_path, engine
 from .conv import Decoder
 
 ACTIVATIONS = ("softmax", "cosine")
@@ -26,7 +26,8 @@ def _check_activation(activation: str) -> str:
 
 class AdaAttnForLoss(nn.Module):
     """Parameter-free AdaAttN used as the local-feature-loss target (``adaDecoder.py:38-81``).
-    Constructor parity only in this round: its forward belongs to the training path."""
+    Training-path component: evaluated with PyTorch-ROCm ops, query-chunked (its head width is
+    qk_dim = 448..1472, not the 64 of the fused MHAda kernel)."""
 
     def __init__(self, v_dim, qk_dim, activation="softmax"):
         super().__init__()
@@ -34,8 +35,7 @@ class AdaAttnForLoss(nn.Module):
         self.activation_name = _check_activation(activation)
 
     def forward(self, c_x, s_x, c_1x, s_1x):
-        raise NotImplementedError("AdaAttnForLoss (training-path loss target) is not on the HIP path yet; "
-                                  "see DESIGN.md §scope")
+        return autograd_path.ada_attn_for_loss(c_x, s_x, c_1x, s_1x, self.activation_name)
 
 
 class AdaAttnMultiHead(nn.Module):
@@ -55,6 +55,8 @@ class AdaAttnMultiHead(nn.Module):
         self.activation_name = _check_activation(activation)
 
     def forward(self, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
+        if autograd_path.needs_grad(self, fc, fs, fcs):
+            return autograd_path.block_forward(self, fc, fs, fcs)
         engine.require_device(fc, "AdaAttnMultiHead")
         dt = engine.resolve_compute_dtype(self)
         fcf = engine._Feat.from_nchw(fc)
@@ -84,4 +86,6 @@ class AdaAttnTransformerMultiHead(nn.Module):
             fc, fs = args
         fc: List[torch.Tensor] = list(fc)
         fs: List[torch.Tensor] = list(fs)
+        if autograd_path.needs_grad(self, *fc, *fs):
+            return autograd_path.adaformer_forward(self, fc, fs)
         return engine.adaformer_forward(self, fc, fs)

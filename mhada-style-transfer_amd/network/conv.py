@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from . import _path  # noqa: F401
-from mhada_hip import engine
+from mhada_hip import autograd_path, engine
 
 
 class Conv(nn.Module):
@@ -59,6 +59,8 @@ class Decoder(nn.Module):
         )
 
     def forward(self, fcs: torch.Tensor) -> torch.Tensor:
+        if autograd_path.needs_grad(self, fcs):
+            return autograd_path.decoder_forward(self, fcs)
         engine.require_device(fcs, "Decoder")
         dt = engine.resolve_compute_dtype(self)
         return engine.decoder_forward_tokens(self, engine.to_tokens(fcs), dt)

@@ -1,11 +1,14 @@
-"""Frozen VGG19 loss network — constructor/state_dict parity with ``MHAdaSTr/network/vgg19.py:15-70``.
+"""Frozen VGG19 loss network — drop-in for ``MHAdaSTr/network/vgg19.py:15-70``.
 
 The reference pulls ImageNet weights from torchvision at construction (a network fetch this
 environment cannot make); here the layers are built with the same indices so a locally
-saved ``slice{1..5}.{idx}.{weight,bias}`` state_dict loads strictly.  Its forward belongs to
-the training path, which is not on the HIP path in this round.
+saved ``slice{1..5}.{idx}.{weight,bias}`` state_dict loads strictly.  Forward = the training
+path's loss features (PyTorch-ROCm ops; gradients flow to the input image).
 """
 import torch.nn as nn
+
+from . import _path  # noqa: F401
+from mhada_hip import autograd_path
 
 # torchvision vgg19 cfg "E" features[0:30]: (index, in, out) of each 3x3 conv; ReLU follows
 # each conv, MaxPool2d(2) at 4, 9, 18, 27.
@@ -34,5 +37,4 @@ class VGG19(nn.Module):
             p.requires_grad = False
 
     def forward(self, x):
-        raise NotImplementedError("VGG19 loss features (training path) are not on the HIP path yet; "
-                                  "see DESIGN.md §scope")
+        return autograd_path.vgg19_forward(self, x)

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import _path  # noqa: F401
-from mhada_hip import engine
+from mhada_hip import autograd_path, engine
 
 
 class PosEmbedding(nn.Module):
@@ -61,4 +61,6 @@ class VisionTransformer(nn.Module):
             [EncoderBlock(num_heads=num_heads, hidden_dim=hidden_dim, mlp_dim=mlp_dim) for _ in range(num_layers)])
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
+        if autograd_path.needs_grad(self, x):  # training / feature inversion: autograd v1
+            return autograd_path.vit_forward(self, x)
         return engine.vit_forward(self, x)

@@ -277,3 +277,122 @@ def to_numpy_params(sd, dtype=np.float32) -> Params:
         arr = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
         out[k] = arr.astype(dtype)
     return out
+
+
+# --------------------------------------------------------------------------------------
+# training-path forward pieces (network/vgg19.py, adaDecoder.py:38-81, utilities.py, lossfn.py)
+# --------------------------------------------------------------------------------------
+VGG_SLICES = ((0, 2), (2, 7), (7, 12), (12, 21), (21, 30))  # relu1_1 .. relu5_1 (vgg19.py:26-44)
+VGG_POOLS = (4, 9, 18, 27)
+
+
+def imagenet_normalize(x: np.ndarray) -> np.ndarray:
+    """``imageNet1k_normalize`` (``network/vgg19.py:6-12``): x/255 then ImageNet mean/std."""
+    mean = np.array([0.485, 0.456, 0.406], dtype=x.dtype).reshape(1, 3, 1, 1)
+    std = np.array([0.229, 0.224, 0.225], dtype=x.dtype).reshape(1, 3, 1, 1)
+    return (x / x.dtype.type(255.0) - mean) / std
+
+
+def maxpool2(x: np.ndarray) -> np.ndarray:
+    n, c, h, w = x.shape
+    return x[:, :, : h // 2 * 2, : w // 2 * 2].reshape(n, c, h // 2, 2, w // 2, 2).max(axis=(3, 5))
+
+
+def vgg19_forward(x: np.ndarray, p: Params) -> Dict[str, np.ndarray]:
+    """``VGG19.forward`` (``network/vgg19.py:42-70``): torchvision VGG19 features[0:30]
+    (3x3 zero-pad convs + ReLU, MaxPool 2x2) returning relu1_1..relu5_1."""
+    x = imagenet_normalize(x)
+    feats = {}
+    for s, (a, b) in enumerate(VGG_SLICES, start=1):
+        for idx in range(a, b):
+            key = f"slice{s}.{idx}.weight"
+            if key in p:
+                x = conv2d(x, p[key], p[f"slice{s}.{idx}.bias"], "zeros")
+            elif idx in VGG_POOLS:
+                x = maxpool2(x)
+            else:
+                x = np.maximum(x, 0)
+        feats[f"relu{s}_1"] = x
+    return feats
+
+
+def feature_down_sample(feat: Dict[str, np.ndarray], last_layer: int) -> np.ndarray:
+    """``utilities.feature_down_sample`` (``utilities.py:86-97``): bilinear resize of relu1..
+    relu(last-1) to relu(last)'s size, concatenated on channels."""
+    h, w = feat[f"relu{last_layer}_1"].shape[-2:]
+    parts = [interp_bilinear(feat[f"relu{i}_1"], h, w) for i in range(1, last_layer)]
+    parts.append(feat[f"relu{last_layer}_1"])
+    return np.concatenate(parts, axis=1)
+
+
+def ada_attn_for_loss(c_x, s_x, c_1x, s_1x, activation: str = "softmax") -> np.ndarray:
+    """``AdaAttnForLoss.forward`` (``network/adaDecoder.py:52-81``): parameter-free AdaAttN."""
+    act = {"softmax": activation_softmax, "cosine": activation_cosine}[activation]
+    b, _, h, w = c_1x.shape
+    q = instance_norm(c_1x).reshape(b, -1, h * w).transpose(0, 2, 1)
+    _, _, hs, ws = s_1x.shape
+    k = instance_norm(s_1x).reshape(b, -1, hs * ws)
+    v = s_x.reshape(b, s_x.shape[1], -1).transpose(0, 2, 1)
+    a = act(q, k)
+    m = a @ v
+    s = np.sqrt(np.maximum(a @ (v ** 2) - m ** 2, 1e-6))
+    bc, _, hc, wc = c_x.shape
+    m = m.reshape(bc, hc, wc, -1).transpose(0, 3, 1, 2)
+    s = s.reshape(bc, hc, wc, -1).transpose(0, 3, 1, 2)
+    return s * instance_norm(c_x) + m
+
+
+def _mse(a, b):
+    return float(((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2).mean())
+
+
+def global_style_loss(fcs, fs) -> float:
+    """``lossfn.py:7-23``: MSE of per-channel means and UNBIASED stds over relu1_1..relu5_1."""
+    loss = 0.0
+    for i in range(1, 6):
+        a, b = fcs[f"relu{i}_1"], fs[f"relu{i}_1"]
+        loss += _mse(a.mean(axis=(2, 3)), b.mean(axis=(2, 3)))
+        loss += _mse(a.std(axis=(2, 3), ddof=1), b.std(axis=(2, 3), ddof=1))
+    return loss
+
+
+def local_feature_loss(fc, fs, fcs, activation: str = "softmax") -> float:
+    """``lossfn.py:26-34`` with AdaAttnForLoss targets at relu3/4/5 (train_image.py:52-58)."""
+    loss = 0.0
+    for i in (3, 4, 5):
+        target = ada_attn_for_loss(fc[f"relu{i}_1"], fs[f"relu{i}_1"], feature_down_sample(fc, i),
+                                   feature_down_sample(fs, i), activation)
+        loss += _mse(fcs[f"relu{i}_1"], target)
+    return loss
+
+
+def identity_loss_1(cc, c, ss, s) -> float:
+    """``lossfn.py:37-38``"""
+    return _mse(cc, c) + _mse(ss, s)
+
+
+def identity_loss_2(fcc, fc, fss, fs) -> float:
+    """``lossfn.py:41-47``"""
+    return sum(_mse(fcc[f"relu{i}_1"], fc[f"relu{i}_1"]) + _mse(fss[f"relu{i}_1"], fs[f"relu{i}_1"])
+               for i in range(1, 6))
+
+
+LAMBDA = {"gs": 70.0, "lf": 15.0, "id1": 5e-2, "id2": 1e-1}  # train_image.py:19-22
+
+
+def train_losses(content, style, p_vc, p_vs, p_ada, p_vgg):
+    """Forward + weighted losses of one ``train_image.py:103-136`` step.  Returns
+    [loss_gs, loss_lf, loss_id1, loss_id2, loss]."""
+    fc_vc = vit_forward(content, p_vc)
+    fs_vs = vit_forward(style, p_vs)
+    _, cs = adaformer_forward(fc_vc, fs_vs, p_ada)
+    fc_vs = vit_forward(content, p_vs)
+    fs_vc = vit_forward(style, p_vc)
+    _, cc = adaformer_forward(fc_vc, fc_vs, p_ada)
+    _, ss = adaformer_forward(fs_vc, fs_vs, p_ada)
+    v = {k: vgg19_forward(x, p_vgg) for k, x in (("s", style), ("c", content), ("cs", cs), ("cc", cc), ("ss", ss))}
+    gs = global_style_loss(v["cs"], v["s"]) * LAMBDA["gs"]
+    lf = local_feature_loss(v["c"], v["s"], v["cs"]) * LAMBDA["lf"]
+    i1 = identity_loss_1(cc, content, ss, style) * LAMBDA["id1"]
+    i2 = identity_loss_2(v["cc"], v["c"], v["ss"], v["s"]) * LAMBDA["id2"]
+    return [gs, lf, i1, i2, gs + lf + i1 + i2]

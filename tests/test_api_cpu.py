@@ -52,12 +52,13 @@ def test_constructor_errors_mirror_reference():
 
 
 def test_forward_refuses_cpu_tensors():
+    """Inference (no autograd) runs only on the HIP kernels: no CPU fallback."""
     vit = network.VisionTransformer()
-    with pytest.raises(RuntimeError, match="ROCm device"):
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
         vit(torch.rand(1, 3, 64, 64) * 255)
     ada = network.AdaAttnTransformerMultiHead()
     f = [torch.rand(1, 512, 8, 8)] * 3
-    with pytest.raises(RuntimeError, match="ROCm device"):
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
         ada(f, f)
 
 

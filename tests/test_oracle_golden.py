@@ -123,3 +123,25 @@ def test_oracle_interp_matches_torch():
     ref = torch.nn.functional.interpolate(torch.from_numpy(x), scale_factor=2, mode="bilinear",
                                           align_corners=False).numpy()
     np.testing.assert_allclose(O.interp_bilinear(x, 10, 14, 0.5, 0.5), ref, rtol=1e-5, atol=1e-6)
+
+
+def _vgg_shapes():
+    import network
+    return {k: tuple(v.shape) for k, v in network.VGG19().state_dict().items()}
+
+
+def test_oracle_training_losses_match_reference():
+    """Forward half of one train_image.py step (ViTs, AdaFormer x3, VGG19 x5, 4 losses)."""
+    g = load_golden("train_64_b2")
+    c = seeded_image(2, 64, 64, int(g["content_seed"])).numpy()
+    s = seeded_image(2, 64, 64, int(g["style_seed"])).numpy()
+    p = [params("vit_c", _vit_shapes(True)), params("vit_s", _vit_shapes(False)), params("ada", _ada_shapes()),
+         params("vgg", _vgg_shapes())]
+    losses = O.train_losses(c, s, *p)
+    np.testing.assert_allclose(losses, g["losses"], rtol=2e-4)
+    fc = O.vgg19_forward(c, p[3])
+    np.testing.assert_allclose(fc["relu3_1"], g["vgg_fc_relu3_1"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(fc["relu5_1"], g["vgg_fc_relu5_1"], rtol=1e-4, atol=1e-5)
+    fs = O.vgg19_forward(s, p[3])
+    t4 = O.ada_attn_for_loss(fc["relu4_1"], fs["relu4_1"], O.feature_down_sample(fc, 4), O.feature_down_sample(fs, 4))
+    np.testing.assert_allclose(t4, g["lf_target4"], rtol=1e-4, atol=1e-4)

@@ -1,0 +1,101 @@
+"""Training path (e) on CPU: one train_image.py step against the reference's
+golden losses/gradients, and the data-parallel gradient all-reduce with 2 gloo ranks."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import network
+from conftest import load_golden
+from mhada_hip.recipe import load_recipe, seeded_image
+from mhada_hip.train import Trainer
+
+
+def build(device="cpu"):
+    torch.manual_seed(0)
+    vc = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c").to(device).train()
+    vs = load_recipe(network.VisionTransformer(pos_embedding=False), "vit_s").to(device).train()
+    ada = load_recipe(network.AdaAttnTransformerMultiHead(), "ada").to(device).train()
+    vgg = load_recipe(network.VGG19(), "vgg").to(device)
+    return vc, vs, ada, vgg
+
+
+def grad_summary(m):
+    return np.array([float(p.grad.double().norm()) if p.grad is not None else 0.0
+                     for _, p in sorted(m.named_parameters())])
+
+
+def check_against_golden(tr, device):
+    g = load_golden("train_64_b2")
+    c = seeded_image(2, 64, 64, int(g["content_seed"])).to(device)
+    s = seeded_image(2, 64, 64, int(g["style_seed"])).to(device)
+    out = tr.backward(c, s)
+    got = np.array([float(out[k].detach()) for k in ("loss_gs", "loss_lf", "loss_id1", "loss_id2", "loss")])
+    np.testing.assert_allclose(got, g["losses"], rtol=2e-4)
+    for name, m in (("vit_c", tr.vit_c), ("vit_s", tr.vit_s), ("ada", tr.ada)):
+        ref = g[f"grad_{name}"]  # tiny norms (<1e-4 of the largest) are rounding noise
+        np.testing.assert_allclose(grad_summary(m), ref, rtol=2e-3, atol=1e-5 * ref.max())
+    np.testing.assert_allclose(tr.ada.decoder.conv3[1].conv.conv.weight.grad.cpu().numpy(),
+                               g["grad_ada_last_conv_w"], rtol=2e-3, atol=1e-3)
+
+
+def test_train_step_matches_reference_golden():
+    torch.set_num_threads(8)
+    check_against_golden(Trainer(*build()), "cpu")
+
+
+def test_checkpoint_dict_roundtrip(tmp_path):
+    tr = Trainer(*build())
+    ck = tr.checkpoint(epoch=1, batch_size=8)
+    assert set(ck) == {"epoch", "batch_size", "model_state", "optim_state"}
+    torch.save(ck, tmp_path / "checkpoint_epoch_1_batchSize_8.pth")
+    ck2 = torch.load(tmp_path / "checkpoint_epoch_1_batchSize_8.pth", weights_only=True)
+    tr2 = Trainer(*build())
+    tr2.load_checkpoint(ck2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _dp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = Trainer(*build(), distributed=True, bucket_mb=4)  # several buckets
+    c = seeded_image(1, 64, 64, 200 + rank)
+    s = seeded_image(1, 64, 64, 300 + rank)
+    tr.backward(c, s)
+    if rank == 0:
+        grads = {n: p.grad.clone() for n, p in tr.ada.named_parameters()}
+        grads.update({"vit_c." + n: p.grad.clone() for n, p in tr.vit_c.named_parameters()})
+        torch.save(grads, os.path.join(out_dir, "dp_grads.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_allreduce_equals_accumulation(tmp_path):
+    """2 gloo ranks, one image each == single process averaging the two micro-batch gradients."""
+    world = 2
+    mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    dp = torch.load(tmp_path / "dp_grads.pt", weights_only=True)
+    torch.set_num_threads(2)  # same intra-op split as the workers: same summation order
+    tr = Trainer(*build(), distributed=False)
+    acc = {}
+    for r in range(world):
+        tr.backward(seeded_image(1, 64, 64, 200 + r), seeded_image(1, 64, 64, 300 + r))
+        named = dict(("vit_c." + n, p) for n, p in tr.vit_c.named_parameters())
+        named.update(dict(tr.ada.named_parameters()))
+        for n, p in named.items():
+            acc[n] = acc.get(n, 0) + p.grad / world
+    torch.set_num_threads(8)
+    for n, g in acc.items():
+        torch.testing.assert_close(dp[n], g, rtol=1e-4, atol=1e-5 * float(g.abs().max()))
