@@ -116,7 +116,8 @@ int mhada_fold_block(const float* wf, const float* wg, const float* wh, const fl
 int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t stream);
 
 /* L2-normalise the 64-wide rows of q [B][H][Nc][64] and the K half of kv [B][H][Ns][128]
- * in place (CosineSimilarity, adaDecoder.py:30-32). */
+ * in place (CosineSimilarity, adaDecoder.py:30-32).  Nc == 0 (q may be NULL) or Ns == 0 (kv
+ * may be NULL) normalises one side only (a cached style's K once, each frame's Q per call). */
 int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns,
                       mhada_stream_t stream);
 

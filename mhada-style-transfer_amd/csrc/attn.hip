@@ -16,8 +16,8 @@
 //       operand with no lane movement; the dv/key index pairing follows the accumulator's
 //       row permutation.
 // Online softmax with a deferred rescale (cdna_hip_programming.md T13): the running max m
-// only moves when a tile's max exceeds it by more than 2^8 (log2 units), so after the first
-// tiles the O accumulators are never touched by VALU (no AGPR<->VGPR traffic); P <= 2^8.
+// only moves when a tile's max exceeds it by more than kRescaleThr (log2 units), so after the
+// first tiles the O accumulators are touched by VALU only in a rare branch; P <= 2^kRescaleThr.
 // Only the last, partial key tile runs the masking code.
 // fp32: v_mfma_f32_32x32x2_f32 (exact fp32), K/V' streamed from kv[.][128] into LDS, V'^2
 //       formed in registers.  bf16: v_mfma_f32_32x32x16_bf16, V'^T and V'^2^T streamed from
@@ -89,10 +89,10 @@ MHADA_DEV void attn_epilogue(const AttnP& p, const f32x16 (&O)[4], float l, int 
 }
 
 // Scores of keys >= Ns: -inf (softmax) / -1 (cosine: p = s + 1 = 0).
-template <int ACT>
-MHADA_DEV void mask_tile(f32x16 (&S)[2], int key0, int Ns, int h) {
+template <int ACT, int NKB>
+MHADA_DEV void mask_tile(f32x16 (&S)[NKB], int key0, int Ns, int h) {
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -102,13 +102,13 @@ MHADA_DEV void mask_tile(f32x16 (&S)[2], int key0, int Ns, int h) {
 
 // Online-softmax update of one tile: S becomes P (in place); returns true (wave-uniform)
 // when the O accumulators must be multiplied by `alpha`.  m2 is the running max in log2 units.
-template <int ACT>
-MHADA_DEV bool softmax_tile(f32x16 (&S)[2], float& m2, float& l, float& alpha) {
+template <int ACT, int NKB>
+MHADA_DEV bool softmax_tile(f32x16 (&S)[NKB], float& m2, float& l, float& alpha) {
   float sum = 0.f;
   if constexpr (ACT == MHADA_ACT_SOFTMAX) {
     float mx = S[0][0];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[kb][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * kLog2e;
@@ -121,7 +121,7 @@ MHADA_DEV bool softmax_tile(f32x16 (&S)[2], float& m2, float& l, float& alpha) {
       m2 = mn;
     }
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float pv = fast_exp2(fmaf(S[kb][r], kLog2e, -m2));
@@ -132,7 +132,7 @@ MHADA_DEV bool softmax_tile(f32x16 (&S)[2], float& m2, float& l, float& alpha) {
     return resc;
   } else {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float pv = S[kb][r] + 1.0f;
@@ -146,21 +146,22 @@ MHADA_DEV bool softmax_tile(f32x16 (&S)[2], float& m2, float& l, float& alpha) {
 }
 
 // Tile max of the scores in log2 units, combined over the two lane halves (same query).
-MHADA_DEV float tile_max_log2(const f32x16 (&S)[2]) {
+template <int NKB>
+MHADA_DEV float tile_max_log2(const f32x16 (&S)[NKB]) {
   float mx = S[0][0];
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[kb][r]);
   return fmaxf(mx, __shfl_xor(mx, 32, 64)) * kLog2e;
 }
 
 // S -> P against the current running max (no rescale); accumulates the row sum.
-template <int ACT>
-MHADA_DEV void softmax_apply(f32x16 (&S)[2], float m2, float& l) {
+template <int ACT, int NKB>
+MHADA_DEV void softmax_apply(f32x16 (&S)[NKB], float m2, float& l) {
   float sum = 0.f;
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float pv = (ACT == MHADA_ACT_SOFTMAX) ? fast_exp2(fmaf(S[kb][r], kLog2e, -m2)) : S[kb][r] + 1.0f;
@@ -189,7 +190,7 @@ MHADA_DEV void decode_block(const AttnP& p, int& b, int& hh, int& qb) {
 // fp32 variant
 // ======================================================================================
 template <int ACT, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_f32_kernel(const AttnP p) {
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(const AttnP p) {
   constexpr int NT = 64 * NW;
   constexpr int LS = 132;  // LDS row (128 + 4 floats): conflict-free b128 K reads, b32 V reads
   constexpr int CH = 2048 / NT;  // 16-B chunks per thread per tile (64 keys x 128 floats)
@@ -273,42 +274,38 @@ __global__ void __launch_bounds__(64 * NW) attn_f32_kernel(const AttnP p) {
   issue(0);
   commit(sKV[0]);
   __syncthreads();
-  // Full tiles.  The hot loop never touches O outside the MFMAs: when a tile's max would
-  // push P past 2^kRescaleThr (always on the first tile) the wave leaves the loop, rescales
-  // O once and re-enters at the same tile (its K/V are still resident).
-  int t = 0;
-  while (t < NFULL) {
-    float mx = 0.f;
-    for (; t < NFULL; ++t) {
-      const float* cur = sKV[t & 1];
-      const bool nxt = t + 1 < NTILE;
-      if (nxt) issue((t + 1) * 64);
-      f32x16 S[2];
-      qk(cur, S);
-      if constexpr (ACT == MHADA_ACT_SOFTMAX) {
-        mx = tile_max_log2(S);
-        if (__any(mx > m2 + kRescaleThr)) break;
+  // Full tiles.  The rescale (P <= 2^kRescaleThr, so after the first tile it is rare) is a
+  // wave-uniform branch inside the single loop: one register assignment for the O accumulators
+  // (a leave-rescale-reenter loop made the compiler copy all of O between two register sets on
+  // every iteration).
+  for (int t = 0; t < NFULL; ++t) {
+    const float* cur = sKV[t & 1];
+    const bool nxt = t + 1 < NTILE;
+    if (nxt) issue((t + 1) * 64);
+    f32x16 S[2];
+    qk(cur, S);
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+      const float mx = tile_max_log2<2>(S);
+      if (__any(mx > m2 + kRescaleThr)) {
+        const float mn = fmaxf(m2, mx);
+        const float alpha = fast_exp2(m2 - mn);
+        l *= alpha;
+        scale_acc(O, alpha);
+        m2 = mn;
       }
-      softmax_apply<ACT>(S, m2, l);
-      pv(cur, S);
-      if (nxt) commit(sKV[(t + 1) & 1]);
-      __syncthreads();
     }
-    if (t < NFULL) {
-      const float mn = fmaxf(m2, mx);
-      const float alpha = fast_exp2(m2 - mn);
-      l *= alpha;
-      scale_acc(O, alpha);
-      m2 = mn;
-    }
+    softmax_apply<ACT, 2>(S, m2, l);
+    pv(cur, S);
+    if (nxt) commit(sKV[(t + 1) & 1]);
+    __syncthreads();
   }
   if (NFULL < NTILE) {  // ragged last tile: masked, full online-softmax update
     const float* cur = sKV[NFULL & 1];
     f32x16 S[2];
     qk(cur, S);
-    mask_tile<ACT>(S, NFULL * 64, p.Ns, h);
+    mask_tile<ACT, 2>(S, NFULL * 64, p.Ns, h);
     float alpha;
-    if (softmax_tile<ACT>(S, m2, l, alpha)) scale_acc(O, alpha);
+    if (softmax_tile<ACT, 2>(S, m2, l, alpha)) scale_acc(O, alpha);
     pv(cur, S);
   }
   attn_epilogue<float>(p, O, l, b, hh, q, h);
@@ -317,12 +314,14 @@ __global__ void __launch_bounds__(64 * NW) attn_f32_kernel(const AttnP p) {
 // ======================================================================================
 // bf16 variant
 // ======================================================================================
-template <int ACT, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
-  constexpr int NT = 64 * NW;
-  constexpr int LK = 72;  // 64 + 8 bf16 (144-B rows): conflict-free 16-B row reads
-  constexpr int KSZ = 64 * LK, VSZ = 128 * LK;
-  constexpr int KCH = 512 / NT, VCH = 1024 / NT;  // 16-B chunks per thread per tile
+template <int ACT, int NW, int TK>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_bf16_kernel(const AttnP p) {
+  constexpr int NT = 64 * NW, NKB = TK / 32;
+  constexpr int LK = 72;       // K rows: 64 + 8 bf16 (144 B): conflict-free 16-B row reads
+  constexpr int LV = TK + 8;   // V'^T rows: TK keys + 8 (row stride = 16 B mod 256 B): conflict-free
+  constexpr int KSZ = TK * LK, VSZ = 128 * LV;
+  constexpr int KCH = TK * 8 / NT, VCH = 128 * (TK / 8) / NT;  // 16-B chunks per thread per tile
+  static_assert(KCH >= 1 && VCH >= 1, "tile config");
   __shared__ __attribute__((aligned(16))) bf16 sK[2][KSZ];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][VSZ];
   int b, hh, qb;
@@ -362,8 +361,13 @@ __global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
-      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
-      sv[i] = *reinterpret_cast<const bf16x8*>(vtb + (long long)row * p.ldt + key0 + col);  // zero-padded to ldt
+      const int c = tid + NT * i, row = c / (TK / 8), col = (c % (TK / 8)) * 8;
+      if (key0 + col < p.ldt) {  // the image is zero padded to ldt = ceil64(Ns)
+        sv[i] = *reinterpret_cast<const bf16x8*>(vtb + (long long)row * p.ldt + key0 + col);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv[i][e] = (bf16)0.0f;
+      }
     }
   };
   auto commit = [&](bf16* dk, bf16* dv) {
@@ -374,8 +378,8 @@ __global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
-      const int c = tid + NT * i, row = c >> 3, col = (c & 7) * 8;
-      *reinterpret_cast<bf16x8*>(dv + row * LK + col) = sv[i];
+      const int c = tid + NT * i, row = c / (TK / 8), col = (c % (TK / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(dv + row * LV + col) = sv[i];
     }
   };
 
@@ -386,9 +390,9 @@ __global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
     for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
   float m2 = -INFINITY, l = 0.f;
 
-  auto qk = [&](const bf16* ck, f32x16 (&S)[2]) {
+  auto qk = [&](const bf16* ck, f32x16 (&S)[NKB]) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) S[kb][e] = 0.f;
       const bf16* krow = ck + (kb * 32 + r32) * LK + 8 * h;
@@ -399,9 +403,9 @@ __global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
       }
     }
   };
-  auto pv = [&](const bf16* cv, const f32x16 (&P)[2]) {
+  auto pv = [&](const bf16* cv, const f32x16 (&P)[NKB]) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // B = P^T: element j <-> key kb*32 + 16s + 8(j>>2) + 4h + (j&3) (accumulator regs 8s..8s+7);
@@ -409,54 +413,50 @@ __global__ void __launch_bounds__(64 * NW) attn_bf16_kernel(const AttnP p) {
         bf16x8 pf;
 #pragma unroll
         for (int j = 0; j < 8; ++j) pf[j] = (bf16)P[kb][8 * s + j];
-        const bf16* vcol = cv + r32 * LK + kb * 32 + 16 * s + 8 * h;
+        const bf16* vcol = cv + r32 * LV + kb * 32 + 16 * s + 8 * h;
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vcol + 32 * blk * LK);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vcol + 32 * blk * LV);
           O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
         }
       }
     }
   };
 
-  const int NTILE = (p.Ns + 63) / 64, NFULL = p.Ns / 64;
+  const int NTILE = (p.Ns + TK - 1) / TK, NFULL = p.Ns / TK;
   issue(0);
   commit(sK[0], sV[0]);
   __syncthreads();
-  // Full tiles; see the fp32 kernel for the leave-rescale-reenter structure.
-  int t = 0;
-  while (t < NFULL) {
-    float mx = 0.f;
-    for (; t < NFULL; ++t) {
-      const int cb = t & 1;
-      const bool nxt = t + 1 < NTILE;
-      if (nxt) issue((t + 1) * 64);
-      f32x16 S[2];
-      qk(sK[cb], S);
-      if constexpr (ACT == MHADA_ACT_SOFTMAX) {
-        mx = tile_max_log2(S);
-        if (__any(mx > m2 + kRescaleThr)) break;
+  // Full tiles.  The rescale (rare after the first tile, P <= 2^kRescaleThr) is a wave-uniform
+  // branch inside the single loop so the O accumulators keep one register assignment.
+  for (int t = 0; t < NFULL; ++t) {
+    const int cb = t & 1;
+    const bool nxt = t + 1 < NTILE;
+    if (nxt) issue((t + 1) * TK);
+    f32x16 S[NKB];
+    qk(sK[cb], S);
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+      const float mx = tile_max_log2<NKB>(S);
+      if (__any(mx > m2 + kRescaleThr)) {
+        const float mn = fmaxf(m2, mx);
+        const float alpha = fast_exp2(m2 - mn);
+        l *= alpha;
+        scale_acc(O, alpha);
+        m2 = mn;
       }
-      softmax_apply<ACT>(S, m2, l);
-      pv(sV[cb], S);
-      if (nxt) commit(sK[cb ^ 1], sV[cb ^ 1]);
-      __syncthreads();
     }
-    if (t < NFULL) {
-      const float mn = fmaxf(m2, mx);
-      const float alpha = fast_exp2(m2 - mn);
-      l *= alpha;
-      scale_acc(O, alpha);
-      m2 = mn;
-    }
+    softmax_apply<ACT, NKB>(S, m2, l);
+    pv(sV[cb], S);
+    if (nxt) commit(sK[cb ^ 1], sV[cb ^ 1]);
+    __syncthreads();
   }
   if (NFULL < NTILE) {
     const int cb = NFULL & 1;
-    f32x16 S[2];
+    f32x16 S[NKB];
     qk(sK[cb], S);
-    mask_tile<ACT>(S, NFULL * 64, p.Ns, h);
+    mask_tile<ACT, NKB>(S, NFULL * TK, p.Ns, h);
     float alpha;
-    if (softmax_tile<ACT>(S, m2, l, alpha)) scale_acc(O, alpha);
+    if (softmax_tile<ACT, NKB>(S, m2, l, alpha)) scale_acc(O, alpha);
     pv(sV[cb], S);
   }
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
@@ -470,6 +470,13 @@ static int attn_waves(int dtype) {
   return 8;
 }
 
+// Keys per bf16 tile (64 | 128): MHADA_ATTN_TK overrides the default (read per call).
+static int attn_tk() {
+  const char* e = getenv("MHADA_ATTN_TK");
+  if (e && atoi(e) == 64) return 64;
+  return 128;
+}
+
 template <int NW>
 static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s) {
   const dim3 grid(p.nblk), blk(64 * NW);
@@ -479,10 +486,14 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
     else
       hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
   } else {
-    if (activation == MHADA_ACT_SOFTMAX)
-      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW>), grid, blk, 0, s, p);
-    else
-      hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
+    const bool t128 = NW == 8 && attn_tk() == 128;  // 2 x 106 KiB of LDS does not fit a CU
+    if (activation == MHADA_ACT_SOFTMAX) {
+      if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
+      else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, 64>), grid, blk, 0, s, p);
+    } else {
+      if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
+      else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, 64>), grid, blk, 0, s, p);
+    }
   }
 }
 

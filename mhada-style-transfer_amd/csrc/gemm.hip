@@ -15,6 +15,7 @@
 #include "common.h"
 
 #include <mutex>
+#include <stdlib.h>
 
 namespace mhada {
 
@@ -28,6 +29,7 @@ struct GemmP {
   const void* r; long long ldr, sr1, sr2;
   void* c; long long ldc, sc1, sc2;
   int relu, tiles_n, ntiles;
+  int dbg;  // ping-pong kernel experiments (MHADA_GEMM_DBG): 1 no DMA in loop, 2 no LDS reads, 4 no barriers
 };
 
 template <typename TC> struct Cfg {
@@ -199,6 +201,72 @@ MHADA_DEV void commit_a(const AStage<TA, TC, AMODE, A_CH>& st, TC* sA, int tid) 
   }
 }
 
+// Epilogue shared by the GEMM kernels.  The MFMAs take W as the A operand, so each
+// accumulator holds C^T: the lane owns ONE output row m (mrow + 32*mi) and registers
+// 4g..4g+3 of acc[mi][ni] hold the 4 consecutive columns ncol + 32*ni + 8g + 4h + 0..3 — every
+// store moves 4 elements (8-16 B) instead of one (a row-per-lane scalar-store tail is
+// store-issue bound).  Fused: + bias[n], ReLU, + residual r[m][n] (after the ReLU).
+template <typename TO, int TM, int TN>
+MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, int z2, int mrow, int ncol, int h) {
+  TO* cbase = reinterpret_cast<TO*>(p.c) + z1 * p.sc1 + z2 * p.sc2;
+  const TO* rbase = p.r ? reinterpret_cast<const TO*>(p.r) + z1 * p.sr1 + z2 * p.sr2 : nullptr;
+  const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = mrow + mi * 32;
+    if (m >= p.M) continue;
+    TO* crow = cbase + (long long)m * p.ldc;
+    const TO* rrow = rbase ? rbase + (long long)m * p.ldr : nullptr;
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = ncol + ni * 32 + 8 * g + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][4 * g + e];
+        if (n + 3 < p.N) {
+          if (bbase) {
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bbase + n);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bb[e];
+          }
+          if (p.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if constexpr (sizeof(TO) == 4) {
+            if (rrow) {
+              const f32x4 rr = *reinterpret_cast<const f32x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += rr[e];
+            }
+            *reinterpret_cast<f32x4*>(crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            if (rrow) {
+              const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += (float)rr[e];
+            }
+            *reinterpret_cast<bf16x4*>(crow + n) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e < p.N) {
+              float x = v[e] + (bbase ? bbase[n + e] : 0.f);
+              if (p.relu) x = fmaxf(x, 0.f);
+              if (rrow) x += to_f32<TO>(rrow[n + e]);
+              crow[n + e] = from_f32<TO>(x);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+
 // ------------------------------------------------------------------------------------
 // BM x BN block tile, WM x WN waves (NT = 64*WM*WN threads); each wave owns a
 // (BM/WM) x (BN/WN) sub-tile of TM x TN 32x32 MFMA blocks.
@@ -346,66 +414,199 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
     __syncthreads();
   }
 
-  // epilogue.  The MFMAs above take W as the A operand, so each accumulator holds C^T: the
-  // lane owns ONE output row m (= lane&31 within the block) and registers 4g..4g+3 hold the 4
-  // consecutive columns 8g + 4h + 0..3 — every store below moves 4 elements (8-16 B) instead of
-  // one (a row-per-lane scalar-store tail is store-issue bound).
-  TO* cbase = reinterpret_cast<TO*>(p.c) + z1 * p.sc1 + z2 * p.sc2;
-  const TO* rbase = p.r ? reinterpret_cast<const TO*>(p.r) + z1 * p.sr1 + z2 * p.sr2 : nullptr;
-  const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
+  store_tile<TO, TM, TN>(p, acc, z1, z2, m0 + arow0, n0 + brow0 - r32, h);
+}
+
+// ------------------------------------------------------------------------------------
+// Ping-pong bf16 GEMM for the large dense contractions (bf16 A rows or reflect-padded 3x3
+// taps, K % 64 == 0).  256x256 block tile, 8 waves in two groups of 4: group g owns output
+// rows 128g..128g+127 and wave (g, wc) a 128x64 sub-tile (4x2 32x32 blocks).  Each K-tile
+// (BK = 64) runs in 4 phases, each one 32-column block x 2 k-steps of the sub-tile; a phase is
+// {LDS fragment reads + LDS-DMA prefetch} -> s_barrier -> {8 MFMAs} -> s_barrier, and group 1
+// runs one barrier behind group 0, so on every SIMD one wave's MFMA phase pairs with the other
+// wave's load phase (cdna_hip_programming.md §5 "256² 8-phase template", T3/T4/T5).
+// Staging: global_load_lds (16 B per lane, lane-linear 1 KiB per wave-instruction) into a
+// 2-deep ring of K-tiles, each split in 4 half-tiles [A rows 0-127 | A 128-255 | W 0-127 |
+// W 128-255] of 128 rows x 128 B; rows are unpadded, chunk slot = chunk ^ ((row >> 1) & 7)
+// (applied on the per-lane SOURCE address, conflict-free ds_read_b128 for the 32x32x16
+// operand groups).  Waits are counted (vmcnt 4/0), never a drain inside the loop; the phase
+// schedule and ring-slot reuse rules are spelled out above the main loop.
+// ------------------------------------------------------------------------------------
+MHADA_DEV void glds16(const void* src, bf16* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+#define PP_BARRIER() do { __builtin_amdgcn_sched_barrier(0); if (!(dbg & 4)) __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+template <typename TO, int AMODE>
+__global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
+  constexpr int BK = 64, HALF = 128 * BK, TILE = 4 * HALF;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];  // 128 KiB, the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wc = wave & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int z = blockIdx.y, z1 = z / p.nb2, z2 = z - z1 * p.nb2;
+  const int t = xcd_remap(blockIdx.x, p.ntiles);
+  const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const bf16* abase = reinterpret_cast<const bf16*>(p.a) + z1 * p.sa1 + z2 * p.sa2;
+  const bf16* wbase = reinterpret_cast<const bf16*>(p.w) + z1 * p.sw1 + z2 * p.sw2;
+
+  // ---- staging geometry: instruction i of this wave covers rows 16*wave + 8i + (lane>>3) of a
+  // half tile; lane slot lane&7 receives source chunk (lane&7) ^ ((row>>1)&7).
+  int cofs[2];
 #pragma unroll
-  for (int mi = 0; mi < TM; ++mi) {
-    const int m = m0 + arow0 + mi * 32;
-    if (m >= p.M) continue;
-    TO* crow = cbase + (long long)m * p.ldc;
-    const TO* rrow = rbase ? rbase + (long long)m * p.ldr : nullptr;
+  for (int i = 0; i < 2; ++i) cofs[i] = 8 * ((lane & 7) ^ (4 * i + (lane >> 4)));
+  unsigned aoff[2][2], woff[2][2];  // element offsets of (half, i) rows (ROWS: incl. chunk)
+  int ab[2][2], ay[2][2], ax[2][2];  // CONV: (image, y, x) of the output pixel
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
+  for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + brow0 - r32 + ni * 32 + 8 * g + 4 * h;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][4 * g + e];
-        if (n + 3 < p.N) {
-          if (bbase) {
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(bbase + n);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bb[e];
-          }
-          if (p.relu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          if constexpr (sizeof(TO) == 4) {
-            if (rrow) {
-              const f32x4 rr = *reinterpret_cast<const f32x4*>(rrow + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += rr[e];
-            }
-            *reinterpret_cast<f32x4*>(crow + n) = f32x4{v[0], v[1], v[2], v[3]};
-          } else {
-            if (rrow) {
-              const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rrow + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += (float)rr[e];
-            }
-            *reinterpret_cast<bf16x4*>(crow + n) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e < p.N) {
-              float x = v[e] + (bbase ? bbase[n + e] : 0.f);
-              if (p.relu) x = fmaxf(x, 0.f);
-              if (rrow) x += to_f32<TO>(rrow[n + e]);
-              crow[n + e] = from_f32<TO>(x);
-            }
-          }
-        }
+    for (int i = 0; i < 2; ++i) {
+      const int rr = 16 * wave + 8 * i + (lane >> 3);
+      const int m = min(m0 + 128 * hh + rr, p.M - 1);
+      const int n = min(n0 + 128 * hh + rr, p.N - 1);
+      woff[hh][i] = (unsigned)((long long)n * p.ldw + cofs[i]);
+      if constexpr (AMODE == MHADA_A_ROWS) {
+        aoff[hh][i] = (unsigned)((long long)m * p.lda + cofs[i]);
+      } else {
+        const int hw = p.out_h * p.out_w;
+        const int b = m / hw, rem = m - b * hw;
+        ab[hh][i] = b; ay[hh][i] = rem / p.out_w; ax[hh][i] = rem - (rem / p.out_w) * p.out_w;
+        aoff[hh][i] = 0;
       }
     }
+  auto stage_a = [&](int hh, int kt) {
+    bf16* dst = smem + (kt & 1) * TILE + hh * HALF + wave * 1024;
+    const int k0 = kt * BK;
+    if constexpr (AMODE == MHADA_A_ROWS) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(abase + aoff[hh][i] + k0, dst + 512 * i);
+    } else {
+      const int cin_n = p.img_c;
+      const int tap = k0 / cin_n, cin0 = k0 - tap * cin_n;
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int Y = reflect1(ay[hh][i] + dy, p.out_h), X = reflect1(ax[hh][i] + dx, p.out_w);
+        const unsigned off = (unsigned)(((ab[hh][i] * p.img_h + Y) * p.img_w + X) * cin_n + cin0 + cofs[i]);
+        glds16(abase + off, dst + 512 * i);
+      }
+    }
+  };
+  auto stage_w = [&](int hh, int kt) {
+    bf16* dst = smem + (kt & 1) * TILE + (2 + hh) * HALF + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(wbase + woff[hh][i] + kt * BK, dst + 512 * i);
+  };
+
+  // ---- fragment reads: row r32 of a 32-row block, 16-B chunk 2ks+h, swizzled slot
+  const int swz = (r32 >> 1) & 7;
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = 8 * ((2 * ks + h) ^ swz);
+  const bf16* sA = smem + grp * HALF + r32 * 64;                              // + mt*2048
+  const bf16* sW = smem + (2 + (wc >> 1)) * HALF + ((wc & 1) * 64 + r32) * 64;  // + nt*2048
+  bf16x8 af[4][2], wf[2][2];  // [mt][k-step of the pair], [nt][k-step of the pair]
+  auto read_a = [&](int kp, int cb) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        af[mt][s2] = *reinterpret_cast<const bf16x8*>(sA + cb * TILE + mt * 2048 + koff[2 * kp + s2]);
+  };
+  auto read_w = [&](int nt, int kp, int cb) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      wf[nt][s2] = *reinterpret_cast<const bf16x8*>(sW + cb * TILE + nt * 2048 + koff[2 * kp + s2]);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  // one phase: the 4 row blocks x one 32-column block x 2 k-steps = 8 MFMAs, 4 independent chains
+  auto compute = [&](int nt) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[nt][s2], af[mt][s2], acc[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // Schedule per K-tile t (buffer t&1), phases:
+  //   0: read A k-steps 0,1 + W cols 0-31   | DMA W-half 0 of t+1
+  //   1: read W cols 32-63                  | DMA W-half 1 of t+1
+  //   2: read A k-steps 2,3 + W cols 0-31   |
+  //   3: read W cols 32-63                  | DMA A-halves of t+2; vmcnt -> tile t+1 landed
+  // A (the large, HBM-streamed operand) is prefetched a whole K-tile earlier than W (L2-hot).
+  // Ring: tile t's A slots are last read in phase 2 and refilled (t+2) in phase 3; its W slots
+  // are last read in phase 3 and refilled (t+2) in phases 0/1 of tile t+1.
+  const int KT = p.K / BK;
+  const int dbg = p.dbg;
+  stage_a(0, 0); stage_a(1, 0); stage_w(0, 0); stage_w(1, 0);
+  if (KT > 1) {
+    stage_a(0, 1); stage_a(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  PP_BARRIER();
+  if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
+
+  const bool rd = !(dbg & 2);
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cb = kt & 1;
+    const bool n1 = kt + 1 < KT && !(dbg & 1), n2 = kt + 2 < KT && !(dbg & 1);
+    // phase 0
+    if (rd) { read_a(0, cb); read_w(0, 0, cb); }
+    if (n1) stage_w(0, kt + 1);
+    PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+    // phase 1
+    if (rd) read_w(1, 0, cb);
+    if (n1) stage_w(1, kt + 1);
+    PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+    // phase 2
+    if (rd) { read_a(1, cb); read_w(0, 1, cb); }
+    PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+    // phase 3
+    if (rd) read_w(1, 1, cb);
+    if (n2) {
+      stage_a(0, kt + 2); stage_a(1, kt + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+  }
+  if (grp == 0) PP_BARRIER();  // balance the barrier count of the two groups
+  store_tile<TO, 4, 2>(p, acc, z1, z2, m0 + grp * 128 + r32, n0 + wc * 64, h);
+}
+
+template <typename TO, int AMODE>
+static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
+  GemmP p = p0;
+  const char* dbg = getenv("MHADA_GEMM_DBG");
+  p.dbg = dbg ? atoi(dbg) : 0;
+  p.tiles_n = (p.N + 255) / 256;
+  p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
+  hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
+  return check_launch("mhada_gemm");
+}
+
+// The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
+// spans addressable with 32-bit element offsets.  MHADA_GEMM_PP=0 disables it (A/B runs).
+static bool pp_enabled() {
+  const char* e = getenv("MHADA_GEMM_PP");
+  return !(e && e[0] == '0');
 }
 
 template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN, int WM, int WN>
@@ -425,6 +626,16 @@ static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
   return check_launch("mhada_gemm");
 }
 
+// 32-bit element offsets inside one z-problem (the ping-pong kernel's staging addresses)
+static bool pp_offsets_fit(const GemmP& p, int amode) {
+  const long long lim = 1LL << 31;
+  const long long wspan = (long long)(p.N - 1) * p.ldw + p.K;
+  long long aspan;
+  if (amode == MHADA_A_ROWS) aspan = (long long)(p.M - 1) * p.lda + p.K;
+  else aspan = (long long)p.M / ((long long)p.out_h * p.out_w) * p.img_h * p.img_w * p.img_c;
+  return wspan < lim && aspan < lim;
+}
+
 // Tile choice.  fp32 MFMA runs 1/16 of the bf16 rate, so 128x128 tiles (64 FLOP per staged
 // byte) are far from L2-bound; bf16 needs 256-row tiles (up to 128 FLOP/B at 256x256) to stay
 // under the ~34 TB/s L2 ceiling at MFMA rate.
@@ -438,6 +649,10 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
     if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {  // 4 bilinear taps staged per chunk: keep the tile small
       return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
     } else {
+      if constexpr (sizeof(TA) == 2 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
+        if (p.N > 128 && p.K % 64 == 0 && pp_enabled() && pp_offsets_fit(p, AMODE))
+          return launch_gemm_pp<TO, AMODE>(p, nz, s);
+      }
       if (p.N <= 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
       return launch_gemm<TC, TA, TO, AMODE, 256, 256, 2, 4>(p, nz, s);
     }

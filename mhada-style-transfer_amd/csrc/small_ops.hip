@@ -479,14 +479,23 @@ extern "C" int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns,
 
 extern "C" int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns, mhada_stream_t s_) {
   hipStream_t s = (hipStream_t)s_;
-  if (!q || !kv || B <= 0 || H <= 0 || Nc <= 0 || Ns <= 0) return fail("mhada_cosine_prep: bad args");
+  // Nc == 0 (q unused) or Ns == 0 (kv unused) normalises one side only: a cached style's K is
+  // normalised once, each new frame's Q per call.
+  if (B <= 0 || H <= 0 || Nc < 0 || Ns < 0 || (Nc == 0 && Ns == 0) || (Nc > 0 && !q) || (Ns > 0 && !kv))
+    return fail("mhada_cosine_prep: bad args");
+  if (dtype != MHADA_F32 && dtype != MHADA_BF16) return fail("mhada_cosine_prep: bad dtype");
   const long long rq = (long long)B * H * Nc, rk = (long long)B * H * Ns;
-  if (dtype == MHADA_F32) {
-    hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (float*)q, rq, 64);
-    hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (float*)kv, rk, 128);
-  } else {
-    hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (bf16*)q, rq, 64);
-    hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (bf16*)kv, rk, 128);
+  if (rq > 0) {
+    if (dtype == MHADA_F32)
+      hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (float*)q, rq, 64);
+    else
+      hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rq + 3) / 4)), dim3(256), 0, s, (bf16*)q, rq, 64);
+  }
+  if (rk > 0) {
+    if (dtype == MHADA_F32)
+      hipLaunchKernelGGL((rownorm_kernel<float>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (float*)kv, rk, 128);
+    else
+      hipLaunchKernelGGL((rownorm_kernel<bf16>), dim3((unsigned)((rk + 3) / 4)), dim3(256), 0, s, (bf16*)kv, rk, 128);
   }
   return check_launch("mhada_cosine_prep");
 }

@@ -14,7 +14,9 @@ Weights are repacked once per (dtype, parameter version) and cached on the modul
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import weakref
 
 import torch
 
@@ -217,8 +219,13 @@ class _Feat:
         return self._stats
 
 
-def block_forward(blk, fc: _Feat, fs: _Feat, fcs: _Feat, dt: torch.dtype) -> _Feat:
-    """AdaAttnMultiHead.forward (adaDecoder.py:162-206)."""
+def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dtype,
+                  side: Optional[dict] = None) -> _Feat:
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206).
+
+    ``side`` carries the block's style-only tensors (IN statistics of fs, the K|V' projection and
+    its V'^T image): when it is filled they are reused (fs may then be None), when it is an empty
+    dict they are computed and stored into it (the per-style cache of adaformer_forward)."""
     if blk.head_dim != HEAD_DIM:
         raise ValueError(f"the HIP MHAda kernels implement head_dim={HEAD_DIM} (qkv_dim/num_heads), "
                          f"got {blk.head_dim}")
@@ -226,11 +233,18 @@ def block_forward(blk, fc: _Feat, fs: _Feat, fcs: _Feat, dt: torch.dtype) -> _Fe
     H = blk.num_heads
     C = H * HEAD_DIM
     B, Nc, Cc = fc.t.shape
-    Ns = fs.t.shape[1]
-    if Cc != C or fs.t.shape[2] != C or fcs.t.shape[2] != C:
+    cached = bool(side)
+    if cached:
+        mu_s, rstd_s, kv, vt = side["mu_s"], side["rstd_s"], side["kv"], side["vt"]
+        if kv.shape[0] != B:
+            raise ValueError(f"cached style batch {kv.shape[0]} != content batch {B}")
+    else:
+        if fs.t.shape[2] != C:
+            raise ValueError(f"channel mismatch: block expects {C}")
+        mu_s, rstd_s = fs.stats()
+    if Cc != C or fcs.t.shape[2] != C:
         raise ValueError(f"channel mismatch: block expects {C}")
     mu_c, rstd_c = fc.stats()
-    mu_s, rstd_s = fs.stats()
     mu_o, rstd_o = fcs.stats()
     wq, wkv, bkv, v_mu = ops.fold_block(prep["wf"], prep["wg"], prep["wh"], prep["bg"], prep["bh"],
                                         rstd_c, mu_s, rstd_s, dt)
@@ -239,19 +253,46 @@ def block_forward(blk, fc: _Feat, fs: _Feat, fcs: _Feat, dt: torch.dtype) -> _Fe
     ops.gemm(a=fc.t, w=wq, c=q, M=Nc, N=HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Nc * C, HEAD_DIM),
              nb=(B, H), a_mu=mu_c, smu=(C, HEAD_DIM), ldw=HEAD_DIM, sw=(H * HEAD_DIM * HEAD_DIM, HEAD_DIM * HEAD_DIM),
              bias=prep["bf"], sb=(0, HEAD_DIM), ldc=HEAD_DIM, sc=(H * Nc * HEAD_DIM, Nc * HEAD_DIM))
-    kv = torch.empty(B, H, Ns, 2 * HEAD_DIM, device=dev, dtype=dt)
-    ops.gemm(a=fs.t, w=wkv, c=kv, M=Ns, N=2 * HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Ns * C, HEAD_DIM),
-             nb=(B, H), a_mu=mu_s, smu=(C, HEAD_DIM), ldw=HEAD_DIM,
-             sw=(H * 2 * HEAD_DIM * HEAD_DIM, 2 * HEAD_DIM * HEAD_DIM), bias=bkv, sb=(0, 2 * HEAD_DIM),
-             ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM))
     act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
+    if not cached:
+        Ns = fs.t.shape[1]
+        kv = torch.empty(B, H, Ns, 2 * HEAD_DIM, device=dev, dtype=dt)
+        ops.gemm(a=fs.t, w=wkv, c=kv, M=Ns, N=2 * HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Ns * C, HEAD_DIM),
+                 nb=(B, H), a_mu=mu_s, smu=(C, HEAD_DIM), ldw=HEAD_DIM,
+                 sw=(H * 2 * HEAD_DIM * HEAD_DIM, 2 * HEAD_DIM * HEAD_DIM), bias=bkv, sb=(0, 2 * HEAD_DIM),
+                 ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM))
+        if act == ACT_COSINE:
+            ops.cosine_prep(None, kv)
+        vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+        if side is not None:
+            side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt)
     if act == ACT_COSINE:
-        ops.cosine_prep(q, kv)
-    vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+        ops.cosine_prep(q, None)
     with _timed("mhada_attn"):
         att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
     out = ops.linear(att.view(B * Nc, C), prep["w_out"], prep["b_out"], torch.float32)
     return _Feat(out.view(B, Nc, C), fc.h, fc.w)
+
+
+def style_cache(ada, fs: Sequence[torch.Tensor], dt: torch.dtype):
+    """Per-style cache of the blocks' style-side tensors (the video path of
+    infer_video.py:58-92: fs = vit_s(style) once, adaFormer(fc, fs) per frame).
+
+    A hit needs the SAME fs tensor objects (held by weak reference, so a freed and reallocated
+    buffer can never alias), unchanged in place (tensor._version), the same compute dtype and
+    unchanged block parameters.  Returns (per-block dicts, hit).  ``ada.cache_style = False``
+    turns the cache off."""
+    if not getattr(ada, "cache_style", True):
+        return [None] * len(ada.adaAttnHead), False
+    sig = tuple(_signature(b) for b in ada.adaAttnHead)
+    vers = tuple(t._version for t in fs)
+    c = ada.__dict__.get("_mhada_style")
+    if (c is not None and c["dt"] == dt and c["sig"] == sig and c["vers"] == vers
+            and len(c["refs"]) == len(fs) and all(r() is t for r, t in zip(c["refs"], fs))):
+        return c["sides"], True
+    sides = [dict() for _ in ada.adaAttnHead]
+    ada.__dict__["_mhada_style"] = dict(dt=dt, sig=sig, vers=vers, refs=[weakref.ref(t) for t in fs], sides=sides)
+    return sides, False
 
 
 # ---------------------------------------------------------------------------------------
@@ -288,12 +329,14 @@ def adaformer_forward(ada, fc: Sequence[torch.Tensor], fs: Sequence[torch.Tensor
     """AdaAttnTransformerMultiHead.forward (adaDecoder.py:253-268): returns (fcs, cs)."""
     require_device(fc[0], "AdaAttnTransformerMultiHead")
     dt = resolve_compute_dtype(ada)
-    fcf = [_Feat.from_nchw(t) for t in fc[: ada.num_layers]]
-    fsf = [_Feat.from_nchw(t) for t in fs[: ada.num_layers]]
+    L = ada.num_layers
+    fcf = [_Feat.from_nchw(t) for t in fc[:L]]
+    sides, hit = style_cache(ada, fs[:L], dt)
+    fsf = [None] * L if hit else [_Feat.from_nchw(t) for t in fs[:L]]
     fcs = fcf[0]
-    for i in range(ada.num_layers):
-        fcs = block_forward(ada.adaAttnHead[2 * i], fcf[i], fsf[i], fcs, dt)
-        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fsf[i], fcs, dt)
+    for i in range(L):
+        fcs = block_forward(ada.adaAttnHead[2 * i], fcf[i], fsf[i], fcs, dt, sides[2 * i])
+        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fsf[i], fcs, dt, sides[2 * i + 1])
     B, N, C = fcs.t.shape
     cs = decoder_forward_tokens(ada.decoder, fcs.t.view(B, fcs.h, fcs.w, C), dt)
     return tokens_to_nchw(fcs.t, fcs.h, fcs.w), cs

@@ -203,10 +203,13 @@ def transpose_v(kv: torch.Tensor) -> torch.Tensor:
     return vt
 
 
-def cosine_prep(q: torch.Tensor, kv: torch.Tensor) -> None:
-    B, H, Nc, _ = q.shape
-    Ns = kv.shape[2]
-    rc = _lib.load().mhada_cosine_prep(q.data_ptr(), kv.data_ptr(), dt_code(q.dtype), B, H, Nc, Ns, _stream())
+def cosine_prep(q: Optional[torch.Tensor], kv: Optional[torch.Tensor]) -> None:
+    """L2-normalise Q rows and/or the K half of KV rows in place (either may be None)."""
+    ref = q if q is not None else kv
+    B, H = ref.shape[0], ref.shape[1]
+    Nc = q.shape[2] if q is not None else 0
+    Ns = kv.shape[2] if kv is not None else 0
+    rc = _lib.load().mhada_cosine_prep(_ptr(q), _ptr(kv), dt_code(ref.dtype), B, H, Nc, Ns, _stream())
     _lib.check(rc, "mhada_cosine_prep")
 
 

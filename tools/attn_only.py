@@ -1,0 +1,20 @@
+"""Run only the bf16 (or fp32) MHAda attention kernel a few times (for rocprofv3 PMC passes)."""
+import os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd")]
+import torch
+from mhada_hip import ops
+
+dt = torch.bfloat16 if (len(sys.argv) < 2 or sys.argv[1] == "bf16") else torch.float32
+B, n = (4, 16384) if dt == torch.bfloat16 else (8, 4096)
+H = 8
+q = torch.randn(B, H, n, 64, device="cuda").to(dt)
+kv = torch.randn(B, H, n, 128, device="cuda").to(dt)
+vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+fcs = torch.randn(B, n, 512, device="cuda")
+mu, rs = ops.instnorm_stats(fcs)
+vmu = torch.zeros(B, 512, device="cuda")
+for _ in range(int(os.environ.get("ITERS", "5"))):
+    ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+torch.cuda.synchronize()
+print("done")

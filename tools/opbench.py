@@ -34,6 +34,18 @@ def bench(fns, rounds=7, iters=10):
     return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
 
 
+def with_env(key, val, fn, *a, **k):
+    old = os.environ.get(key)
+    os.environ[key] = val
+    try:
+        return fn(*a, **k)
+    finally:
+        if old is None:
+            del os.environ[key]
+        else:
+            os.environ[key] = old
+
+
 def gemm_suite():
     dev = "cuda"
     for dt in (torch.bfloat16, torch.float32):
@@ -46,6 +58,8 @@ def gemm_suite():
             r = torch.randn(M, N, device=dev) if res else None
             fns = {"ours": lambda: ops.linear(x, w, b, out, residual=r, relu=relu),
                    "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
+            if dt == torch.bfloat16:
+                fns["old"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r, relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
@@ -64,6 +78,8 @@ def conv_suite():
             w = (torch.randn(Co, 9 * Ci, device=dev) / (9 * Ci) ** 0.5).to(dt)
             bias = torch.randn(Co, device=dev)
             fns = {"fused": lambda: ops.conv3x3(x, w, bias, dt, upsample=up)}
+            if dt == torch.bfloat16 and not up:
+                fns["old"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.conv3x3, x, w, bias, dt, upsample=False)
             if up:
                 fns["sep"] = lambda: ops.conv3x3(ops.upsample2x(x), w, bias, dt, upsample=False)
                 fns["upsample_only"] = lambda: ops.upsample2x(x)
@@ -86,13 +102,13 @@ def attn_suite():
         fcs = torch.randn(B, n, 512, device=dev)
         mu, rs = ops.instnorm_stats(fcs)
         vmu = torch.zeros(B, 512, device=dev)
-        def run(nw, var=""):
+        def run(nw, tk=128):
             def f():
                 os.environ["MHADA_ATTN_WAVES"] = str(nw)
-                os.environ["MHADA_ATTN_VARIANT"] = var
+                os.environ["MHADA_ATTN_TK"] = str(tk)
                 ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
             return f
-        fns = {"attn_w4": run(4), "attn_w8": run(8)}
+        fns = {"attn_w4": run(4), "attn_w8_tk64": run(8, 64), "attn_w8_tk128": run(8, 128)}
         t = bench(fns, rounds=5, iters=3)
         # the variants must agree
         outs = {k: (f(), ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0))[1] for k, f in fns.items()}
@@ -101,7 +117,7 @@ def attn_suite():
             err = ((o.float() - ref).norm() / ref.norm()).item()
             print(f"   variant {k}: rel diff vs first {err:.2e}")
         os.environ.pop("MHADA_ATTN_WAVES", None)
-        os.environ.pop("MHADA_ATTN_VARIANT", None)
+        os.environ.pop("MHADA_ATTN_TK", None)
         fl = 6 * n * n * 512 * B
         print(f"attn {str(dt)[6:]:8s} B={B} N={n}: " + "  ".join(f"{k} {v:7.3f} ms {fl / v / 1e9:7.1f} TF"
                                                                for k, v in t.items()))
