@@ -3,7 +3,8 @@
 A "step" is one full style-transfer forward — vit_c(content), vit_s(style),
 adaFormer(fc, fs) (infer_image.py:83-85 / infer_time.py:74-77) — over one synthetic batch
 already resident in HBM.  Headline workload = BASELINE configs[1]: 512x512, batch 8, fp32.
-The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path) under "configs".
+The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path) and configs[4] (1080p
+video frames against a cached 256^2 style + warping error, fp32 and bf16) under "configs".
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -135,6 +136,63 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
     }
 
 
+def run_video(dtype, steps, warmup, rank, world):
+    """BASELINE configs[4]: infer_video.py per-frame stylisation at 1080x1920 with a 256^2
+    style encoded once (its K/V cached by the AdaFormer, engine.style_cache) plus the temporal
+    warping-error metric of the new frame against the previous one (exps_sintel.py:101-109,
+    HIP warp kernel).  Synthetic smooth video: seeded low-frequency noise translating by a known
+    (3, 1) px per frame; the flow is that translation, the mask its forward/backward check."""
+    from mhada_hip import video
+    from mhada_hip.recipe import seeded_image
+    vc, vs, ada = build_models(dtype)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    H, W, n = 1080, 1920, steps + warmup + 1
+    g = torch.Generator(device="cpu").manual_seed(500 + rank)
+    base = torch.nn.functional.interpolate(torch.rand(1, 3, H // 8 + 2, W // 8 + 2, generator=g) * 255,
+                                           size=(H + 16 * n, W + 16 * n), mode="bilinear", align_corners=False)
+    frames = [base[:, :, 1 * t: 1 * t + H, 3 * t: 3 * t + W].contiguous().to(dev) for t in range(n)]
+    flow = torch.empty(1, 2, H, W, device=dev)
+    flow[:, 0], flow[:, 1] = 3.0, 1.0  # frame t+1 at p equals frame t at p + (3, 1)
+    st = video.VideoStylizer(vc, vs, ada)
+    with torch.no_grad():
+        st.set_style(seeded_image(1, 256, 256, 12 + 1000 * rank).to(dev))
+        mask = video.flow_warp_mask(flow[0], -flow[0])
+        st(frames[0])
+
+        def step(t):
+            st(frames[t])
+            return st.warping_error(flow, mask)
+
+        for t in range(1, warmup + 1):
+            step(t)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(warmup + 1, warmup + 1 + steps):
+            err = step(t)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    assert torch.isfinite(err).all()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    nc, ns = (H // 8) * (W // 8), (256 // 8) ** 2
+    d = 64
+    fl = (72 * nc * C * C + 196608 * nc + 6 * (6 * nc * ns * C + 2 * nc * C * d + 2 * nc * C * C)
+          + 30892032 * nc)  # SURVEY §8d, style side cached
+    dts = "f32" if dtype == torch.float32 else "bf16"
+    return {"value": steps * world / elapsed, "unit": "frames/s", "ms_per_frame": elapsed / steps * 1e3,
+            "dtype": dts, "tflops": fl * steps / elapsed / 1e12, "warping_error_last": float(err[0]),
+            "config": {"workload": "infer_video.py: 1080x1920 frames, 256x256 style cached, + warping error",
+                       "batch_per_gpu": 1, "compute_dtype": dts, "parallelism": f"replicas x{world}"}}
+
+
 def run_train(steps, warmup, rank, world):
     """BASELINE configs[3]: train_image.py step at 512^2, 8 images per GPU, DP over RCCL."""
     import network
@@ -240,6 +298,9 @@ def main():
         return
     main_cfg = run_config(512, 8, torch.float32, args.steps, args.warmup, rank, world)
     second = None if args.no_secondary else run_config(1024, 4, torch.bfloat16, args.steps, args.warmup, rank, world)
+    videos = {} if args.no_secondary else {
+        f"video_1080p_s256_{'f32' if dt == torch.float32 else 'bf16'}": run_video(dt, args.steps, args.warmup, rank, world)
+        for dt in (torch.float32, torch.bfloat16)}
 
     if rank == 0:
         line = {
@@ -263,6 +324,8 @@ def main():
             line["configs"] = {"1024x1024_b4_bf16": {k: second[k] for k in
                                                     ("value", "ms_per_step", "frames_per_s_per_gpu", "dtype",
                                                      "tflops_whole_step", "roofline", "config")}}
+        if videos:
+            line.setdefault("configs", {}).update(videos)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

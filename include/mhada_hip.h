@@ -145,6 +145,26 @@ int mhada_conv3x3_out3(const void* x, int dtype, const float* w, const float* b,
 int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int C,
                      mhada_stream_t stream);
 
+/* ---- video path: optical-flow warping, NCHW fp32 ---------------------- */
+
+/* warp (utilities.py:100-118): y = grid_sample(x, (grid + flow) normalised by (W-1, H-1),
+ * bilinear, align_corners=False).  x, y [B][C][H][W]; flow [B][2][H][W] (x then y
+ * displacement, pixels); padding 0 = "zeros", 1 = "border". */
+int mhada_warp(const float* x, const float* flow, float* y, int B, int C, int H, int W,
+               int padding, mhada_stream_t stream);
+
+/* flow_warp_mask (utilities.py:121-151): mask [H][W] = 1 where the forward flow flo01 warped
+ * back by flo10 returns within `threshold` (L1, pixels) of the start, else 0.  flo01, flo10
+ * [2][H][W]; padding as mhada_warp. */
+int mhada_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int H, int W,
+                         float threshold, int padding, mhada_stream_t stream);
+
+/* Warping error (exps_sintel.py:101-109): out[b] = sum(mask * |cs2 - warp(cs1, flow)|) /
+ * (C*H*W) per image, zero padding; cs1, cs2 [B][C][H][W], flow [B][2][H][W], mask [B][H][W].
+ * work: fp64 scratch of B * ceil(H*W/256) entries (fixed-order partial sums). */
+int mhada_warp_l1(const float* cs1, const float* cs2, const float* flow, const float* mask,
+                  double* work, float* out, int B, int C, int H, int W, mhada_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -644,6 +644,10 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // N <= 64: 8 waves of 32x64 (one 256x64 tile keeps 8 waves per CU at 92 KiB of LDS)
   if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
   if constexpr (sizeof(TC) == 4) {
+    // MHADA_GEMM_F32_TILE=256x128|128x256 (experiments; read per call)
+    const char* e = getenv("MHADA_GEMM_F32_TILE");
+    if (e && e[0] == '2' && p.N > 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
+    if (e && e[0] == '1' && e[3] == 'x' && e[4] == '2' && p.N > 128) return launch_gemm<TC, TA, TO, AMODE, 128, 256, 2, 4>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
   } else {
     if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {  // 4 bilinear taps staged per chunk: keep the tile small

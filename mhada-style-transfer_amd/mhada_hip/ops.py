@@ -222,3 +222,64 @@ def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch
                                 Ns, activation, _stream())
     _lib.check(rc, "mhada_attn")
     return out
+
+
+# ---- video path: optical-flow warping (NCHW fp32) ---------------------------------------
+_PADDING = {"zeros": 0, "border": 1}
+
+
+def _padding_code(padding_mode: str) -> int:
+    try:
+        return _PADDING[padding_mode]
+    except KeyError:
+        raise ValueError(f"padding_mode {padding_mode!r}: the HIP warp implements 'zeros' and 'border'")
+
+
+def _f32c(t: torch.Tensor, what: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise ValueError(f"{what} must be float32")
+    return t.contiguous()
+
+
+def warp(x: torch.Tensor, flow: torch.Tensor, padding_mode: str = "zeros") -> torch.Tensor:
+    """``mhada_warp``: x [B][C][H][W], flow [B][2][H][W] -> warped x (utilities.py:100-118)."""
+    _need_gpu(x, flow)
+    x, flow = _f32c(x, "x"), _f32c(flow, "flow")
+    B, C, H, W = x.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"flow must be [B,2,H,W] = {[B, 2, H, W]}, got {list(flow.shape)}")
+    y = torch.empty_like(x)
+    rc = _lib.load().mhada_warp(x.data_ptr(), flow.data_ptr(), y.data_ptr(), B, C, H, W,
+                                _padding_code(padding_mode), _stream())
+    _lib.check(rc, "mhada_warp")
+    return y
+
+
+def flow_warp_mask(flo01: torch.Tensor, flo10: torch.Tensor, padding_mode: str = "zeros",
+                   threshold: float = 2) -> torch.Tensor:
+    """``mhada_flow_warp_mask``: flo01, flo10 [2][H][W] -> mask [H][W] (utilities.py:121-151)."""
+    _need_gpu(flo01, flo10)
+    flo01, flo10 = _f32c(flo01, "flo01"), _f32c(flo10, "flo10")
+    if flo01.dim() != 3 or flo01.shape[0] != 2 or flo01.shape != flo10.shape:
+        raise ValueError("flows must both be [2,H,W]")
+    H, W = flo01.shape[1:]
+    mask = torch.empty(H, W, device=flo01.device, dtype=torch.float32)
+    rc = _lib.load().mhada_flow_warp_mask(flo01.data_ptr(), flo10.data_ptr(), mask.data_ptr(), H, W,
+                                          float(threshold), _padding_code(padding_mode), _stream())
+    _lib.check(rc, "mhada_flow_warp_mask")
+    return mask
+
+
+def warp_l1(cs1: torch.Tensor, cs2: torch.Tensor, flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """``mhada_warp_l1``: per-image sum(mask * |cs2 - warp(cs1, flow)|) / (C*H*W)."""
+    _need_gpu(cs1, cs2, flow, mask)
+    cs1, cs2, flow, mask = (_f32c(t, n) for t, n in ((cs1, "cs1"), (cs2, "cs2"), (flow, "flow"), (mask, "mask")))
+    B, C, H, W = cs1.shape
+    if cs2.shape != cs1.shape or tuple(flow.shape) != (B, 2, H, W) or tuple(mask.shape) != (B, H, W):
+        raise ValueError("warp_l1: cs1/cs2 [B,C,H,W], flow [B,2,H,W], mask [B,H,W]")
+    work = torch.empty(B * ((H * W + 255) // 256), device=cs1.device, dtype=torch.float64)
+    out = torch.empty(B, device=cs1.device, dtype=torch.float32)
+    rc = _lib.load().mhada_warp_l1(cs1.data_ptr(), cs2.data_ptr(), flow.data_ptr(), mask.data_ptr(),
+                                   work.data_ptr(), out.data_ptr(), B, C, H, W, _stream())
+    _lib.check(rc, "mhada_warp_l1")
+    return out

@@ -1,0 +1,72 @@
+"""Video-path helpers with the reference's signatures.
+
+* ``warp(x, flo, padding_mode)`` — ``utilities.warp`` (utilities.py:100-118);
+* ``flow_warp_mask(flo01, flo10, padding_mode, threshold)`` — utilities.py:121-151;
+* ``warping_error(cs1, cs2, flow, mask)`` — the per-frame optical-flow metric of
+  exps_sintel.py:101-109 (sum(mask * |cs2 - warp(cs1, flow)|) / (C*H*W));
+* ``VideoStylizer`` — the infer_video.py:58-92 loop: the style is encoded once and, through the
+  AdaFormer's per-style cache (engine.style_cache), its K/V projections are reused per frame.
+
+The inference forms run the HIP kernels (csrc/warp.hip).  When autograd needs a gradient
+through the warp (train_video.py temporal losses) ``warp`` evaluates the same expression with
+differentiable device ops (training v1).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import losses, ops
+
+
+def warp(x: torch.Tensor, flo: torch.Tensor, padding_mode: str = "zeros") -> torch.Tensor:
+    """utilities.warp: bilinear backward warp of x [B,C,H,W] by flow flo [B,2,H,W]."""
+    if torch.is_grad_enabled() and (x.requires_grad or flo.requires_grad):
+        return losses.warp(x, flo, padding_mode)
+    return ops.warp(x, flo, padding_mode)
+
+
+def flow_warp_mask(flo01: torch.Tensor, flo10: torch.Tensor, padding_mode: str = "zeros",
+                   threshold: float = 2) -> torch.Tensor:
+    """utilities.flow_warp_mask: forward/backward flow consistency mask [H,W] (1.0 = valid)."""
+    return ops.flow_warp_mask(flo01, flo10, padding_mode, threshold)
+
+
+def warping_error(cs1: torch.Tensor, cs2: torch.Tensor, flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """exps_sintel.py:101-109 per image: sum(mask * |cs2 - warp(cs1, flow)|) / (C*H*W).
+    mask is [B,H,W] (or [H,W] for B == 1)."""
+    if mask.dim() == 2:
+        mask = mask.unsqueeze(0)
+    return ops.warp_l1(cs1, cs2, flow, mask)
+
+
+class VideoStylizer:
+    """infer_video.py:58-92 on the drop-in modules: ``set_style(s)`` encodes the style once,
+    ``__call__(frame)`` stylises one content frame [B,3,H,W] (0..255) against it and returns the
+    clamped output; ``warping_error(flow, mask)`` scores the last two outputs (exps_sintel)."""
+
+    def __init__(self, vit_c, vit_s, ada):
+        self.vit_c, self.vit_s, self.ada = vit_c, vit_s, ada
+        self.fs = None
+        self.prev: Optional[torch.Tensor] = None
+        self.cur: Optional[torch.Tensor] = None
+
+    @torch.no_grad()
+    def set_style(self, s: torch.Tensor) -> None:
+        self.fs = self.vit_s(s)
+
+    @torch.no_grad()
+    def __call__(self, frame: torch.Tensor) -> torch.Tensor:
+        if self.fs is None:
+            raise RuntimeError("VideoStylizer: call set_style(style_image) first")
+        _, cs = self.ada(self.vit_c(frame), self.fs)
+        cs = cs.clamp(0, 255)
+        self.prev, self.cur = self.cur, cs
+        return cs
+
+    @torch.no_grad()
+    def warping_error(self, flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        if self.prev is None:
+            raise RuntimeError("VideoStylizer: need two frames")
+        return warping_error(self.prev / 255.0, self.cur / 255.0, flow, mask)

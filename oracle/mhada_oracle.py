@@ -396,3 +396,70 @@ def train_losses(content, style, p_vc, p_vs, p_ada, p_vgg):
     i1 = identity_loss_1(cc, content, ss, style) * LAMBDA["id1"]
     i2 = identity_loss_2(v["cc"], v["c"], v["ss"], v["s"]) * LAMBDA["id2"]
     return [gs, lf, i1, i2, gs + lf + i1 + i2]
+
+
+# --------------------------------------------------------------------------------------
+# video path: optical-flow warping (utilities.py:100-151, exps_sintel.py:101-109)
+# --------------------------------------------------------------------------------------
+def _warp_coords(flow_x: np.ndarray, flow_y: np.ndarray, padding: str):
+    """Sample coordinates of ``warp`` (utilities.py:104-117): vgrid = grid + flow normalised by
+    (W-1, H-1), then grid_sample's align_corners=False unnormalisation (fp32 op order)."""
+    H, W = flow_x.shape[-2:]
+    f32 = np.float32
+    xx = np.arange(W, dtype=f32)[None, :]
+    yy = np.arange(H, dtype=f32)[:, None]
+    gx = (f32(2.0) * (xx + flow_x)) / f32(max(W - 1, 1)) - f32(1.0)
+    gy = (f32(2.0) * (yy + flow_y)) / f32(max(H - 1, 1)) - f32(1.0)
+    ix = ((gx + f32(1)) * f32(W) - f32(1)) / f32(2)
+    iy = ((gy + f32(1)) * f32(H) - f32(1)) / f32(2)
+    if padding == "border":
+        ix = np.clip(ix, 0, W - 1).astype(f32)
+        iy = np.clip(iy, 0, H - 1).astype(f32)
+    elif padding != "zeros":
+        raise ValueError(padding)
+    return ix, iy
+
+
+def _bilinear_sample(plane: np.ndarray, ix: np.ndarray, iy: np.ndarray) -> np.ndarray:
+    """F.grid_sample bilinear on one [H, W] plane, zero outside (taps nw, ne, sw, se)."""
+    H, W = plane.shape
+    x0 = np.floor(ix)
+    y0 = np.floor(iy)
+    wts = ((x0 + 1 - ix) * (y0 + 1 - iy), (ix - x0) * (y0 + 1 - iy), (x0 + 1 - ix) * (iy - y0), (ix - x0) * (iy - y0))
+    x0i, y0i = x0.astype(np.int64), y0.astype(np.int64)
+    out = np.zeros(ix.shape, dtype=np.float32)
+    for (dx, dy), wt in zip(((0, 0), (1, 0), (0, 1), (1, 1)), wts):
+        xs, ys = x0i + dx, y0i + dy
+        ok = (xs >= 0) & (xs < W) & (ys >= 0) & (ys < H)
+        v = plane[np.clip(ys, 0, H - 1), np.clip(xs, 0, W - 1)]
+        out = out + np.where(ok, v * wt, np.float32(0)).astype(np.float32)
+    return out
+
+
+def warp(x: np.ndarray, flow: np.ndarray, padding: str = "zeros") -> np.ndarray:
+    """``warp`` (utilities.py:100-118): x [B,C,H,W], flow [B,2,H,W]."""
+    out = np.empty_like(x, dtype=np.float32)
+    for b in range(x.shape[0]):
+        ix, iy = _warp_coords(flow[b, 0], flow[b, 1], padding)
+        for c in range(x.shape[1]):
+            out[b, c] = _bilinear_sample(x[b, c].astype(np.float32), ix, iy)
+    return out
+
+
+def flow_warp_mask(flo01: np.ndarray, flo10: np.ndarray, threshold: float = 2) -> np.ndarray:
+    """``flow_warp_mask`` (utilities.py:121-151), zero padding: [2,H,W] flows -> [H,W] mask."""
+    H, W = flo01.shape[1:]
+    grid = np.stack((np.broadcast_to(np.arange(W, dtype=np.float32)[None, :], (H, W)),
+                     np.broadcast_to(np.arange(H, dtype=np.float32)[:, None], (H, W))))
+    field = grid + flo01
+    ix, iy = _warp_coords(flo10[0], flo10[1], "zeros")
+    err = np.abs(_bilinear_sample(field[0], ix, iy) - grid[0]) + np.abs(_bilinear_sample(field[1], ix, iy) - grid[1])
+    return (err < threshold).astype(np.float32)
+
+
+def warping_error(cs1: np.ndarray, cs2: np.ndarray, flow: np.ndarray, mask: np.ndarray) -> np.ndarray:
+    """exps_sintel.py:101-109 per image: sum(mask * |cs2 - warp(cs1, flow)|) / (C*H*W)."""
+    w = warp(cs1, flow)
+    B, C, H, W = cs1.shape
+    m = mask.reshape(B, 1, H, W)
+    return (np.abs(cs2.astype(np.float64) - w) * m).reshape(B, -1).sum(axis=1) / (C * H * W)

@@ -145,3 +145,26 @@ def test_oracle_training_losses_match_reference():
     fs = O.vgg19_forward(s, p[3])
     t4 = O.ada_attn_for_loss(fc["relu4_1"], fs["relu4_1"], O.feature_down_sample(fc, 4), O.feature_down_sample(fs, 4))
     np.testing.assert_allclose(t4, g["lf_target4"], rtol=1e-4, atol=1e-4)
+
+
+def test_oracle_warp_functions_match_reference():
+    """utilities.warp (both paddings), flow_warp_mask and the exps_sintel warping error."""
+    g = load_golden("video_warp")
+    for pad in ("zeros", "border"):
+        np.testing.assert_allclose(O.warp(g["x"], g["flow"], pad), g[f"warp_{pad}"], rtol=0, atol=1e-3)
+    np.testing.assert_array_equal(O.flow_warp_mask(g["flo01"], g["flo10"]), g["mask"])
+    err = O.warping_error(g["cs1"], g["cs2"], g["flow"][:1], g["mask"][None])
+    np.testing.assert_allclose(err, [g["warp_err"]], rtol=1e-5)
+
+
+def test_temporal_losses_match_reference():
+    """lossfn.output/feature_level_temporal_loss restated in mhada_hip.losses (autograd form)."""
+    from mhada_hip import losses as L
+    g = load_golden("video_warp")
+    t = {k: torch.from_numpy(g[k]) for k in ("c1", "c2", "cs1", "cs2", "flow", "mask", "f1", "f2")}
+    mse = torch.nn.MSELoss(reduction="none")
+    m = t["mask"].unsqueeze(0)
+    out = L.output_level_temporal_loss(t["c1"], t["c2"], t["cs1"] * 255, t["cs2"] * 255, t["flow"][:1], m, mse)
+    np.testing.assert_allclose(float(out), float(g["out_temporal"]), rtol=1e-5)
+    feat = L.feature_level_temporal_loss(t["f1"], t["f2"], t["flow"][:1], m, mse)
+    np.testing.assert_allclose(float(feat), float(g["feat_temporal"]), rtol=1e-5)
