@@ -27,6 +27,7 @@
 // onto one XCD so they share K/V in its L2.
 #include "common.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <type_traits>
 
@@ -45,6 +46,8 @@ struct AttnP {
   const float* v_mu;
   void* out;        // [B][Nc][C]
   int B, H, Nc, Ns, ldt, nqb, nblk;
+  unsigned long long* stamps;  // diagnostics only (MHADA_ATTN_STAMPS): s_memtime per barrier
+  int dbg;                     // diagnostics only (MHADA_ATTN_DBG): 1 = no LDS-DMA in the loop
 };
 
 MHADA_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -462,6 +465,238 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_bf16_kernel(con
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
 }
 
+// --------------------------------------------------------------------------------------
+// bf16 ping-pong variant.  The plain kernel's per-tile __syncthreads keeps the two waves of a
+// SIMD in the same phase — both issue QK^T, then both run the softmax (matrix pipe idle), then
+// both issue PV (PMC: 42 % of wave time parked at waitcnt/barrier, MFMA busy 44 %).  Here each
+// wave software-pipelines one tile: an MFMA segment {QK^T(u), PV(u-1)} and a VALU segment
+// {softmax(u) -> P(u)}, separated by s_barrier, and waves 4-7 (group B) run one barrier behind
+// waves 0-3 (group A), so on every SIMD one wave's MFMA segment pairs with the other wave's
+// VALU segment (cdna_hip_programming.md T15/T16 in ping-pong form).
+// K/V tiles arrive by LDS-DMA (global_load_lds, 16 B per lane) into 2-slot rings of unpadded
+// 128-B rows, chunk slot = chunk ^ ((row >> 1) & 7) (applied on the source address; conflict-free
+// 32x32x16 operand reads).  Each group moves its own half of every tile (A: K rows 0-31 and
+// V'^T rows 0-63, B: the rest).  With A's segments at barrier intervals 2u (MFMA) / 2u+1 (VALU)
+// and B's at 2u+1 / 2u+2:
+//   A issues K(u+1), V(u) at the start of MFMA(u)  (slots last read in intervals 2u-2 / 2u-1),
+//     waits vmcnt(0) at the end of VALU(u)         (first reader: A's MFMA(u+1), interval 2u+2);
+//   B issues K(u+2), V(u+1) at the start of VALU(u) (slots last read in 2u / 2u+1),
+//     waits vmcnt(0) at the end of MFMA(u+1)        (first reader: A's MFMA(u+2), interval 2u+4).
+// Every LDS read retires (lgkmcnt(0)) before its segment's barrier; the DMAs stay in flight
+// across one barrier (raw s_barrier: __syncthreads would drain them).
+// Online-softmax rescale: decided in VALU(u) after PV(u-1) has been issued, so it scales O with
+// every P at the old max included exactly once (T13's hazard), then P(u) uses the new max.
+#define PPA_BARRIER()                                    \
+  do {                                                   \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    __builtin_amdgcn_s_barrier();                        \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    asm volatile("" ::: "memory");                       \
+  } while (0)
+
+MHADA_DEV void attn_glds16(const void* src, bf16* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(512) attn_bf16_pp_kernel(const AttnP p) {
+  constexpr int KSZ = 64 * 64, VSZ = 128 * 64;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * KSZ + 2 * VSZ];  // the only LDS object
+  bf16* const sK = smem;            // [2][64 keys][64 d]
+  bf16* const sV = smem + 2 * KSZ;  // [2][128 dv][64 keys]
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wl = wave & 3;
+  const int q = qb * 256 + wave * 32 + r32;
+  const long long bh = (long long)b * p.H + hh;
+  const int Ns = p.Ns, NTILE = (Ns + 63) / 64;
+
+  bf16x8 qf[4];
+  {
+    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+      if (q >= p.Nc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
+      }
+    }
+  }
+  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
+  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
+
+  // One LDS-DMA piece = 8 rows x 128 B; lane l fills row (l >> 3), slot (l & 7).
+  auto k_piece = [&](int kt, int row0) {  // rows row0..row0+7 of K(kt); keys past Ns clamped
+    const int row = row0 + (lane >> 3);  // (their scores are masked)
+    const int key = min(kt * 64 + row, Ns - 1);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    attn_glds16(kvb + (long long)key * 128 + 8 * c, sK + (kt & 1) * KSZ + row0 * 64);
+  };
+  auto v_piece = [&](int vtile, int row0) {  // dv rows row0..row0+7 of the V'^T tile vtile
+    const int row = row0 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    attn_glds16(vtb + (long long)row * p.ldt + vtile * 64 + 8 * c, sV + (vtile & 1) * VSZ + row0 * 64);
+  };
+  // this group's half of K(kt) (4 pieces) and V(vtile) (8 pieces): 3 pieces per wave
+  auto dma = [&](int kt, int vtile) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int gi = wl * 3 + j;  // wave-uniform
+      if (gi < 4) {
+        if (kt < NTILE) k_piece(kt, 32 * grp + 8 * gi);
+      } else {
+        if (vtile < NTILE) v_piece(vtile, 64 * grp + 8 * (gi - 4));
+      }
+    }
+  };
+
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
+  float m2 = -INFINITY, l = 0.f;
+  f32x16 S[2];
+  bf16x8 pf[2][2];
+
+  // element offset of this lane's 16-B chunk 2j + h inside a swizzled row (rows r32 + 32k
+  // share it); indexed only with compile-time j (a runtime index becomes a select chain)
+  const int swz = (r32 >> 1) & 7;
+  int koff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) koff[j] = 8 * ((2 * j + h) ^ swz);
+  // diagnostics: lane 0 of each wave of the first block stamps s_memtime after its barriers
+  int nst = 0;
+  auto stamp = [&]() {
+    if (p.stamps && blockIdx.x == 0 && lane == 0 && nst < 96) p.stamps[wave * 96 + nst] = __builtin_amdgcn_s_memtime();
+    ++nst;
+  };
+  // MFMA segment body: all operand fragments are read in batches ahead of their MFMAs (with
+  // one MFMA-issuing wave per SIMD nothing else hides a ds_read's latency).
+  auto mfma_segment = [&](const bf16* ck, const bf16* cv, bool with_pv) {
+    bf16x8 kf[2][4], vf[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        kf[kb][s2] = *reinterpret_cast<const bf16x8*>(ck + (kb * 32 + r32) * 64 + koff[s2]);
+    if (with_pv) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk)
+          vf[s2][blk] = *reinterpret_cast<const bf16x8*>(cv + (r32 + 32 * blk) * 64 + koff[s2]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMAs (the scheduler sinks them)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[kb][e] = 0.f;
+    // the two score chains alternate: a chain's next MFMA never waits on its previous result
+    // (with one MFMA wave per SIMD nothing else fills that latency)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][s2], qf[s2], S[kb], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA, in this order
+      }
+    if (p.stamps) { __builtin_amdgcn_sched_barrier(0); stamp(); __builtin_amdgcn_sched_barrier(0); }
+    if (with_pv) {
+      // the second key block's V fragments reuse the K fragments' registers (dead once the
+      // QK^T MFMAs have issued) and are in flight while the first block's PV MFMAs run
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk)
+          kf[s2][blk] = *reinterpret_cast<const bf16x8*>(cv + (r32 + 32 * blk) * 64 + koff[2 + s2]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk)
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s2][blk], pf[0][s2], O[blk], 0, 0, 0);
+      if (p.stamps) { __builtin_amdgcn_sched_barrier(0); stamp(); __builtin_amdgcn_sched_barrier(0); }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk)
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s2][blk], pf[1][s2], O[blk], 0, 0, 0);
+    }
+  };
+  auto pv_only = [&](const bf16* cv) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+          const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(cv + (r32 + 32 * blk) * 64 + koff[2 * kb + s2]);
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v8, pf[kb][s2], O[blk], 0, 0, 0);
+        }
+  };
+
+  // prologue: K(0) whole (one piece per wave), group B's halves of K(1) and V(0)
+  k_piece(0, 8 * wave);
+  if (grp == 1) dma(1, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (grp == 1) PPA_BARRIER();  // group B runs one barrier behind
+
+  stamp();
+  auto tile = [&](int u, auto MASKC) {
+    // ---- MFMA segment: QK^T(u), PV(u-1)
+    if (grp == 0 && !(p.dbg & 1)) dma(u + 1, u);
+    mfma_segment(sK + (u & 1) * KSZ, sV + ((u - 1) & 1) * VSZ, u > 0);
+    if (p.stamps) { __builtin_amdgcn_sched_barrier(0); stamp(); __builtin_amdgcn_sched_barrier(0); }
+    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B's DMA from VALU(u-1)
+    PPA_BARRIER();
+    stamp();
+    // ---- VALU segment: softmax(u) -> P(u)
+    if (grp == 1 && !(p.dbg & 1)) dma(u + 2, u + 1);
+    if constexpr (decltype(MASKC)::value) mask_tile<ACT, 2>(S, u * 64, Ns, h);
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+      const float mx = tile_max_log2<2>(S);
+      if (__any(mx > m2 + kRescaleThr)) {
+        const float mn = fmaxf(m2, mx);
+        const float alpha = fast_exp2(m2 - mn);
+        l *= alpha;
+        scale_acc(O, alpha);
+        m2 = mn;
+      }
+    }
+    softmax_apply<ACT, 2>(S, m2, l);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[kb][s2][j] = (bf16)S[kb][8 * s2 + j];
+    if (p.stamps) { __builtin_amdgcn_sched_barrier(0); stamp(); __builtin_amdgcn_sched_barrier(0); }
+    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A's DMA from MFMA(u)
+    PPA_BARRIER();
+    stamp();
+  };
+  const int NFULL = Ns / 64;
+  for (int u = 0; u < NFULL; ++u) tile(u, std::false_type{});
+  if (NFULL < NTILE) tile(NFULL, std::true_type{});  // ragged last tile: key masks
+  pv_only(sV + ((NTILE - 1) & 1) * VSZ);
+  if (grp == 0) PPA_BARRIER();  // balance group B's extra barrier
+  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
+}
+
+// Opt-in (MHADA_ATTN_PP=1): measured 10-20 % slower than the plain 128-key kernel.
+static bool attn_pp_enabled() {
+  const char* e = getenv("MHADA_ATTN_PP");
+  return e && e[0] == '1';
+}
+
 // Waves per workgroup (32 queries each).  Default per dtype; MHADA_ATTN_WAVES=4|8 overrides
 // (read per call, for in-process A/B measurements).
 static int attn_waves(int dtype) {
@@ -486,6 +721,15 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
     else
       hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
   } else {
+    if constexpr (NW == 8) {
+      if (attn_pp_enabled()) {
+        if (activation == MHADA_ACT_SOFTMAX)
+          hipLaunchKernelGGL((attn_bf16_pp_kernel<MHADA_ACT_SOFTMAX>), grid, blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((attn_bf16_pp_kernel<MHADA_ACT_COSINE>), grid, blk, 0, s, p);
+        return;
+      }
+    }
     const bool t128 = NW == 8 && attn_tk() == 128;  // 2 x 106 KiB of LDS does not fit a CU
     if (activation == MHADA_ACT_SOFTMAX) {
       if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
@@ -512,6 +756,13 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   AttnP p;
   p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
   p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
+  p.stamps = nullptr;
+  p.dbg = getenv("MHADA_ATTN_DBG") ? atoi(getenv("MHADA_ATTN_DBG")) : 0;
+  const bool stamps = getenv("MHADA_ATTN_STAMPS") != nullptr;
+  if (stamps) {
+    (void)hipMalloc((void**)&p.stamps, 8 * 96 * sizeof(unsigned long long));
+    (void)hipMemsetAsync(p.stamps, 0, 8 * 96 * sizeof(unsigned long long), s);
+  }
   p.ldt = (Ns + 63) / 64 * 64;
   const int nw = attn_waves(dtype);
   p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
@@ -522,6 +773,17 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
     launch_attn<8>(p, dtype, activation, s);
   } else {
     launch_attn<4>(p, dtype, activation, s);
+  }
+  if (stamps) {  // diagnostics: per-wave cycles between consecutive barrier stamps of block 0
+    unsigned long long h[8 * 96];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, p.stamps, sizeof(h), hipMemcpyDeviceToHost);
+    for (int w = 0; w < 8; ++w) {
+      fprintf(stderr, "wave %d:", w);
+      for (int k = 1; k < 96 && h[w * 96 + k]; ++k) fprintf(stderr, " %llu", h[w * 96 + k] - h[w * 96 + k - 1]);
+      fprintf(stderr, "\n");
+    }
+    (void)hipFree(p.stamps);
   }
   return check_launch("mhada_attn");
 }

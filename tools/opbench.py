@@ -102,13 +102,14 @@ def attn_suite():
         fcs = torch.randn(B, n, 512, device=dev)
         mu, rs = ops.instnorm_stats(fcs)
         vmu = torch.zeros(B, 512, device=dev)
-        def run(nw, tk=128):
+        def run(nw, tk=128, pp=0):
             def f():
                 os.environ["MHADA_ATTN_WAVES"] = str(nw)
                 os.environ["MHADA_ATTN_TK"] = str(tk)
+                os.environ["MHADA_ATTN_PP"] = str(pp)
                 ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
             return f
-        fns = {"attn_w4": run(4), "attn_w8_tk64": run(8, 64), "attn_w8_tk128": run(8, 128)}
+        fns = {"pingpong": run(8, 64, 1), "w8_tk64": run(8, 64), "w8_tk128": run(8, 128)}
         t = bench(fns, rounds=5, iters=3)
         # the variants must agree
         outs = {k: (f(), ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0))[1] for k, f in fns.items()}
@@ -118,6 +119,7 @@ def attn_suite():
             print(f"   variant {k}: rel diff vs first {err:.2e}")
         os.environ.pop("MHADA_ATTN_WAVES", None)
         os.environ.pop("MHADA_ATTN_TK", None)
+        os.environ.pop("MHADA_ATTN_PP", None)
         fl = 6 * n * n * 512 * B
         print(f"attn {str(dt)[6:]:8s} B={B} N={n}: " + "  ".join(f"{k} {v:7.3f} ms {fl / v / 1e9:7.1f} TF"
                                                                for k, v in t.items()))
