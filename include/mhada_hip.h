@@ -100,14 +100,15 @@ int mhada_instnorm_stats(const float* x, float* mu, float* rstd, double* work, i
 /* Fold the InstanceNorm scale into the per-head 1x1-conv weights of one AdaAttnMultiHead
  * block (adaDecoder.py:173,178,182) and derive the style-side mean of V:
  *   wq[b][h][o][c]  = Wf[h][o][c] * rstd_c[b][64h+c]            (A is centred on load)
- *   wkv[b][h][o][c] = o<64 ? Wg[h][o][c] * rstd_s[b][64h+c] : Wh[h][o-64][c]
- *   bkv[h][o]       = o<64 ? bg[h][o] : 0                        (V' = V - mean_tokens(V))
+ *   wkv[b][h][o][c] = o<64 ? Wg[h][o][c] * rstd_s[b][64h+c] * kscale : Wh[h][o-64][c]
+ *   bkv[h][o]       = o<64 ? bg[h][o] * kscale : 0               (V' = V - mean_tokens(V))
  *   v_mu[b][64h+o]  = sum_c Wh[h][o][c] * mu_s[b][64h+c] + bh[h][o]
+ * kscale = log2(e) for the softmax activation (mhada_attn's K contract), 1 for cosine.
  * W* fp32 [H][64][64]; wq/wkv dtype `dtype`. */
 int mhada_fold_block(const float* wf, const float* wg, const float* wh, const float* bg,
                      const float* bh, const float* rstd_c, const float* mu_s,
                      const float* rstd_s, void* wq, void* wkv, float* bkv, float* v_mu,
-                     int dtype, int B, int H, mhada_stream_t stream);
+                     float kscale, int dtype, int B, int H, mhada_stream_t stream);
 
 /* bf16 path: the transposed operand image the attention kernel streams, from kv [B][H][Ns][128]:
  * VT[b][h][o][pos(n)] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), row stride
@@ -125,6 +126,8 @@ int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns
  *   A = softmax(Q K^T) (no 1/sqrt(d); or the cosine form), M = A V, E2 = A V^2,
  *   S = sqrt(max(E2 - M^2, 1e-6)), out = S * IN(fcs) + M
  * computed flash-style (A never materialised) with V centred (v_mu added back to M).
+ * Softmax: the K half of kv carries the factor log2(e) (mhada_fold_block kscale), so Q.K^T is
+ * the logit in log2 units and P = exp2(Q.K^T - max).
  * q [B][H][Nc][64], kv [B][H][Ns][128] (K | V'), vt (bf16 only) [B][H][128][Ns],
  * fcs [B][Nc][64H] fp32 with its stats fcs_mu/fcs_rstd [B][64H], v_mu [B][64H];
  * out [B][Nc][64H] dtype. */

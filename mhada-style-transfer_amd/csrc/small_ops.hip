@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf,
                                                    const float* __restrict__ bh, const float* __restrict__ rstd_c,
                                                    const float* __restrict__ mu_s, const float* __restrict__ rstd_s,
                                                    T* __restrict__ wq, T* __restrict__ wkv, float* __restrict__ bkv,
-                                                   float* __restrict__ v_mu, int H) {
+                                                   float* __restrict__ v_mu, float kscale, int H) {
   constexpr int D = 64;
   const int b = blockIdx.x / H, hh = blockIdx.x - (blockIdx.x / H) * H;
   const int C = H * D;
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf,
   for (int i = threadIdx.x; i < D * D; i += 256) {
     const int c = i & (D - 1);
     oq[i] = from_f32<T>(Wf[i] * rc[c]);
-    okv[i] = from_f32<T>(Wg[i] * rs[c]);
+    okv[i] = from_f32<T>(Wg[i] * rs[c] * kscale);
     okv[D * D + i] = from_f32<T>(Wh[i]);
   }
   if (threadIdx.x < D) {
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf,
     for (int c = 0; c < D; ++c) acc += Wh[o * D + c] * ms[c];
     v_mu[(long long)b * C + hh * D + o] = acc;
     if (b == 0) {
-      bkv[hh * 2 * D + o] = bg[hh * D + o];
+      bkv[hh * 2 * D + o] = bg[hh * D + o] * kscale;
       bkv[hh * 2 * D + D + o] = 0.f;
     }
   }
@@ -455,17 +455,17 @@ extern "C" int mhada_instnorm_stats(const float* x, float* mu, float* rstd, doub
 
 extern "C" int mhada_fold_block(const float* wf, const float* wg, const float* wh, const float* bg, const float* bh,
                                 const float* rstd_c, const float* mu_s, const float* rstd_s, void* wq, void* wkv,
-                                float* bkv, float* v_mu, int dtype, int B, int H, mhada_stream_t s_) {
+                                float* bkv, float* v_mu, float kscale, int dtype, int B, int H, mhada_stream_t s_) {
   hipStream_t s = (hipStream_t)s_;
   if (!wf || !wg || !wh || !bg || !bh || !rstd_c || !mu_s || !rstd_s || !wq || !wkv || !bkv || !v_mu || B <= 0 ||
       H <= 0)
     return fail("mhada_fold_block: bad args");
   if (dtype == MHADA_F32)
     hipLaunchKernelGGL((fold_kernel<float>), dim3(B * H), dim3(256), 0, s, wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s,
-                       (float*)wq, (float*)wkv, bkv, v_mu, H);
+                       (float*)wq, (float*)wkv, bkv, v_mu, kscale, H);
   else
     hipLaunchKernelGGL((fold_kernel<bf16>), dim3(B * H), dim3(256), 0, s, wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s,
-                       (bf16*)wq, (bf16*)wkv, bkv, v_mu, H);
+                       (bf16*)wq, (bf16*)wkv, bkv, v_mu, kscale, H);
   return check_launch("mhada_fold_block");
 }
 

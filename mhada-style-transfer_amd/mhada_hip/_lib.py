@@ -47,7 +47,7 @@ SIGNATURES = {
     "mhada_vit_batch_attn": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_pos_embed": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_instnorm_stats": (_I, [_vp, _vp, _vp, _vp, _I, _I, _I, _I, _F, _vp]),
-    "mhada_fold_block": (_I, [_vp] * 12 + [_I, _I, _I, _vp]),
+    "mhada_fold_block": (_I, [_vp] * 12 + [_F, _I, _I, _I, _vp]),
     "mhada_transpose_v": (_I, [_vp, _vp, _I, _I, _I, _vp]),
     "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),

@@ -246,14 +246,14 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
         raise ValueError(f"channel mismatch: block expects {C}")
     mu_c, rstd_c = fc.stats()
     mu_o, rstd_o = fcs.stats()
+    act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
     wq, wkv, bkv, v_mu = ops.fold_block(prep["wf"], prep["wg"], prep["wh"], prep["bg"], prep["bh"],
-                                        rstd_c, mu_s, rstd_s, dt)
+                                        rstd_c, mu_s, rstd_s, dt, ops.LOG2E if act == ACT_SOFTMAX else 1.0)
     dev = fc.t.device
     q = torch.empty(B, H, Nc, HEAD_DIM, device=dev, dtype=dt)
     ops.gemm(a=fc.t, w=wq, c=q, M=Nc, N=HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Nc * C, HEAD_DIM),
              nb=(B, H), a_mu=mu_c, smu=(C, HEAD_DIM), ldw=HEAD_DIM, sw=(H * HEAD_DIM * HEAD_DIM, HEAD_DIM * HEAD_DIM),
              bias=prep["bf"], sb=(0, HEAD_DIM), ldc=HEAD_DIM, sc=(H * Nc * HEAD_DIM, Nc * HEAD_DIM))
-    act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
     if not cached:
         Ns = fs.t.shape[1]
         kv = torch.empty(B, H, Ns, 2 * HEAD_DIM, device=dev, dtype=dt)

@@ -178,7 +178,12 @@ def instnorm_stats(x: torch.Tensor, eps: float = 1e-5):
     return mu, rstd
 
 
-def fold_block(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s, dtype: torch.dtype):
+LOG2E = 1.4426950408889634
+
+
+def fold_block(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s, dtype: torch.dtype, kscale: float = LOG2E):
+    """Per-call weight fold of one MHAda block (include/mhada_hip.h).  kscale = log2(e) puts K
+    in the softmax attention's log2 units (mhada_attn's K contract); 1.0 for cosine."""
     B, C = rstd_c.shape
     H = wf.shape[0]
     dev = wf.device
@@ -188,7 +193,7 @@ def fold_block(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s, dtype: torch.dtype):
     v_mu = torch.empty(B, C, device=dev, dtype=torch.float32)
     rc = _lib.load().mhada_fold_block(wf.data_ptr(), wg.data_ptr(), wh.data_ptr(), bg.data_ptr(), bh.data_ptr(),
                                       rstd_c.data_ptr(), mu_s.data_ptr(), rstd_s.data_ptr(), wq.data_ptr(),
-                                      wkv.data_ptr(), bkv.data_ptr(), v_mu.data_ptr(), dt_code(dtype), B, H,
+                                      wkv.data_ptr(), bkv.data_ptr(), v_mu.data_ptr(), kscale, dt_code(dtype), B, H,
                                       _stream())
     _lib.check(rc, "mhada_fold_block")
     return wq, wkv, bkv, v_mu

@@ -236,3 +236,43 @@ def test_mhada_is_per_sample_independent():
         y = blk(fc, fs, fc)
         y1 = blk(fc[1:2], fs[1:2], fc[1:2])
     assert rel(y[1:2], y1) < 1e-6
+
+
+def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
+    """fp64 mhada_attn (include/mhada_hip.h): K carries log2(e), so the natural-unit logit is
+    (q.k) * ln 2; out = sqrt(max(E[v'^2] - E[v']^2, 1e-6)) * (fcs - mu) * rstd + E[v'] + v_mu."""
+    B, H, Nc, _ = q.shape
+    qd, kd, vd = q.double(), kv[..., :64].double(), kv[..., 64:].double()
+    a = torch.softmax(qd @ kd.transpose(-1, -2) * math.log(2.0), dim=-1)
+    m = a @ vd
+    e2 = a @ (vd * vd)
+    s = torch.sqrt(torch.clamp(e2 - m * m, min=1e-6))
+    out = s.permute(0, 2, 1, 3).reshape(B, Nc, H * 64)
+    mm = m.permute(0, 2, 1, 3).reshape(B, Nc, H * 64)
+    f = (fcs.double() - mu.double()[:, None]) * rstd.double()[:, None]
+    return out * f + mm + v_mu.double()[:, None]
+
+
+@pytest.mark.parametrize("kernel", ["fs", "w8"])
+@pytest.mark.parametrize("Nc,Ns", [(300, 700), (256, 128), (97, 33)])
+def test_mhada_attn_late_max_jump(kernel, Nc, Ns, monkeypatch):
+    """A key far beyond the first tile's scores (> 2^64 in P against the first tile's max): the
+    fixed-shift kernel ("fs", attn.hip) must take its exact-recompute path, the online-max
+    kernel ("w8") its rescale branch; both against fp64 torch on the same bf16 operands."""
+    monkeypatch.setenv("MHADA_ATTN_KERNEL", kernel)
+    B, H = 1, 8
+    q = rnd(B, H, Nc, 64, seed=11)
+    q = q / q.norm(dim=-1, keepdim=True) * 4.0
+    kv = rnd(B, H, Ns, 128, scale=0.1, seed=12)
+    late = Ns - 5  # in the last key tile
+    kv[:, :, late, :64] = 30.0 * q[:, :, : min(Nc, 1), :].mean(dim=2)  # ~120 log2 units above
+    kv[:, :, late - 1, :64] = -kv[:, :, late, :64]
+    q, kv = q.bfloat16(), kv.bfloat16()
+    vt = ops.transpose_v(kv)
+    fcs = rnd(B, Nc, 512, seed=13)
+    mu, rs = ops.instnorm_stats(fcs)
+    vmu = rnd(B, 512, seed=14)
+    y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+    ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
+    assert torch.isfinite(y.float()).all()
+    assert rel(y.float(), ref) < 1.5e-2

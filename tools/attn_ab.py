@@ -1,0 +1,63 @@
+"""A/B of the bf16 MHAda attention kernel variants (MHADA_ATTN_* switches, attn.hip) in one process:
+agreement on the same operands and interleaved timing (median of rounds) at the bench shapes.
+
+    python tools/attn_ab.py
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd")]
+
+import torch
+
+from mhada_hip import ops
+
+SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1080p/s256", 1, 32400, 1024),
+          ("ragged", 2, 1000, 777)]
+
+
+VARIANTS = {"fs": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128", "MHADA_ATTN_PRIO": "1"},
+            "fs_noprio": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128", "MHADA_ATTN_PRIO": "0"},
+            "fs64": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "64", "MHADA_ATTN_PRIO": "1"},
+            "w8": {"MHADA_ATTN_KERNEL": "w8", "MHADA_ATTN_TK": "128"}}
+
+
+def run(variant, args):
+    os.environ.update(VARIANTS[variant])
+    return ops.mhada_attn(*args, 0)
+
+
+def main():
+    torch.manual_seed(0)
+    H = 8
+    for name, B, nc, ns in SHAPES:
+        q = (torch.randn(B, H, nc, 64, device="cuda") * 0.35).bfloat16()
+        kv = (torch.randn(B, H, ns, 128, device="cuda") * 0.35).bfloat16()
+        vt = ops.transpose_v(kv)
+        fcs = torch.randn(B, nc, 512, device="cuda")
+        mu, rs = ops.instnorm_stats(fcs)
+        vmu = torch.zeros(B, 512, device="cuda")
+        args = (q, kv, vt, fcs, mu, rs, vmu)
+        ref = run("w8", args).float()
+        errs = {v: ((run(v, args).float() - ref).abs().max() / ref.abs().max()).item() for v in VARIANTS}
+        times = {v: [] for v in VARIANTS}
+        for _ in range(7):
+            for v in VARIANTS:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(5):
+                    run(v, args)
+                e.record()
+                torch.cuda.synchronize()
+                times[v].append(s.elapsed_time(e) / 5)
+        med = {k: sorted(v)[3] for k, v in times.items()}
+        fl = 6.0 * nc * ns * 512 * B
+        print(f"{name:18s} " + "   ".join(f"{v} {med[v]:.3f} ms {fl / med[v] / 1e9:.0f} TF (err {errs[v]:.1e})"
+                                           for v in VARIANTS), flush=True)
+    for k in ("MHADA_ATTN_KERNEL", "MHADA_ATTN_PRIO", "MHADA_ATTN_TK"):
+        os.environ.pop(k, None)
+
+
+if __name__ == "__main__":
+    main()
