@@ -14,6 +14,7 @@
 // LDS after them (register-staged async split).
 #include "common.h"
 
+#include <algorithm>
 #include <mutex>
 #include <stdlib.h>
 
@@ -591,6 +592,206 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
   store_tile<TO, 4, 2>(p, acc, z1, z2, m0 + grp * 128 + r32, n0 + wc * 64, h);
 }
 
+// ------------------------------------------------------------------------------------
+// Persistent form of the ping-pong kernel: one workgroup per CU walks work items
+// w = blockIdx.x + i * gridDim.x (tile x z-batch, dealt to XCDs as a one-shot launch of
+// `total` blocks would be, then xcd_remap'ed so an XCD's 32 concurrent tiles share A rows and
+// W in its L2).  The K-tile stream is continuous across tiles: the ring slot is the global
+// K-tile counter's parity and the lookahead stages (W one K-tile ahead, A two) reach into the
+// NEXT tile's first K-tiles, so the next tile's operands are in flight while this tile's
+// last phases and its epilogue run — the one-shot kernel pays the HBM latency of every
+// tile's prologue and drains the CU at every epilogue (K = 512: 8 K-tiles per tile).
+// Needs K >= 128 (two K-tiles: the A lookahead never skips a whole tile).
+// ------------------------------------------------------------------------------------
+template <typename TO, int AMODE>
+__global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total) {
+  constexpr int BK = 64, HALF = 128 * BK, TILE = 4 * HALF;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];  // 128 KiB, the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wc = wave & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int G = gridDim.x;
+
+  int cofs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) cofs[i] = 8 * ((lane & 7) ^ (4 * i + (lane >> 4)));
+  // per-tile staging state (rows 16*wave + 8i + (lane>>3) of each 128-row half)
+  struct St {
+    const bf16* ab;
+    const bf16* wb;
+    unsigned aoff[2][2], woff[2][2];
+    int b[2][2], y[2][2], x[2][2];
+    int m0, n0, z1, z2;
+  };
+  auto setup = [&](int w, St& s) {
+    const int lg = xcd_remap(w, total);
+    const int z = lg / p.ntiles, t = lg - z * p.ntiles;
+    s.z1 = z / p.nb2;
+    s.z2 = z - s.z1 * p.nb2;
+    const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
+    s.m0 = tm * 256;
+    s.n0 = tn * 256;
+    s.ab = reinterpret_cast<const bf16*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2;
+    s.wb = reinterpret_cast<const bf16*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rr = 16 * wave + 8 * i + (lane >> 3);
+        const int m = min(s.m0 + 128 * hh + rr, p.M - 1);
+        const int n = min(s.n0 + 128 * hh + rr, p.N - 1);
+        s.woff[hh][i] = (unsigned)((long long)n * p.ldw + cofs[i]);
+        if constexpr (AMODE == MHADA_A_ROWS) {
+          s.aoff[hh][i] = (unsigned)((long long)m * p.lda + cofs[i]);
+        } else {
+          const int hw = p.out_h * p.out_w;
+          const int b = m / hw, rem = m - b * hw;
+          s.b[hh][i] = b;
+          s.y[hh][i] = rem / p.out_w;
+          s.x[hh][i] = rem - (rem / p.out_w) * p.out_w;
+          s.aoff[hh][i] = 0;
+        }
+      }
+  };
+  auto stage_a = [&](const St& s, int hh, int kt, int slot) {
+    bf16* dst = smem + slot * TILE + hh * HALF + wave * 1024;
+    const int k0 = kt * BK;
+    if constexpr (AMODE == MHADA_A_ROWS) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(s.ab + s.aoff[hh][i] + k0, dst + 512 * i);
+    } else {
+      const int cin_n = p.img_c;
+      const int tap = k0 / cin_n, cin0 = k0 - tap * cin_n;
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int Y = reflect1(s.y[hh][i] + dy, p.out_h), X = reflect1(s.x[hh][i] + dx, p.out_w);
+        const unsigned off = (unsigned)(((s.b[hh][i] * p.img_h + Y) * p.img_w + X) * cin_n + cin0 + cofs[i]);
+        glds16(s.ab + off, dst + 512 * i);
+      }
+    }
+  };
+  auto stage_w = [&](const St& s, int hh, int kt, int slot) {
+    bf16* dst = smem + slot * TILE + (2 + hh) * HALF + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(s.wb + s.woff[hh][i] + kt * BK, dst + 512 * i);
+  };
+
+  const int swz = (r32 >> 1) & 7;
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = 8 * ((2 * ks + h) ^ swz);
+  const bf16* sA = smem + grp * HALF + r32 * 64;
+  const bf16* sW = smem + (2 + (wc >> 1)) * HALF + ((wc & 1) * 64 + r32) * 64;
+  bf16x8 af[4][2], wf[2][2];
+  auto read_a = [&](int kp, int cb) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        af[mt][s2] = *reinterpret_cast<const bf16x8*>(sA + cb * TILE + mt * 2048 + koff[2 * kp + s2]);
+  };
+  auto read_w = [&](int nt, int kp, int cb) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      wf[nt][s2] = *reinterpret_cast<const bf16x8*>(sW + cb * TILE + nt * 2048 + koff[2 * kp + s2]);
+  };
+  f32x16 acc[4][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  };
+  auto compute = [&](int nt) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[nt][s2], af[mt][s2], acc[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const int dbg = 0;
+
+  const int KT = p.K / BK;
+  int w = blockIdx.x;
+  St cur, nxt;
+  setup(w, cur);
+  bool has_nxt = w + G < total;
+  if (has_nxt) setup(w + G, nxt);
+  zero_acc();
+  stage_a(cur, 0, 0, 0); stage_a(cur, 1, 0, 0); stage_w(cur, 0, 0, 0); stage_w(cur, 1, 0, 0);
+  stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  PP_BARRIER();
+  if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
+
+  int g = 0;  // global K-tile counter: ring slot g & 1
+  while (true) {
+    for (int kt = 0; kt < KT; ++kt, ++g) {
+      const int cb = g & 1;
+      // sources of K-tiles g+1 (W) and g+2 (A): this tile or the next one
+      const bool w1 = kt + 1 < KT || has_nxt;
+      const St& s1 = kt + 1 < KT ? cur : nxt;
+      const int k1 = kt + 1 < KT ? kt + 1 : 0;
+      const bool a2 = kt + 2 < KT || has_nxt;
+      const St& s2 = kt + 2 < KT ? cur : nxt;
+      const int k2 = kt + 2 < KT ? kt + 2 : kt + 2 - KT;
+      // phase 0
+      read_a(0, cb); read_w(0, 0, cb);
+      if (w1) stage_w(s1, 0, k1, cb ^ 1);
+      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+      // phase 1
+      read_w(1, 0, cb);
+      if (w1) stage_w(s1, 1, k1, cb ^ 1);
+      PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+      // phase 2
+      read_a(1, cb); read_w(0, 1, cb);
+      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+      // phase 3
+      read_w(1, 1, cb);
+      if (a2) {
+        stage_a(s2, 0, k2, cb); stage_a(s2, 1, k2, cb);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+    }
+    // tile boundary: re-align the groups so both store in the same interval (a store between
+    // staggered barriers would hold the other group's compute phase), then re-stagger
+    if (grp == 0) PP_BARRIER();
+    store_tile<TO, 4, 2>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * 64, h);
+    if (!has_nxt) break;
+    if (grp == 1) PP_BARRIER();
+    zero_acc();
+    cur = nxt;
+    w += G;
+    has_nxt = w + G < total;
+    if (has_nxt) setup(w + G, nxt);
+  }
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// MHADA_GEMM_PERSIST=0 selects the one-shot ping-pong kernel (A/B runs; read per call).
+static bool persist_enabled() {
+  const char* e = getenv("MHADA_GEMM_PERSIST");
+  return !(e && e[0] == '0');
+}
+
 template <typename TO, int AMODE>
 static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
@@ -598,6 +799,12 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   p.dbg = dbg ? atoi(dbg) : 0;
   p.tiles_n = (p.N + 255) / 256;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
+  const long long total = (long long)p.ntiles * nz;
+  if (p.K >= 128 && persist_enabled() && total < (1LL << 31)) {
+    const int grid = (int)std::min<long long>(total, num_cus());
+    hipLaunchKernelGGL((gemm_ppp_kernel<TO, AMODE>), dim3(grid), dim3(512), 0, stream, p, (int)total);
+    return check_launch("mhada_gemm");
+  }
   hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
   return check_launch("mhada_gemm");
 }

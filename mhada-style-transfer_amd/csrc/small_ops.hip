@@ -4,6 +4,8 @@
 // (Cin -> 3) decoder convolution.  All activations are token-major.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace mhada {
 
 // ---------------------------------------------------------------------------------------
@@ -335,6 +337,104 @@ __global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------------
+// bf16 form of the last decoder layer on MFMA (v_mfma_f32_16x16x32_bf16).  A workgroup walks a
+// strip of kOut3Rows 4-row x 64-pixel output tiles (the weight fragments are loaded once per
+// strip); per tile the reflect-padded 6 x 66-pixel input halo is staged in LDS (double
+// buffered, the next halo in flight in registers during the MFMAs) (pixel rows padded to CIN+8 elements: the 16-lane groups' 16-B reads hit distinct bank
+// slots) and read 9x (one per tap) from there.  Per 16 output pixels the wave accumulates
+// D^T (16 out-channels x 16 pixels) = W^T (16 x 32 cin) . X^T (32 cin x 16 pixels) over the 9
+// taps x CIN/32 channel chunks; out-channels 3..15 are zero rows of W^T, so lanes 0-15 end
+// up holding channels 0-2 of pixel (lane) and store 16 consecutive floats per channel plane.
+// (The per-pixel VALU kernel above re-reads each input pixel 9x from L1/L2 and spends 1728
+// FMAs + 576 conversions per pixel: ~8x slower at 1024^2.)
+// ---------------------------------------------------------------------------------------
+constexpr int kOut3Rows = 8;  // row tiles per workgroup strip
+
+template <int CIN>
+__global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, float* __restrict__ y,
+                                                             int H, int W, int tiles_x, int strips_y, int clamp255) {
+  constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2, LP = CIN + 8, NH = CIN / 32;
+  constexpr int CH = CIN / 8, NCH = HR * HC * CH, PER = (NCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16 tile[2][HR * HC * LP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bt = blockIdx.x, tx = bt % tiles_x, sy = (bt / tiles_x) % strips_y, b = bt / (tiles_x * strips_y);
+  const int x0 = tx * TC, ys = sy * TR * kOut3Rows;
+  const bf16* xb = x + (long long)b * H * W * CIN;
+  // A = W^T fragments (loaded once per block, amortised over the strip's kOut3Rows tiles):
+  // row n = lane & 15 (out channel; rows 3..15 zero), k = 32*hc + 8*(lane >> 4) + j
+  bf16x8 wa[9][NH];
+  const int n = lane & 15, kg = lane >> 4;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int hc = 0; hc < NH; ++hc)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        wa[tap][hc][j] = (bf16)(n < 3 ? w[(tap * CIN + 32 * hc + 8 * kg + j) * 3 + n] : 0.f);
+  const float bo[3] = {bias[0], bias[1], bias[2]};
+  // halo of row tile r (rows y0-1 .. y0+4, reflect-padded, clamped past the image edge) into
+  // registers; written to LDS after the previous tile's MFMAs
+  bf16x8 st[PER];
+  auto fetch = [&](int y0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = min(tid + 256 * i, NCH - 1);
+      const int pix = c / CH, ch = c - pix * CH;
+      const int r = pix / HC, cc = pix - r * HC;
+      int Y = y0 - 1 + r, X = x0 - 1 + cc;
+      Y = Y < 0 ? -Y : (Y >= H ? 2 * H - 2 - Y : Y);
+      X = X < 0 ? -X : (X >= W ? 2 * W - 2 - X : X);
+      Y = min(max(Y, 0), H - 1);
+      X = min(max(X, 0), W - 1);
+      st[i] = *reinterpret_cast<const bf16x8*>(xb + ((long long)Y * W + X) * CIN + ch * 8);
+    }
+  };
+  auto commit = [&](bf16* t) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + 256 * i;
+      if (c < NCH) {
+        const int pix = c / CH, ch = c - pix * CH;
+        *reinterpret_cast<bf16x8*>(t + pix * LP + ch * 8) = st[i];
+      }
+    }
+  };
+  const int nt = min(kOut3Rows, (H - ys + TR - 1) / TR);
+  fetch(ys);
+  commit(tile[0]);
+  __syncthreads();
+  for (int r = 0; r < nt; ++r) {
+    const bf16* t = tile[r & 1];
+    if (r + 1 < nt) fetch(ys + (r + 1) * TR);
+    const int yy = ys + r * TR + wave;
+#pragma unroll
+    for (int g = 0; g < TC / 16; ++g) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const bf16* px = t + ((wave + tap / 3) * HC + 16 * g + (lane & 15) + tap % 3) * LP + 8 * kg;
+#pragma unroll
+        for (int hc = 0; hc < NH; ++hc)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[tap][hc], *reinterpret_cast<const bf16x8*>(px + 32 * hc),
+                                                        acc, 0, 0, 0);
+      }
+      const int xx = x0 + 16 * g + lane;
+      if (lane < 16 && yy < H && xx < W) {
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+          float v = fmaxf(acc[o] + bo[o], 0.f);
+          if (clamp255) v = fminf(v, 255.f);
+          y[(((long long)b * 3 + o) * H + yy) * W + xx] = v;
+        }
+      }
+    }
+    if (r + 1 < nt) commit(tile[(r + 1) & 1]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Bilinear x2 upsample on NHWC (F.interpolate(scale_factor=2, bilinear, align_corners=False),
 // conv.py:71): one thread per (output pixel, 8-channel group), fp32 blend in PyTorch's order.
 // ---------------------------------------------------------------------------------------
@@ -507,6 +607,19 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
   const long long pix = (long long)B * H * W;
   const dim3 grid((unsigned)((pix + 255) / 256));
   hipStream_t s = (hipStream_t)s_;
+  // bf16, Cin 32/64: the MFMA tile kernel (MHADA_OUT3_MFMA=0 selects the per-pixel VALU kernel)
+  const char* e = getenv("MHADA_OUT3_MFMA");
+  if (dtype == MHADA_BF16 && !(e && e[0] == '0') && (Cin == 32 || Cin == 64)) {
+    const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3Rows - 1) / (4 * kOut3Rows);
+    const long long nb = (long long)B * strips_y * tiles_x;
+    if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");
+    const dim3 g((unsigned)nb);
+    if (Cin == 64)
+      hipLaunchKernelGGL((conv_out3_mfma_kernel<64>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
+    else
+      hipLaunchKernelGGL((conv_out3_mfma_kernel<32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
+    return check_launch("mhada_conv3x3_out3");
+  }
 #define OUT3_CASE(CI)                                                                                          \
   case CI:                                                                                                     \
     if (dtype == MHADA_F32)                                                                                    \

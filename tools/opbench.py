@@ -1,6 +1,6 @@
 """Per-op microbenchmarks on the GPU (interleaved rounds in one process, median of rounds).
 
-    python tools/opbench.py [gemm|conv|attn|all]
+    python tools/opbench.py [gemm|conv|attn|all]     (attn: tools/attn_ab.py)
 
 GEMM shapes are the forward path's (1024^2 batch 4 -> M = 65536 tokens); hipBLASLt via
 torch.matmul is timed beside ours on the same operands as a calibration point.
@@ -59,11 +59,27 @@ def gemm_suite():
             fns = {"ours": lambda: ops.linear(x, w, b, out, residual=r, relu=relu),
                    "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
             if dt == torch.bfloat16:
-                fns["old"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r, relu=relu)
+                fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.linear, x, w, b, out, residual=r,
+                                                  relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
                   + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
+
+
+def out3_suite():
+    dev = "cuda"
+    for dt, B, res in ((torch.bfloat16, 4, 1024), (torch.float32, 8, 512)):
+        x = torch.rand(B, res, res, 64, device=dev).to(dt)
+        w = torch.randn(3, 3, 64, 3, device=dev) * 0.05
+        b = torch.randn(3, device=dev)
+        fns = {"default": lambda: ops.conv3x3_out3(x, w, b)}
+        if dt == torch.bfloat16:
+            fns["valu"] = lambda: with_env("MHADA_OUT3_MFMA", "0", ops.conv3x3_out3, x, w, b)
+        t = bench(fns)
+        by = x.numel() * x.element_size() + B * 3 * res * res * 4
+        print(f"out3 {str(dt)[6:]:8s} B={B} {res}^2: " + "  ".join(f"{k} {v * 1e3:8.1f} us {by / v / 1e6:7.1f} GB/s"
+                                                                for k, v in t.items()))
 
 
 def conv_suite():
@@ -79,7 +95,8 @@ def conv_suite():
             bias = torch.randn(Co, device=dev)
             fns = {"fused": lambda: ops.conv3x3(x, w, bias, dt, upsample=up)}
             if dt == torch.bfloat16 and not up:
-                fns["old"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.conv3x3, x, w, bias, dt, upsample=False)
+                fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
+                                                  upsample=False)
             if up:
                 fns["sep"] = lambda: ops.conv3x3(ops.upsample2x(x), w, bias, dt, upsample=False)
                 fns["upsample_only"] = lambda: ops.upsample2x(x)
@@ -89,42 +106,6 @@ def conv_suite():
                   + "  ".join(f"{k} {v * 1e3:8.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
 
 
-def attn_suite():
-    import network
-    from mhada_hip import engine
-    from mhada_hip.recipe import load_recipe
-    dev = "cuda"
-    for dt, B, n in ((torch.bfloat16, 4, 16384), (torch.float32, 8, 4096)):
-        H = 8
-        q = torch.randn(B, H, n, 64, device=dev).to(dt)
-        kv = torch.randn(B, H, n, 128, device=dev).to(dt)
-        vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
-        fcs = torch.randn(B, n, 512, device=dev)
-        mu, rs = ops.instnorm_stats(fcs)
-        vmu = torch.zeros(B, 512, device=dev)
-        def run(nw, tk=128, pp=0):
-            def f():
-                os.environ["MHADA_ATTN_WAVES"] = str(nw)
-                os.environ["MHADA_ATTN_TK"] = str(tk)
-                os.environ["MHADA_ATTN_PP"] = str(pp)
-                ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
-            return f
-        fns = {"pingpong": run(8, 64, 1), "w8_tk64": run(8, 64), "w8_tk128": run(8, 128)}
-        t = bench(fns, rounds=5, iters=3)
-        # the variants must agree
-        outs = {k: (f(), ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0))[1] for k, f in fns.items()}
-        ref = next(iter(outs.values())).float()
-        for k, o in outs.items():
-            err = ((o.float() - ref).norm() / ref.norm()).item()
-            print(f"   variant {k}: rel diff vs first {err:.2e}")
-        os.environ.pop("MHADA_ATTN_WAVES", None)
-        os.environ.pop("MHADA_ATTN_TK", None)
-        os.environ.pop("MHADA_ATTN_PP", None)
-        fl = 6 * n * n * 512 * B
-        print(f"attn {str(dt)[6:]:8s} B={B} N={n}: " + "  ".join(f"{k} {v:7.3f} ms {fl / v / 1e9:7.1f} TF"
-                                                               for k, v in t.items()))
-
-
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     torch.manual_seed(0)
@@ -132,5 +113,9 @@ if __name__ == "__main__":
         gemm_suite()
     if what in ("conv", "all"):
         conv_suite()
+    if what in ("out3", "conv", "all"):
+        out3_suite()
     if what in ("attn", "all"):
-        attn_suite()
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import attn_ab  # the attention kernel variants (MHADA_ATTN_* switches)
+        attn_ab.main()
