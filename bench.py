@@ -36,6 +36,16 @@ PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense MFMA 
 C = 512
 
 
+def max_over_ranks(x: float, world: int) -> float:
+    """The job's time: max over ranks (RCCL on the GPU; gloo when MHADA_BENCH_BACKEND=gloo)."""
+    if world == 1:
+        return x
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def flops_per_frame(res: int, style_res: int) -> dict:
     """SURVEY.md §8(d) algorithmic FLOPs (2 FLOP/MAC)."""
     nc, ns = (res // 8) ** 2, (style_res // 8) ** 2
@@ -108,10 +118,7 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
     assert torch.isfinite(out[1]).all()
     ev = log.get("mhada_attn", [])
     attn_ms = [a.elapsed_time(b) for a, b in ev]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world)
     frames = batch * steps * world
     dts = "f32" if dtype == torch.float32 else "bf16"
     fl = flops_per_frame(res, res)
@@ -178,10 +185,7 @@ def run_video(dtype, steps, warmup, rank, world):
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
     assert torch.isfinite(err).all()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world)
     nc, ns = (H // 8) * (W // 8), (256 // 8) ** 2
     d = 64
     fl = (72 * nc * C * C + 196608 * nc + 6 * (6 * nc * ns * C + 2 * nc * C * d + 2 * nc * C * C)
@@ -220,10 +224,7 @@ def run_train(steps, warmup, rank, world):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    el = max_over_ranks(el, world)
     return {"metric": "train_image.py step throughput at 512x512, 8 images/GPU [configs[3]]",
             "value": round(batch * steps * world / el, 3), "unit": "images/s", "n_gpus": world, "steps": steps,
             "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
@@ -279,9 +280,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; the modulo only matters when ranks outnumber devices (a 2-rank
+    # rehearsal of the multi-GPU path on a 1-GPU box, with MHADA_BENCH_BACKEND=gloo)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MHADA_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     if args.train:
         r = run_train(args.steps, args.warmup, rank, world)

@@ -848,7 +848,8 @@ static bool pp_offsets_fit(const GemmP& p, int amode) {
 // under the ~34 TB/s L2 ceiling at MFMA rate.
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
-  // N <= 64: 8 waves of 32x64 (one 256x64 tile keeps 8 waves per CU at 92 KiB of LDS)
+  // N <= 64: 8 waves of 32x64 (one 256x64 tile keeps 8 waves per CU at 92 KiB of LDS; a
+  // 4-wave 64x64-per-wave form with 2 workgroups per CU measured 1.3-2x slower)
   if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
   if constexpr (sizeof(TC) == 4) {
     // MHADA_GEMM_F32_TILE=256x128|128x256 (experiments; read per call)
