@@ -36,7 +36,7 @@ enum {
   MHADA_A_CONV3X3_UP2 = 3  /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
 };
 
-int mhada_abi_version(void);
+int mhada_abi_version(void);  /* 2 (mhada_fold_block gained kscale) */
 const char* mhada_last_error(void);
 
 /*

@@ -23,6 +23,6 @@ int check_launch(const char* what) {
 
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 1; }
+extern "C" int mhada_abi_version(void) { return 2; }  // 2: mhada_fold_block takes kscale
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }

@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
 // operand groups).  Waits are counted (vmcnt 4/0), never a drain inside the loop; the phase
 // schedule and ring-slot reuse rules are spelled out above the main loop.
 // ------------------------------------------------------------------------------------
-MHADA_DEV void glds16(const void* src, bf16* lds) {
+MHADA_DEV void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -601,12 +601,15 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
 // NEXT tile's first K-tiles, so the next tile's operands are in flight while this tile's
 // last phases and its epilogue run — the one-shot kernel pays the HBM latency of every
 // tile's prologue and drains the CU at every epilogue (K = 512: 8 K-tiles per tile).
-// Needs K >= 128 (two K-tiles: the A lookahead never skips a whole tile).
+// Needs two K-tiles (K >= 128 bf16 / 64 fp32: the A lookahead never skips a whole tile).
+// fp32 form: same 128-B rows (BK = 32), v_mfma_f32_32x32x2_f32, 32 MFMAs per phase.
 // ------------------------------------------------------------------------------------
-template <typename TO, int AMODE>
+template <typename TC, typename TO, int AMODE>
 __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total) {
-  constexpr int BK = 64, HALF = 128 * BK, TILE = 4 * HALF;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];  // 128 KiB, the only LDS object
+  // 128-B operand rows: BK = 64 bf16 or 32 fp32; CE elements per 16-B chunk, PE per 1-KiB piece
+  constexpr int CE = 16 / sizeof(TC), BK = 8 * CE, PE = 1024 / sizeof(TC), HALF = 128 * BK, TILE = 4 * HALF;
+  typedef typename Vec16<TC>::type Frag;
+  __shared__ __attribute__((aligned(16))) TC smem[2 * TILE];  // 128 KiB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wc = wave & 3;
@@ -615,11 +618,11 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 
   int cofs[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) cofs[i] = 8 * ((lane & 7) ^ (4 * i + (lane >> 4)));
+  for (int i = 0; i < 2; ++i) cofs[i] = CE * ((lane & 7) ^ (4 * i + (lane >> 4)));
   // per-tile staging state (rows 16*wave + 8i + (lane>>3) of each 128-row half)
   struct St {
-    const bf16* ab;
-    const bf16* wb;
+    const TC* ab;
+    const TC* wb;
     unsigned aoff[2][2], woff[2][2];
     int b[2][2], y[2][2], x[2][2];
     int m0, n0, z1, z2;
@@ -632,8 +635,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
     s.m0 = tm * 256;
     s.n0 = tn * 256;
-    s.ab = reinterpret_cast<const bf16*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2;
-    s.wb = reinterpret_cast<const bf16*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2;
+    s.ab = reinterpret_cast<const TC*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2;
+    s.wb = reinterpret_cast<const TC*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
@@ -655,11 +658,11 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       }
   };
   auto stage_a = [&](const St& s, int hh, int kt, int slot) {
-    bf16* dst = smem + slot * TILE + hh * HALF + wave * 1024;
+    TC* dst = smem + slot * TILE + hh * HALF + wave * 2 * PE;
     const int k0 = kt * BK;
     if constexpr (AMODE == MHADA_A_ROWS) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) glds16(s.ab + s.aoff[hh][i] + k0, dst + 512 * i);
+      for (int i = 0; i < 2; ++i) glds16(s.ab + s.aoff[hh][i] + k0, dst + PE * i);
     } else {
       const int cin_n = p.img_c;
       const int tap = k0 / cin_n, cin0 = k0 - tap * cin_n;
@@ -668,34 +671,38 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       for (int i = 0; i < 2; ++i) {
         const int Y = reflect1(s.y[hh][i] + dy, p.out_h), X = reflect1(s.x[hh][i] + dx, p.out_w);
         const unsigned off = (unsigned)(((s.b[hh][i] * p.img_h + Y) * p.img_w + X) * cin_n + cin0 + cofs[i]);
-        glds16(s.ab + off, dst + 512 * i);
+        glds16(s.ab + off, dst + PE * i);
       }
     }
   };
   auto stage_w = [&](const St& s, int hh, int kt, int slot) {
-    bf16* dst = smem + slot * TILE + (2 + hh) * HALF + wave * 1024;
+    TC* dst = smem + slot * TILE + (2 + hh) * HALF + wave * 2 * PE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(s.wb + s.woff[hh][i] + kt * BK, dst + 512 * i);
+    for (int i = 0; i < 2; ++i) glds16(s.wb + s.woff[hh][i] + kt * BK, dst + PE * i);
   };
 
+  // fragment reads: row r32 of a 32-row block, logical 16-B chunk j at swizzled slot j ^ swz.
+  //   bf16 (32x32x16): k-step ks takes chunk 2ks + h (8 k per lane half).
+  //   fp32 (32x32x2, one k per lane half per MFMA): lane half h supplies k = 16h + s at step s
+  //   (A and W agree, so any such bijection is the same sum): its 16 floats are chunks 4h + q.
   const int swz = (r32 >> 1) & 7;
   int koff[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) koff[ks] = 8 * ((2 * ks + h) ^ swz);
-  const bf16* sA = smem + grp * HALF + r32 * 64;
-  const bf16* sW = smem + (2 + (wc >> 1)) * HALF + ((wc & 1) * 64 + r32) * 64;
-  bf16x8 af[4][2], wf[2][2];
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = sizeof(TC) == 2 ? CE * ((2 * ks + h) ^ swz) : CE * ((4 * h + ks) ^ swz);
+  const TC* sA = smem + grp * HALF + r32 * BK;
+  const TC* sW = smem + (2 + (wc >> 1)) * HALF + ((wc & 1) * 64 + r32) * BK;
+  Frag af[4][2], wf[2][2];
   auto read_a = [&](int kp, int cb) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
-        af[mt][s2] = *reinterpret_cast<const bf16x8*>(sA + cb * TILE + mt * 2048 + koff[2 * kp + s2]);
+        af[mt][s2] = *reinterpret_cast<const Frag*>(sA + cb * TILE + mt * 32 * BK + koff[2 * kp + s2]);
   };
   auto read_w = [&](int nt, int kp, int cb) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
-      wf[nt][s2] = *reinterpret_cast<const bf16x8*>(sW + cb * TILE + nt * 2048 + koff[2 * kp + s2]);
+      wf[nt][s2] = *reinterpret_cast<const Frag*>(sW + cb * TILE + nt * 32 * BK + koff[2 * kp + s2]);
   };
   f32x16 acc[4][2];
   auto zero_acc = [&]() {
@@ -706,13 +713,24 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   };
+  // one phase: 4 row blocks x one 32-column block x half a K-tile (bf16: 8 MFMAs, fp32: 32)
   auto compute = [&](int nt) {
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (sizeof(TC) == 2) {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[nt][s2], af[mt][s2], acc[mt][nt], 0, 0, 0);
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[nt][s2], af[mt][s2], acc[mt][nt], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[nt][s2][e], af[mt][s2][e], acc[mt][nt], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   const int dbg = 0;
@@ -792,7 +810,7 @@ static bool persist_enabled() {
   return !(e && e[0] == '0');
 }
 
-template <typename TO, int AMODE>
+template <typename TC, typename TO, int AMODE>
 static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   const char* dbg = getenv("MHADA_GEMM_DBG");
@@ -800,13 +818,16 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   p.tiles_n = (p.N + 255) / 256;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
   const long long total = (long long)p.ntiles * nz;
-  if (p.K >= 128 && persist_enabled() && total < (1LL << 31)) {
+  if (sizeof(TC) == 4 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
-    hipLaunchKernelGGL((gemm_ppp_kernel<TO, AMODE>), dim3(grid), dim3(512), 0, stream, p, (int)total);
+    hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE>), dim3(grid), dim3(512), 0, stream, p, (int)total);
     return check_launch("mhada_gemm");
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
-  return check_launch("mhada_gemm");
+  if constexpr (sizeof(TC) == 2) {
+    hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
+    return check_launch("mhada_gemm");
+  }
+  return fail("mhada_gemm: no ping-pong form");
 }
 
 // The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
@@ -852,6 +873,14 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // 4-wave 64x64-per-wave form with 2 workgroups per CU measured 1.3-2x slower)
   if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
   if constexpr (sizeof(TC) == 4) {
+    // persistent ping-pong (256x256 tiles) when there are at least as many tiles as CUs (below
+    // that the 128x128 kernel keeps more of the chip busy); MHADA_GEMM_PP=0 / PERSIST=0 disable
+    if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
+      const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
+      if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && t256 >= num_cus() && pp_enabled() && persist_enabled() &&
+          pp_offsets_fit(p, AMODE))
+        return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
+    }
     // MHADA_GEMM_F32_TILE=256x128|128x256 (experiments; read per call)
     const char* e = getenv("MHADA_GEMM_F32_TILE");
     if (e && e[0] == '2' && p.N > 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
@@ -863,7 +892,7 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
     } else {
       if constexpr (sizeof(TA) == 2 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
         if (p.N > 128 && p.K % 64 == 0 && pp_enabled() && pp_offsets_fit(p, AMODE))
-          return launch_gemm_pp<TO, AMODE>(p, nz, s);
+          return launch_gemm_pp<bf16, TO, AMODE>(p, nz, s);
       }
       if (p.N <= 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
       return launch_gemm<TC, TA, TO, AMODE, 256, 256, 2, 4>(p, nz, s);

@@ -88,7 +88,7 @@ def test_library_loads_and_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
-    assert lib.mhada_abi_version() == 1
+    assert lib.mhada_abi_version() == 2
 
 
 def test_abi_argument_errors_without_gpu():

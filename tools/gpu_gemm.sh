@@ -2,4 +2,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "linear or conv or grouped or patch" -x -q --timeout 120 --timeout-method thread > gpurun_out/gemm_tests.log 2>&1 && \
-timeout -k 10 300 python -u tools/opbench.py out3 > gpurun_out/opbench_out3.log 2>&1
+timeout -k 10 300 python -u tools/opbench.py gemm > gpurun_out/opbench_gemm.log 2>&1 && \
+timeout -k 10 300 python -u tools/opbench.py conv > gpurun_out/opbench_conv.log 2>&1

@@ -61,6 +61,9 @@ def gemm_suite():
             if dt == torch.bfloat16:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
+            else:
+                fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r,
+                                                  relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
@@ -94,6 +97,9 @@ def conv_suite():
             w = (torch.randn(Co, 9 * Ci, device=dev) / (9 * Ci) ** 0.5).to(dt)
             bias = torch.randn(Co, device=dev)
             fns = {"fused": lambda: ops.conv3x3(x, w, bias, dt, upsample=up)}
+            if dt == torch.float32 and Co > 128:
+                fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.conv3x3, ops.upsample2x(x) if up else x, w,
+                                                  bias, dt, upsample=False)
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
