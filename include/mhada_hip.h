@@ -110,11 +110,11 @@ int mhada_fold_block(const float* wf, const float* wg, const float* wh, const fl
                      const float* rstd_s, void* wq, void* wkv, float* bkv, float* v_mu,
                      float kscale, int dtype, int B, int H, mhada_stream_t stream);
 
-/* bf16 path: the transposed operand image the attention kernel streams, from kv [B][H][Ns][128]:
- * VT[b][h][o][pos(n)] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), row stride
- * ceil64(Ns) (zero padded); pos() swaps bits 2 and 3 of n (keys permuted inside groups of 16
- * to match the MFMA accumulator's row order). */
-int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t stream);
+/* The transposed V' operand image the attention kernel streams, from kv [B][H][Ns][128] of
+ * dtype `dtype`: VT[b][h][o][pos(n)] = V'[b][h][n][64+o] (o<64) and V'^2 (64<=o<128), row
+ * stride ceil64(Ns) (zero padded).  bf16: pos() swaps bits 2 and 3 of n (keys permuted inside
+ * groups of 16 to match the 32x32x16 accumulator's row order); fp32: pos(n) = n. */
+int mhada_transpose_v(const void* kv, void* vt, int dtype, int B, int H, int Ns, mhada_stream_t stream);
 
 /* L2-normalise the 64-wide rows of q [B][H][Nc][64] and the K half of kv [B][H][Ns][128]
  * in place (CosineSimilarity, adaDecoder.py:30-32).  Nc == 0 (q may be NULL) or Ns == 0 (kv
@@ -128,7 +128,7 @@ int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns
  * computed flash-style (A never materialised) with V centred (v_mu added back to M).
  * Softmax: the K half of kv carries the factor log2(e) (mhada_fold_block kscale), so Q.K^T is
  * the logit in log2 units and P = exp2(Q.K^T - max).
- * q [B][H][Nc][64], kv [B][H][Ns][128] (K | V'), vt (bf16 only) [B][H][128][Ns],
+ * q [B][H][Nc][64], kv [B][H][Ns][128] (K | V'), vt [B][H][128][ceil64(Ns)] (mhada_transpose_v),
  * fcs [B][Nc][64H] fp32 with its stats fcs_mu/fcs_rstd [B][64H], v_mu [B][64H];
  * out [B][Nc][64H] dtype. */
 int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,

@@ -134,9 +134,10 @@ MHADA_DEV void scale_acc(f32x16 (&O)[4], float alpha) {
 template <int ACT, int NW>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(const AttnP p) {
   constexpr int NT = 64 * NW;
-  constexpr int LS = 132;  // LDS row (128 + 4 floats): conflict-free b128 K reads, b32 V reads
-  constexpr int CH = 2048 / NT;  // 16-B chunks per thread per tile (64 keys x 128 floats)
-  __shared__ __attribute__((aligned(16))) float sKV[2][64 * LS];
+  constexpr int LK = 68, LV = 68;  // padded rows (272 B): conflict-free 16-B reads down a column
+  constexpr int KCH = 1024 / NT, VCH = 2048 / NT;  // 16-B chunks per thread per 64-key tile
+  __shared__ __attribute__((aligned(16))) float sK[2][64 * LK];   // K rows
+  __shared__ __attribute__((aligned(16))) float sV[2][128 * LV];  // V'^T | V'^2^T rows, 64 keys
   int b, hh, qb;
   decode_block(p, b, hh, qb);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
@@ -155,21 +156,35 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
     }
   }
   const float* kvb = reinterpret_cast<const float*>(p.kv) + bh * p.Ns * 128;
+  const float* vtb = reinterpret_cast<const float*>(p.vt) + bh * 128 * (long long)p.ldt;
 
-  f32x4 stg[CH];
+  // K rows from kv, V'^T | V'^2^T columns from the vt image (mhada_transpose_v, zero padded to
+  // ldt): the PV operands are then one 16-B LDS read per 4 MFMAs with no VALU (reading V' rows
+  // and squaring in registers cost an LDS wait and a VALU->MFMA hazard nop per 4 MFMAs)
+  f32x4 sk[KCH], sv[VCH];
   auto issue = [&](int key0) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int c = tid + NT * i, row = c >> 5, col = (c & 31) * 4;
+    for (int i = 0; i < KCH; ++i) {
+      const int c = tid + NT * i, row = c >> 4, col = (c & 15) * 4;
       const int key = key0 + row;
-      stg[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sk[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + NT * i, row = c >> 4, col = (c & 15) * 4;
+      sv[i] = *reinterpret_cast<const f32x4*>(vtb + (long long)row * p.ldt + key0 + col);
     }
   };
-  auto commit = [&](float* dst) {
+  auto commit = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int c = tid + NT * i, row = c >> 5, col = (c & 31) * 4;
-      *reinterpret_cast<f32x4*>(dst + row * LS + col) = stg[i];
+    for (int i = 0; i < KCH; ++i) {
+      const int c = tid + NT * i, row = c >> 4, col = (c & 15) * 4;
+      *reinterpret_cast<f32x4*>(&sK[buf][row * LK + col]) = sk[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + NT * i, row = c >> 4, col = (c & 15) * 4;
+      *reinterpret_cast<f32x4*>(&sV[buf][row * LV + col]) = sv[i];
     }
   };
 
@@ -185,7 +200,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) S[kb][e] = 0.f;
-      const float* krow = cur + (kb * 32 + r32) * LS + 32 * h;
+      const float* krow = cur + (kb * 32 + r32) * LK + 32 * h;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const f32x4 kk = *reinterpret_cast<const f32x4*>(krow + 4 * i);
@@ -195,37 +210,44 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
       }
     }
   };
-  auto pv = [&](const float* cur, const f32x16 (&P)[2]) {
+  // PV step r of key block kb takes key kb*32 + (r&3) + 8(r>>2) + 4h (the accumulator row of
+  // P^T): for r = 4j..4j+3 those are the 4 consecutive keys kb*32 + 8j + 4h + e of the V'^T rows
+  auto pv = [&](const float* cv, const f32x16 (&P)[2]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float* vrow = cur + key * LS + 64;
-        const float v0 = vrow[r32], v1 = vrow[32 + r32];
-        const float pr = P[kb][r];
-        O[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, pr, O[0], 0, 0, 0);
-        O[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, pr, O[1], 0, 0, 0);
-        O[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0 * v0, pr, O[2], 0, 0, 0);
-        O[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1 * v1, pr, O[3], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const float* vc = cv + r32 * LV + kb * 32 + 8 * j + 4 * h;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(vc);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(vc + 32 * LV);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(vc + 64 * LV);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(vc + 96 * LV);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pr = P[kb][4 * j + e];
+          O[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0[e], pr, O[0], 0, 0, 0);
+          O[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1[e], pr, O[1], 0, 0, 0);
+          O[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[e], pr, O[2], 0, 0, 0);
+          O[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[e], pr, O[3], 0, 0, 0);
+        }
       }
     }
   };
 
   const int NTILE = (p.Ns + 63) / 64, NFULL = p.Ns / 64;
   issue(0);
-  commit(sKV[0]);
+  commit(0);
   __syncthreads();
   // Full tiles.  The rescale (P <= 2^kRescaleThr, so after the first tile it is rare) is a
   // wave-uniform branch inside the single loop: one register assignment for the O accumulators
   // (a leave-rescale-reenter loop made the compiler copy all of O between two register sets on
   // every iteration).
   for (int t = 0; t < NFULL; ++t) {
-    const float* cur = sKV[t & 1];
+    const int cb = t & 1;
     const bool nxt = t + 1 < NTILE;
     if (nxt) issue((t + 1) * 64);
     f32x16 S[2];
-    qk(cur, S);
+    qk(sK[cb], S);
     if constexpr (ACT == MHADA_ACT_SOFTMAX) {
       const float mx = tile_max_log2<2>(S);
       if (__any(mx > m2 + kRescaleThr)) {
@@ -237,18 +259,18 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
       }
     }
     softmax_apply<ACT, 2>(S, m2, l);
-    pv(cur, S);
-    if (nxt) commit(sKV[(t + 1) & 1]);
+    pv(sV[cb], S);
+    if (nxt) commit(cb ^ 1);
     __syncthreads();
   }
   if (NFULL < NTILE) {  // ragged last tile: masked, full online-softmax update
-    const float* cur = sKV[NFULL & 1];
+    const int cb = NFULL & 1;
     f32x16 S[2];
-    qk(cur, S);
+    qk(sK[cb], S);
     mask_tile<ACT, 2>(S, NFULL * 64, p.Ns, h);
     float alpha;
     if (softmax_tile<ACT, 2>(S, m2, l, alpha)) scale_acc(O, alpha);
-    pv(cur, S);
+    pv(sV[cb], S);
   }
   attn_epilogue<float>(p, O, l, b, hh, q, h);
 }
@@ -618,7 +640,7 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   hipStream_t s = (hipStream_t)s_;
   if (!q || !kv || !fcs || !fcs_mu || !fcs_rstd || !v_mu || !out || B <= 0 || H <= 0 || Nc <= 0 || Ns <= 0)
     return fail("mhada_attn: bad args");
-  if (dtype == MHADA_BF16 && !vt) return fail("mhada_attn: bf16 needs the transposed V image");
+  if (!vt) return fail("mhada_attn: needs the transposed V' image (mhada_transpose_v)");
   if (activation != MHADA_ACT_SOFTMAX && activation != MHADA_ACT_COSINE) return fail("mhada_attn: bad activation");
   AttnP p;
   p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;

@@ -254,25 +254,28 @@ __global__ void __launch_bounds__(256) fold_kernel(const float* __restrict__ wf,
 // V transpose for the bf16 attention: vt[bh][o][pos(n)] = V'[n][o], vt[bh][64+o][pos(n)] = V'[n][o]^2
 // (row stride ldt = Ns rounded up to 64, padding zero-filled).  64x64 tiles through LDS.
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) transpose_v_kernel(const bf16* __restrict__ kv, bf16* __restrict__ vt,
-                                                          int Ns, int ldt) {
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_v_kernel(const T* __restrict__ kv, T* __restrict__ vt, int Ns,
+                                                          int ldt) {
   __shared__ float tile[64][65];
   const int bh = blockIdx.y, n0 = blockIdx.x * 64;
-  const bf16* src = kv + (long long)bh * Ns * 128 + 64;
+  const T* src = kv + (long long)bh * Ns * 128 + 64;
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int n = i >> 6, o = i & 63;
-    tile[n][o] = (n0 + n < Ns) ? (float)src[(long long)(n0 + n) * 128 + o] : 0.f;
+    tile[n][o] = (n0 + n < Ns) ? to_f32<T>(src[(long long)(n0 + n) * 128 + o]) : 0.f;
   }
   __syncthreads();
-  bf16* dst = vt + (long long)bh * 128 * ldt + n0;
+  T* dst = vt + (long long)bh * 128 * ldt + n0;
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int o = i >> 6, pos = i & 63;
-    // key stored at position pos: swap bits 2 and 3 inside each group of 16 (an involution),
-    // so the 8 keys {4h..4h+3, 8+4h..8+4h+3} one MFMA lane half needs are contiguous.
-    const int n = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1);
+    // bf16: key stored at position pos = swap bits 2 and 3 inside each group of 16 (an
+    // involution), so the 8 keys {4h..4h+3, 8+4h..8+4h+3} one 32x32x16 lane half needs are
+    // contiguous.  fp32 (32x32x2, one key per MFMA): natural order — a lane's keys 8q+4h..+3
+    // are already contiguous (one 16-B read per 4 MFMAs).
+    const int n = sizeof(T) == 2 ? ((pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1)) : pos;
     const float v = tile[n][o];
-    dst[(long long)o * ldt + pos] = (bf16)v;
-    dst[(long long)(64 + o) * ldt + pos] = (bf16)(v * v);
+    dst[(long long)o * ldt + pos] = from_f32<T>(v);
+    dst[(long long)(64 + o) * ldt + pos] = from_f32<T>(v * v);
   }
 }
 
@@ -569,11 +572,17 @@ extern "C" int mhada_fold_block(const float* wf, const float* wg, const float* w
   return check_launch("mhada_fold_block");
 }
 
-extern "C" int mhada_transpose_v(const void* kv, void* vt, int B, int H, int Ns, mhada_stream_t s_) {
+extern "C" int mhada_transpose_v(const void* kv, void* vt, int dtype, int B, int H, int Ns, mhada_stream_t s_) {
   if (!kv || !vt || B <= 0 || H <= 0 || Ns <= 0) return fail("mhada_transpose_v: bad args");
+  if (dtype != MHADA_F32 && dtype != MHADA_BF16) return fail("mhada_transpose_v: bad dtype");
   const int ldt = (Ns + 63) / 64 * 64;
-  hipLaunchKernelGGL(transpose_v_kernel, dim3(ldt / 64, B * H), dim3(256), 0, (hipStream_t)s_, (const bf16*)kv,
-                     (bf16*)vt, Ns, ldt);
+  const dim3 grid(ldt / 64, B * H);
+  if (dtype == MHADA_F32)
+    hipLaunchKernelGGL((transpose_v_kernel<float>), grid, dim3(256), 0, (hipStream_t)s_, (const float*)kv, (float*)vt,
+                       Ns, ldt);
+  else
+    hipLaunchKernelGGL((transpose_v_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)kv, (bf16*)vt,
+                       Ns, ldt);
   return check_launch("mhada_transpose_v");
 }
 

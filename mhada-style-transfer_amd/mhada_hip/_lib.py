@@ -48,7 +48,7 @@ SIGNATURES = {
     "mhada_pos_embed": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_instnorm_stats": (_I, [_vp, _vp, _vp, _vp, _I, _I, _I, _I, _F, _vp]),
     "mhada_fold_block": (_I, [_vp] * 12 + [_F, _I, _I, _I, _vp]),
-    "mhada_transpose_v": (_I, [_vp, _vp, _I, _I, _I, _vp]),
+    "mhada_transpose_v": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),

@@ -6,7 +6,7 @@ Layout in HBM (per forward call, B images, N = (H/8)(W/8) tokens, C = 512):
   * GEMM operands             compute dtype (fp32 | bf16) [B*N][K]
   * per-layer ViT outputs     fp32 [B][N][C]; handed to callers as NCHW *views*
                               (x.view(B,h,w,C).permute(0,3,1,2)) — no transpose kernel
-  * MHAda per block           Q [B][H][Nc][64], KV [B][H][Ns][128] (K | V'), bf16 adds
+  * MHAda per block           Q [B][H][Nc][64], KV [B][H][Ns][128] (K | V'), and
                               VT [B][H][128][ceil64(Ns)] (V'^T | V'^2^T); out [B][Nc][C]
   * decoder                   NHWC activations in the compute dtype; the module output is
                               NCHW fp32 (B,3,8h,8w), written directly by the last conv.
@@ -263,7 +263,7 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
                  ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM))
         if act == ACT_COSINE:
             ops.cosine_prep(None, kv)
-        vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+        vt = ops.transpose_v(kv)
         if side is not None:
             side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt)
     if act == ACT_COSINE:

@@ -203,7 +203,7 @@ def transpose_v(kv: torch.Tensor) -> torch.Tensor:
     B, H, Ns, _ = kv.shape
     ldt = (Ns + 63) // 64 * 64
     vt = torch.empty(B, H, 128, ldt, device=kv.device, dtype=kv.dtype)
-    rc = _lib.load().mhada_transpose_v(kv.data_ptr(), vt.data_ptr(), B, H, Ns, _stream())
+    rc = _lib.load().mhada_transpose_v(kv.data_ptr(), vt.data_ptr(), dt_code(kv.dtype), B, H, Ns, _stream())
     _lib.check(rc, "mhada_transpose_v")
     return vt
 

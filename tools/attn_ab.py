@@ -57,6 +57,27 @@ def main():
                                            for v in VARIANTS), flush=True)
     for k in ("MHADA_ATTN_KERNEL", "MHADA_ATTN_PRIO", "MHADA_ATTN_TK"):
         os.environ.pop(k, None)
+    # fp32 (one kernel; compare with the launch averages in profiles/r01_attn_launch_stats.txt)
+    for name, B, nc, ns in SHAPES[1:]:
+        q = torch.randn(B, H, nc, 64, device="cuda") * 0.35
+        kv = torch.randn(B, H, ns, 128, device="cuda") * 0.35
+        vt = ops.transpose_v(kv)
+        fcs = torch.randn(B, nc, 512, device="cuda")
+        mu, rs = ops.instnorm_stats(fcs)
+        vmu = torch.zeros(B, 512, device="cuda")
+        ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(7):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+            e.record()
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e) / 3)
+        t = sorted(ts)[3]
+        print(f"fp32 {name:18s} {t:.3f} ms {6.0 * nc * ns * 512 * B / t / 1e9:.1f} TF", flush=True)
 
 
 if __name__ == "__main__":

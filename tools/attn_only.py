@@ -10,7 +10,7 @@ B, n = (4, 16384) if dt == torch.bfloat16 else (8, 4096)
 H = 8
 q = torch.randn(B, H, n, 64, device="cuda").to(dt)
 kv = torch.randn(B, H, n, 128, device="cuda").to(dt)
-vt = ops.transpose_v(kv) if dt == torch.bfloat16 else None
+vt = ops.transpose_v(kv)
 fcs = torch.randn(B, n, 512, device="cuda")
 mu, rs = ops.instnorm_stats(fcs)
 vmu = torch.zeros(B, 512, device="cuda")

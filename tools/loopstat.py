@@ -11,7 +11,7 @@ end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
 body = lines[start:end]
 labels = {l.split(":")[0]: i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l)}
 for i, l in enumerate(body):
-    m = re.search(r"s_cbranch_\w+\s+(\.LBB\w+)", l)
+    m = re.search(r"s_(?:c)?branch\w*\s+(\.LBB\w+)", l)
     if m and m.group(1) in labels and labels[m.group(1)] < i:
         seg = [x.split()[0] for x in body[labels[m.group(1)] + 1:i] if x.strip() and not x.strip().startswith(";") and not x.startswith(".")]
         c = collections.Counter(seg)
