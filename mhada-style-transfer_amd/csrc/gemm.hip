@@ -604,12 +604,18 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
 // Needs two K-tiles (K >= 128 bf16 / 64 fp32: the A lookahead never skips a whole tile).
 // fp32 form: same 128-B rows (BK = 32), v_mfma_f32_32x32x2_f32, 32 MFMAs per phase.
 // ------------------------------------------------------------------------------------
-template <typename TC, typename TO, int AMODE>
+template <typename TC, typename TO, int AMODE, int BN>
 __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total) {
-  // 128-B operand rows: BK = 64 bf16 or 32 fp32; CE elements per 16-B chunk, PE per 1-KiB piece
-  constexpr int CE = 16 / sizeof(TC), BK = 8 * CE, PE = 1024 / sizeof(TC), HALF = 128 * BK, TILE = 4 * HALF;
+  // 128-B operand rows: BK = 64 bf16 or 32 fp32; CE elements per 16-B chunk, PE per 1-KiB piece.
+  // BN = 256: each wave owns 128 rows x 64 columns (TN = 2 column blocks, 4 phases per K-tile);
+  // BN = 128 (N <= 128 layers): 128 rows x 32 columns (TN = 1, 2 phases), one W half per stage;
+  // with only 2 phases per K-tile the lagging group still reads A(g) when the leading group
+  // could stage A(g+2), so the ring has 3 slots (A two K-tiles ahead needs slot (g+2) % 3).
+  constexpr int TN = BN / 128, NWH = BN / 128;
+  constexpr int CE = 16 / sizeof(TC), BK = 8 * CE, PE = 1024 / sizeof(TC), HALF = 128 * BK, TILE = (2 + NWH) * HALF;
+  constexpr int NSLOT = BN == 256 ? 2 : 3;
   typedef typename Vec16<TC>::type Frag;
-  __shared__ __attribute__((aligned(16))) TC smem[2 * TILE];  // 128 KiB, the only LDS object
+  __shared__ __attribute__((aligned(16))) TC smem[NSLOT * TILE];  // 128 / 144 KiB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wc = wave & 3;
@@ -634,7 +640,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     s.z2 = z - s.z1 * p.nb2;
     const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
     s.m0 = tm * 256;
-    s.n0 = tn * 256;
+    s.n0 = tn * BN;
     s.ab = reinterpret_cast<const TC*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2;
     s.wb = reinterpret_cast<const TC*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2;
 #pragma unroll
@@ -643,7 +649,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       for (int i = 0; i < 2; ++i) {
         const int rr = 16 * wave + 8 * i + (lane >> 3);
         const int m = min(s.m0 + 128 * hh + rr, p.M - 1);
-        const int n = min(s.n0 + 128 * hh + rr, p.N - 1);
+        const int n = min(s.n0 + 128 * (hh % NWH) + rr, p.N - 1);
         s.woff[hh][i] = (unsigned)((long long)n * p.ldw + cofs[i]);
         if constexpr (AMODE == MHADA_A_ROWS) {
           s.aoff[hh][i] = (unsigned)((long long)m * p.lda + cofs[i]);
@@ -690,8 +696,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) koff[ks] = sizeof(TC) == 2 ? CE * ((2 * ks + h) ^ swz) : CE * ((4 * h + ks) ^ swz);
   const TC* sA = smem + grp * HALF + r32 * BK;
-  const TC* sW = smem + (2 + (wc >> 1)) * HALF + ((wc & 1) * 64 + r32) * BK;
-  Frag af[4][2], wf[2][2];
+  const TC* sW = smem + (2 + (wc * TN * 32) / 128) * HALF + ((wc * TN * 32) % 128 + r32) * BK;
+  Frag af[4][2], wf[TN][2];
   auto read_a = [&](int kp, int cb) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -704,12 +710,12 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     for (int s2 = 0; s2 < 2; ++s2)
       wf[nt][s2] = *reinterpret_cast<const Frag*>(sW + cb * TILE + nt * 32 * BK + koff[2 * kp + s2]);
   };
-  f32x16 acc[4][2];
+  f32x16 acc[4][TN];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < TN; ++b)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   };
@@ -742,16 +748,18 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   bool has_nxt = w + G < total;
   if (has_nxt) setup(w + G, nxt);
   zero_acc();
-  stage_a(cur, 0, 0, 0); stage_a(cur, 1, 0, 0); stage_w(cur, 0, 0, 0); stage_w(cur, 1, 0, 0);
+  stage_a(cur, 0, 0, 0); stage_a(cur, 1, 0, 0); stage_w(cur, 0, 0, 0);
+  if constexpr (NWH == 2) stage_w(cur, 1, 0, 0);
   stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   PP_BARRIER();
   if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
 
-  int g = 0;  // global K-tile counter: ring slot g & 1
+  // ring slots of K-tiles g, g+1, g+2 (global K-tile counter g, continuous across tiles)
+  int sl0 = 0, sl1 = 1, sl2 = NSLOT == 2 ? 0 : 2;
   while (true) {
-    for (int kt = 0; kt < KT; ++kt, ++g) {
-      const int cb = g & 1;
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cb = sl0;
       // sources of K-tiles g+1 (W) and g+2 (A): this tile or the next one
       const bool w1 = kt + 1 < KT || has_nxt;
       const St& s1 = kt + 1 < KT ? cur : nxt;
@@ -759,31 +767,46 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       const bool a2 = kt + 2 < KT || has_nxt;
       const St& s2 = kt + 2 < KT ? cur : nxt;
       const int k2 = kt + 2 < KT ? kt + 2 : kt + 2 - KT;
-      // phase 0
-      read_a(0, cb); read_w(0, 0, cb);
-      if (w1) stage_w(s1, 0, k1, cb ^ 1);
-      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
-      // phase 1
-      read_w(1, 0, cb);
-      if (w1) stage_w(s1, 1, k1, cb ^ 1);
-      PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
-      // phase 2
-      read_a(1, cb); read_w(0, 1, cb);
-      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
-      // phase 3
-      read_w(1, 1, cb);
+      if constexpr (TN == 2) {
+        // phase 0
+        read_a(0, cb); read_w(0, 0, cb);
+        if (w1) stage_w(s1, 0, k1, sl1);
+        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+        // phase 1
+        read_w(1, 0, cb);
+        if (w1) stage_w(s1, 1, k1, sl1);
+        PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+        // phase 2
+        read_a(1, cb); read_w(0, 1, cb);
+        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+        // phase 3
+        read_w(1, 1, cb);
+      } else {
+        // phase 0: k-steps of pair 0
+        read_a(0, cb); read_w(0, 0, cb);
+        if (w1) stage_w(s1, 0, k1, sl1);
+        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+        // phase 1: pair 1
+        read_a(1, cb); read_w(0, 1, cb);
+      }
       if (a2) {
-        stage_a(s2, 0, k2, cb); stage_a(s2, 1, k2, cb);
+        stage_a(s2, 0, k2, sl2); stage_a(s2, 1, k2, sl2);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+      PP_LGKM0(); PP_BARRIER(); compute(TN - 1); PP_BARRIER();
+      if constexpr (NSLOT == 2) {
+        sl0 ^= 1; sl1 ^= 1; sl2 ^= 1;
+      } else {
+        const int o = sl0;
+        sl0 = sl1; sl1 = sl2; sl2 = o;
+      }
     }
     // tile boundary: re-align the groups so both store in the same interval (a store between
     // staggered barriers would hold the other group's compute phase), then re-stagger
     if (grp == 0) PP_BARRIER();
-    store_tile<TO, 4, 2>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * 64, h);
+    store_tile<TO, 4, TN>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * TN * 32, h);
     if (!has_nxt) break;
     if (grp == 1) PP_BARRIER();
     zero_acc();
@@ -810,20 +833,20 @@ static bool persist_enabled() {
   return !(e && e[0] == '0');
 }
 
-template <typename TC, typename TO, int AMODE>
+template <typename TC, typename TO, int AMODE, int BN = 256>
 static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   const char* dbg = getenv("MHADA_GEMM_DBG");
   p.dbg = dbg ? atoi(dbg) : 0;
-  p.tiles_n = (p.N + 255) / 256;
+  p.tiles_n = (p.N + BN - 1) / BN;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
   const long long total = (long long)p.ntiles * nz;
-  if (sizeof(TC) == 4 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
+  if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
-    hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE>), dim3(grid), dim3(512), 0, stream, p, (int)total);
+    hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN>), dim3(grid), dim3(512), 0, stream, p, (int)total);
     return check_launch("mhada_gemm");
   }
-  if constexpr (sizeof(TC) == 2) {
+  if constexpr (sizeof(TC) == 2 && BN == 256) {
     hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
     return check_launch("mhada_gemm");
   }
@@ -893,6 +916,11 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       if constexpr (sizeof(TA) == 2 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
         if (p.N > 128 && p.K % 64 == 0 && pp_enabled() && pp_offsets_fit(p, AMODE))
           return launch_gemm_pp<bf16, TO, AMODE>(p, nz, s);
+        // 65..128 columns: the 256x128 persistent ping-pong form (MHADA_GEMM_PP128=0 disables)
+        const char* e128 = getenv("MHADA_GEMM_PP128");
+        if (p.N > 64 && p.N <= 128 && p.K % 64 == 0 && p.K >= 128 && !(e128 && e128[0] == '0') && pp_enabled() &&
+            pp_offsets_fit(p, AMODE))
+          return launch_gemm_pp<bf16, TO, AMODE, 128>(p, nz, s);
       }
       if (p.N <= 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
       return launch_gemm<TC, TA, TO, AMODE, 256, 256, 2, 4>(p, nz, s);

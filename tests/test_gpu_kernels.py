@@ -35,7 +35,7 @@ def test_library_is_the_native_one():
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(100, 96, 64), (1024, 1536, 512), (333, 512, 2048), (4096, 64, 64), (17, 2048, 512),
-                                   (1000, 384, 576), (8192, 512, 64)])
+                                   (1000, 384, 576), (8192, 512, 64), (2000, 128, 512), (700, 100, 256)])
 def test_linear(cdt, M, N, K):
     x = rnd(M, K, seed=1, dtype=cdt)
     w = rnd(N, K, scale=K ** -0.5, seed=2, dtype=cdt)
@@ -91,7 +91,7 @@ def test_patch_embed(cdt, H, W):
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("up", [False, True])
 @pytest.mark.parametrize("Ci,Co,H,W", [(64, 64, 9, 13), (128, 64, 16, 16), (512, 256, 8, 8), (256, 128, 5, 3),
-                                         (256, 256, 40, 36), (64, 320, 23, 50)])
+                                         (256, 256, 40, 36), (64, 320, 23, 50), (128, 128, 33, 20)])
 def test_conv3x3(cdt, up, Ci, Co, H, W):
     B = 2
     x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(Ci + H)).to(DEV)

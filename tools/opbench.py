@@ -100,6 +100,9 @@ def conv_suite():
             if dt == torch.float32 and Co > 128:
                 fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.conv3x3, ops.upsample2x(x) if up else x, w,
                                                   bias, dt, upsample=False)
+            if dt == torch.bfloat16 and 64 < Co <= 128:
+                fns["pp128_off"] = lambda: with_env("MHADA_GEMM_PP128", "0", ops.conv3x3, ops.upsample2x(x) if up else x,
+                                                    w, bias, dt, upsample=False)
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
