@@ -17,9 +17,8 @@ SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1
           ("ragged", 2, 1000, 777)]
 
 
-VARIANTS = {"fs": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128", "MHADA_ATTN_PRIO": "1"},
-            "fs_noprio": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128", "MHADA_ATTN_PRIO": "0"},
-            "fs64": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "64", "MHADA_ATTN_PRIO": "1"},
+VARIANTS = {"fs": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128"},
+            "fs64": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "64"},
             "w8": {"MHADA_ATTN_KERNEL": "w8", "MHADA_ATTN_TK": "128"}}
 
 
