@@ -93,7 +93,7 @@ int mhada_pos_embed(const float* pos, float* out, int C, int bh, int bw, int oh,
 
 /* InstanceNorm2d(affine=False) statistics (adaDecoder.py:147-149): per (b, c) mean and
  * 1/sqrt(biased var + eps) over the N tokens of x [B][N][C] fp32.  `work` holds
- * splits*B*C*2 doubles (any splits >= 1). */
+ * splits*B*C*2 doubles (any splits >= 1).  C % 4 == 0, x 16-byte aligned. */
 int mhada_instnorm_stats(const float* x, float* mu, float* rstd, double* work, int B, int N,
                          int C, int splits, float eps, mhada_stream_t stream);
 

@@ -30,7 +30,6 @@ struct GemmP {
   const void* r; long long ldr, sr1, sr2;
   void* c; long long ldc, sc1, sc2;
   int relu, tiles_n, ntiles;
-  int dbg;  // ping-pong kernel experiments (MHADA_GEMM_DBG): 1 no DMA in loop, 2 no LDS reads, 4 no barriers
 };
 
 template <typename TC> struct Cfg {
@@ -438,7 +437,7 @@ MHADA_DEV void glds16(const void* src, void* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-#define PP_BARRIER() do { __builtin_amdgcn_sched_barrier(0); if (!(dbg & 4)) __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define PP_BARRIER() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
 template <typename TO, int AMODE>
@@ -552,7 +551,6 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
   // Ring: tile t's A slots are last read in phase 2 and refilled (t+2) in phase 3; its W slots
   // are last read in phase 3 and refilled (t+2) in phases 0/1 of tile t+1.
   const int KT = p.K / BK;
-  const int dbg = p.dbg;
   stage_a(0, 0); stage_a(1, 0); stage_w(0, 0); stage_w(1, 0);
   if (KT > 1) {
     stage_a(0, 1); stage_a(1, 1);
@@ -563,23 +561,22 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
   PP_BARRIER();
   if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
 
-  const bool rd = !(dbg & 2);
   for (int kt = 0; kt < KT; ++kt) {
     const int cb = kt & 1;
-    const bool n1 = kt + 1 < KT && !(dbg & 1), n2 = kt + 2 < KT && !(dbg & 1);
+    const bool n1 = kt + 1 < KT, n2 = kt + 2 < KT;
     // phase 0
-    if (rd) { read_a(0, cb); read_w(0, 0, cb); }
+    read_a(0, cb); read_w(0, 0, cb);
     if (n1) stage_w(0, kt + 1);
     PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
     // phase 1
-    if (rd) read_w(1, 0, cb);
+    read_w(1, 0, cb);
     if (n1) stage_w(1, kt + 1);
     PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
     // phase 2
-    if (rd) { read_a(1, cb); read_w(0, 1, cb); }
+    read_a(1, cb); read_w(0, 1, cb);
     PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
     // phase 3
-    if (rd) read_w(1, 1, cb);
+    read_w(1, 1, cb);
     if (n2) {
       stage_a(0, kt + 2); stage_a(1, kt + 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -739,7 +736,6 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     }
     __builtin_amdgcn_s_setprio(0);
   };
-  const int dbg = 0;
 
   const int KT = p.K / BK;
   int w = blockIdx.x;
@@ -836,8 +832,6 @@ static bool persist_enabled() {
 template <typename TC, typename TO, int AMODE, int BN = 256>
 static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
-  const char* dbg = getenv("MHADA_GEMM_DBG");
-  p.dbg = dbg ? atoi(dbg) : 0;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
   const long long total = (long long)p.ntiles * nz;
@@ -905,10 +899,6 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)
     }
-    // MHADA_GEMM_F32_TILE=256x128|128x256 (experiments; read per call)
-    const char* e = getenv("MHADA_GEMM_F32_TILE");
-    if (e && e[0] == '2' && p.N > 128) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
-    if (e && e[0] == '1' && e[3] == 'x' && e[4] == '2' && p.N > 128) return launch_gemm<TC, TA, TO, AMODE, 128, 256, 2, 4>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
   } else {
     if constexpr (AMODE == MHADA_A_CONV3X3_UP2) {  // 4 bilinear taps staged per chunk: keep the tile small

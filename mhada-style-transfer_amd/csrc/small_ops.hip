@@ -80,6 +80,90 @@ __global__ void __launch_bounds__(256) vit_batch_attn_kernel(const T* __restrict
   }
 }
 
+// Vectorised small-batch form (L <= 8): a group of 8 lanes owns one (token, head), lane = 8
+// consecutive features (one 16-B bf16 / two 16-B fp32 loads per q/k/v row instead of 2-4-byte
+// per-lane loads); the L x L dot products are 8-lane shuffle reductions, the softmax and PV
+// are lane-local.
+template <typename T>
+__global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                 int L, int ntok, int heads) {
+  constexpr int D = 64, E = 8;
+  const int g8 = threadIdx.x & 7;
+  const long long pair = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool valid = pair < (long long)ntok * heads;
+  const long long pp = valid ? pair : 0;
+  const int C = heads * D;
+  const int n = (int)(pp / heads), hh = (int)(pp - (long long)n * heads);
+  const long long row_stride = (long long)ntok * 3 * C;
+  const T* base = qkv + (long long)n * 3 * C + hh * D + g8 * E;
+  auto load8 = [&](const T* p, float (&f)[E]) {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+      for (int e = 0; e < E; ++e) f[e] = (float)v[e];
+    } else {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = a[e];
+        f[4 + e] = b[e];
+      }
+    }
+  };
+  float q[8][E], k[8][E], v[8][E];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < L) {
+      load8(base + i * row_stride, q[i]);
+      load8(base + i * row_stride + C, k[i]);
+      load8(base + i * row_stride + 2 * C, v[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i >= L) break;
+    float sc[8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < L) {
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) d = fmaf(q[i][e], k[j][e], d);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) d += __shfl_xor(d, o, 64);
+        sc[j] = d * 0.125f;  // 1/sqrt(64)
+        m = fmaxf(m, sc[j]);
+      }
+    }
+    float l = 0.f, o8[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) o8[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < L) {
+        const float p = __expf(sc[j] - m);
+        l += p;
+#pragma unroll
+        for (int e = 0; e < E; ++e) o8[e] = fmaf(p, v[j][e], o8[e]);
+      }
+    }
+    const float inv = 1.f / l;
+    if (valid) {
+      T* dst = out + ((long long)i * ntok + n) * C + hh * D + g8 * E;
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 r;
+#pragma unroll
+        for (int e = 0; e < E; ++e) r[e] = (bf16)(o8[e] * inv);
+        *reinterpret_cast<bf16x8*>(dst) = r;
+      } else {
+        *reinterpret_cast<f32x4*>(dst) = f32x4{o8[0] * inv, o8[1] * inv, o8[2] * inv, o8[3] * inv};
+        *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o8[4] * inv, o8[5] * inv, o8[6] * inv, o8[7] * inv};
+      }
+    }
+  }
+}
+
 // Small-batch form (L <= 8, every bench/training config): each (token, head) reads q, k, v
 // once — q/k staged in LDS, v in registers — and the L x L scores are computed in parallel with
 // lane = (i, j); the softmax over j is an 8-lane group reduction.
@@ -165,33 +249,44 @@ __global__ void pos_embed_kernel(const float* __restrict__ pos, float* __restric
 // InstanceNorm statistics: partial sums in fp64 per (split, b, c), then a finalize pass.
 // grid (C/64, B, splits), 256 threads = 64 channels x 4 row phases (coalesced 256-B rows).
 // ---------------------------------------------------------------------------------------
+// One block = 64 channels x one split of the token range; thread (quad, ph) accumulates channels
+// 4*quad..4*quad+3 of every 16th row (16-B loads: 16 threads read one row's 256-B channel block,
+// a wave 4 rows), in fp64; the 16 row phases reduce through LDS in a fixed order.
 __global__ void __launch_bounds__(256) in_partial_kernel(const float* __restrict__ x, double* __restrict__ work,
                                                          int B, int N, int C, int splits) {
-  __shared__ double red[2][4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ph = threadIdx.x >> 6;
+  __shared__ double red[2][16][65];
+  const int quad = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + 4 * quad;
   const int b = blockIdx.y, s = blockIdx.z;
   const int per = (N + splits - 1) / splits;
   const int r0 = s * per, r1 = min(N, r0 + per);
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    const float* xb = x + (long long)b * N * C + c;
-    for (int r = r0 + ph; r < r1; r += 4) {
-      const double v = (double)xb[(long long)r * C];
-      s1 += v;
-      s2 += v * v;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c0 < C) {  // C % 4 == 0 (checked by the entry point)
+    const float* xb = x + (long long)b * N * C + c0;
+#pragma unroll 4
+    for (int r = r0 + ph; r < r1; r += 16) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xb + (long long)r * C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double d = (double)v[e];
+        s1[e] += d;
+        s2[e] += d * d;
+      }
     }
   }
-  red[0][ph][threadIdx.x & 63] = s1;
-  red[1][ph][threadIdx.x & 63] = s2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][ph][4 * quad + e] = s1[e];
+    red[1][ph][4 * quad + e] = s2[e];
+  }
   __syncthreads();
-  if (ph == 0 && c < C) {
-    const int t = threadIdx.x & 63;
-    const double a = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
-    const double q = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
-    double* w = work + (((long long)s * B + b) * C + c) * 2;
-    w[0] = a;
-    w[1] = q;
+  if (threadIdx.x < 128) {
+    const int t = threadIdx.x & 63, which = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + t;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += red[which][k][t];
+    if (c < C) work[(((long long)s * B + b) * C + c) * 2 + which] = a;
   }
 }
 
@@ -517,6 +612,19 @@ extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L
   const size_t lds = 0;
   const dim3 grid((unsigned)((pairs + 3) / 4));
   if (L <= 8) {
+    // the vectorised form needs 16-byte aligned rows (qkv, out); MHADA_VIT_ATTN_VEC=0 selects
+    // the per-lane form (A/B)
+    const char* e = getenv("MHADA_VIT_ATTN_VEC");
+    if (!(e && e[0] == '0') && aligned16(qkv) && aligned16(out)) {
+      const dim3 g32((unsigned)((pairs + 31) / 32));
+      if (dtype == MHADA_F32)
+        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<float>), g32, dim3(256), 0, s, (const float*)qkv, (float*)out, L,
+                           ntok, heads);
+      else
+        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
+                           ntok, heads);
+      return check_launch("mhada_vit_batch_attn");
+    }
     if (dtype == MHADA_F32)
       hipLaunchKernelGGL((vit_batch_attn_small_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv, (float*)out,
                          L, ntok, heads);
@@ -548,6 +656,7 @@ extern "C" int mhada_instnorm_stats(const float* x, float* mu, float* rstd, doub
   if (!x || !mu || !rstd || !work || B <= 0 || N <= 0 || C <= 0 || splits <= 0)
     return fail("mhada_instnorm_stats: bad args");
   if (splits > 65535) return fail("mhada_instnorm_stats: too many splits");
+  if (C % 4 || ((uintptr_t)x & 15)) return fail("mhada_instnorm_stats: needs C % 4 == 0 and a 16-byte aligned x");
   hipLaunchKernelGGL(in_partial_kernel, dim3((C + 63) / 64, B, splits), dim3(256), 0, s, x, work, B, N, C, splits);
   int rc = check_launch("mhada_instnorm_stats/partial");
   if (rc) return rc;

@@ -168,8 +168,9 @@ def test_pos_embed(oh, ow):
     assert rel(y, ref) < 1e-6
 
 
-def test_instnorm_stats():
-    x = rnd(3, 4097, 512, seed=2) * 5 + 10
+@pytest.mark.parametrize("B,N,C", [(3, 4097, 512), (1, 37, 68), (2, 16384, 512)])
+def test_instnorm_stats(B, N, C):
+    x = rnd(B, N, C, seed=2) * 5 + 10
     mu, rstd = ops.instnorm_stats(x)
     xd = x.double()
     ref_mu = xd.mean(1)
