@@ -164,6 +164,17 @@ __global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __rest
   }
 }
 
+// L = 1 (one image per call: the video path's per-frame encoder): the softmax over one key is
+// exactly 1, so the attention output is V bit for bit; a strided 16-B row copy of the V slice.
+__global__ void __launch_bounds__(256) vit_batch_copy_v_kernel(const uint4* __restrict__ qkv, uint4* __restrict__ out,
+                                                               int ntok, int row16) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)ntok * row16) return;
+  const long long n = idx / row16;
+  const int c = (int)(idx - n * row16);
+  out[n * row16 + c] = qkv[n * 3 * row16 + 2 * row16 + c];
+}
+
 // Small-batch form (L <= 8, every bench/training config): each (token, head) reads q, k, v
 // once — q/k staged in LDS, v in registers — and the L x L scores are computed in parallel with
 // lane = (i, j); the softmax over j is an 8-lane group reduction.
@@ -290,20 +301,38 @@ __global__ void __launch_bounds__(256) in_partial_kernel(const float* __restrict
   }
 }
 
-__global__ void in_finalize_kernel(const double* __restrict__ work, float* __restrict__ mu,
-                                   float* __restrict__ rstd, int B, int N, int C, int splits, float eps) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * C) return;
+// 16 outputs x 16 split phases per block: each thread sums every 16th split in order, the 16
+// partials are added in a fixed order (deterministic; a split-serial loop per output was
+// latency bound at B = 1, where the partial kernel uses 256 splits).
+__global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restrict__ work, float* __restrict__ mu,
+                                                          float* __restrict__ rstd, int B, int N, int C, int splits,
+                                                          float eps) {
+  __shared__ double red[2][16][17];
+  const int o = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int idx = blockIdx.x * 16 + o;
   double a = 0.0, q = 0.0;
-  for (int s = 0; s < splits; ++s) {
-    a += work[((long long)s * B * C + idx) * 2];
-    q += work[((long long)s * B * C + idx) * 2 + 1];
+  if (idx < B * C) {
+    for (int s = ph; s < splits; s += 16) {
+      a += work[((long long)s * B * C + idx) * 2];
+      q += work[((long long)s * B * C + idx) * 2 + 1];
+    }
   }
-  const double mean = a / N;
-  double var = q / N - mean * mean;
-  if (var < 0.0) var = 0.0;
-  mu[idx] = (float)mean;
-  rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+  red[0][ph][o] = a;
+  red[1][ph][o] = q;
+  __syncthreads();
+  if (ph == 0 && idx < B * C) {
+    double sa = 0.0, sq = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      sa += red[0][k][o];
+      sq += red[1][k][o];
+    }
+    const double mean = sa / N;
+    double var = sq / N - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mu[idx] = (float)mean;
+    rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -611,18 +640,22 @@ extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L
   const long long pairs = (long long)ntok * heads;
   const size_t lds = 0;
   const dim3 grid((unsigned)((pairs + 3) / 4));
+  if (L == 1 && aligned16(qkv) && aligned16(out)) {
+    const int row16 = heads * head_dim * (dtype == MHADA_F32 ? 4 : 2) / 16;
+    const long long n16 = (long long)ntok * row16;
+    hipLaunchKernelGGL(vit_batch_copy_v_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s,
+                       (const uint4*)qkv, (uint4*)out, ntok, row16);
+    return check_launch("mhada_vit_batch_attn");
+  }
   if (L <= 8) {
-    // the vectorised form needs 16-byte aligned rows (qkv, out); MHADA_VIT_ATTN_VEC=0 selects
-    // the per-lane form (A/B)
+    // bf16: the vectorised form (16-byte aligned rows in qkv and out; 97 -> 67 us at 1024^2 B4).
+    // fp32 keeps the per-lane form: its vectorised instance needs ~214 VGPRs and measured
+    // 54.8 vs 51.4 us at 512^2 B8. MHADA_VIT_ATTN_VEC=0 selects the per-lane form (A/B).
     const char* e = getenv("MHADA_VIT_ATTN_VEC");
-    if (!(e && e[0] == '0') && aligned16(qkv) && aligned16(out)) {
+    if (dtype != MHADA_F32 && !(e && e[0] == '0') && aligned16(qkv) && aligned16(out)) {
       const dim3 g32((unsigned)((pairs + 31) / 32));
-      if (dtype == MHADA_F32)
-        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<float>), g32, dim3(256), 0, s, (const float*)qkv, (float*)out, L,
-                           ntok, heads);
-      else
-        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
-                           ntok, heads);
+      hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
+                         ntok, heads);
       return check_launch("mhada_vit_batch_attn");
     }
     if (dtype == MHADA_F32)
@@ -660,8 +693,8 @@ extern "C" int mhada_instnorm_stats(const float* x, float* mu, float* rstd, doub
   hipLaunchKernelGGL(in_partial_kernel, dim3((C + 63) / 64, B, splits), dim3(256), 0, s, x, work, B, N, C, splits);
   int rc = check_launch("mhada_instnorm_stats/partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, work, mu, rstd, B, N, C,
-                     splits, eps);
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((B * C + 15) / 16), dim3(256), 0, s, work, mu, rstd, B, N, C, splits,
+                     eps);
   return check_launch("mhada_instnorm_stats/finalize");
 }
 

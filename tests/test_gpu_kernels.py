@@ -145,9 +145,10 @@ def test_layernorm(dt):
     assert rel(y, ref) < (1e-6 if dt == torch.float32 else 5e-3)
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt,vec", [(torch.float32, "1"), (torch.bfloat16, "1"), (torch.bfloat16, "0")])
 @pytest.mark.parametrize("L", [1, 2, 3, 8, 11])
-def test_vit_batch_attention_matches_nn_mha(dt, L):
+def test_vit_batch_attention_matches_nn_mha(dt, vec, L, monkeypatch):
+    monkeypatch.setenv("MHADA_VIT_ATTN_VEC", vec)  # bf16 L <= 8: vectorised form unless "0"
     N, C, heads = 300, 512, 8
     mha = torch.nn.MultiheadAttention(C, heads).to(DEV).double()
     x = rnd(L, N, C, seed=L).double()
@@ -168,7 +169,7 @@ def test_pos_embed(oh, ow):
     assert rel(y, ref) < 1e-6
 
 
-@pytest.mark.parametrize("B,N,C", [(3, 4097, 512), (1, 37, 68), (2, 16384, 512)])
+@pytest.mark.parametrize("B,N,C", [(3, 4097, 512), (1, 37, 68), (2, 16384, 512), (1, 32400, 512)])
 def test_instnorm_stats(B, N, C):
     x = rnd(B, N, C, seed=2) * 5 + 10
     mu, rstd = ops.instnorm_stats(x)
