@@ -30,6 +30,7 @@ struct GemmP {
   const void* r; long long ldr, sr1, sr2;
   void* c; long long ldc, sc1, sc2;
   int relu, tiles_n, ntiles;
+  int lds_epi;  // ping-pong kernels: stage the output through LDS (MHADA_GEMM_LDSEPI=0: direct stores)
 };
 
 template <typename TC> struct Cfg {
@@ -266,6 +267,88 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
   }
 }
 
+
+// Epilogue through a per-wave LDS scratch (4 KiB = one 32x32 fp32 block): the accumulator
+// block (lane = row r32, 4-column groups 8g + 4h) is written raw, read back row-major (lane =
+// row 8i + (lane >> 3), columns 4 (lane & 7) .. +3) and stored so that one store instruction
+// covers 8 rows x 32 columns (64-128 contiguous bytes per row) instead of 32 rows x 16 B;
+// bias, ReLU and the residual (read in the same coalesced layout) are applied in row layout.
+// The 16-B chunk c of row r sits at slot c ^ (r & 7) (spreads both the column-group writes and
+// the row reads over the banks).  No barrier: each wave owns its scratch.
+template <typename TO, int TM, int TN>
+MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, int z2, int mrow0, int ncol0,
+                              int lane, float* scr) {
+  TO* cbase = reinterpret_cast<TO*>(p.c) + z1 * p.sc1 + z2 * p.sc2;
+  const TO* rbase = p.r ? reinterpret_cast<const TO*>(p.r) + z1 * p.sr1 + z2 * p.sr2 : nullptr;
+  const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int rr = lane >> 3, cq = lane & 7;  // read-back: row rr (+ 8i), 16-B chunk cq
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = ncol0 + ni * 32 + 4 * cq;
+    f32x4 bb = {0.f, 0.f, 0.f, 0.f};
+    if (bbase) {
+      if (n + 3 < p.N) {
+        bb = *reinterpret_cast<const f32x4*>(bbase + n);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bb[e] = n + e < p.N ? bbase[n + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 2 * g + h;
+        *reinterpret_cast<f32x4*>(scr + r32 * 32 + 4 * (c ^ (r32 & 7))) =
+            f32x4{acc[mi][ni][4 * g], acc[mi][ni][4 * g + 1], acc[mi][ni][4 * g + 2], acc[mi][ni][4 * g + 3]};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f32x4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 8 * i + rr;
+        v[i] = *reinterpret_cast<const f32x4*>(scr + r * 32 + 4 * (cq ^ (r & 7)));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mrow0 + mi * 32 + 8 * i + rr;
+        if (m >= p.M) continue;
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = v[i][e] + bb[e];
+          if (p.relu) x[e] = fmaxf(x[e], 0.f);
+        }
+        TO* crow = cbase + (long long)m * p.ldc;
+        const TO* rrow = rbase ? rbase + (long long)m * p.ldr : nullptr;
+        if (n + 3 < p.N) {
+          if constexpr (sizeof(TO) == 4) {
+            if (rrow) {
+              const f32x4 q = *reinterpret_cast<const f32x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) x[e] += q[e];
+            }
+            *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+          } else {
+            if (rrow) {
+              const bf16x4 q = *reinterpret_cast<const bf16x4*>(rrow + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) x[e] += (float)q[e];
+            }
+            *reinterpret_cast<bf16x4*>(crow + n) = bf16x4{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e < p.N) crow[n + e] = from_f32<TO>(x[e] + (rrow ? to_f32<TO>(rrow[n + e]) : 0.f));
+          }
+        }
+      }
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------
 // BM x BN block tile, WM x WN waves (NT = 64*WM*WN threads); each wave owns a
@@ -612,7 +695,9 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   constexpr int CE = 16 / sizeof(TC), BK = 8 * CE, PE = 1024 / sizeof(TC), HALF = 128 * BK, TILE = (2 + NWH) * HALF;
   constexpr int NSLOT = BN == 256 ? 2 : 3;
   typedef typename Vec16<TC>::type Frag;
-  __shared__ __attribute__((aligned(16))) TC smem[NSLOT * TILE];  // 128 / 144 KiB, the only LDS object
+  // BN = 256 adds 8 x 4 KiB of epilogue scratch (store_tile_lds): 160 KiB in all
+  constexpr int SCR = BN == 256 ? 8 * 4096 / (int)sizeof(TC) : 0;
+  __shared__ __attribute__((aligned(16))) TC smem[NSLOT * TILE + SCR];  // 160 / 144 KiB, the only LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wc = wave & 3;
@@ -802,7 +887,15 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     // tile boundary: re-align the groups so both store in the same interval (a store between
     // staggered barriers would hold the other group's compute phase), then re-stagger
     if (grp == 0) PP_BARRIER();
-    store_tile<TO, 4, TN>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * TN * 32, h);
+    if constexpr (SCR > 0) {
+      if (p.lds_epi)
+        store_tile_lds<TO, 4, TN>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane,
+                                  reinterpret_cast<float*>(smem + NSLOT * TILE) + wave * 1024);
+      else
+        store_tile<TO, 4, TN>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * TN * 32, h);
+    } else {
+      store_tile<TO, 4, TN>(p, acc, cur.z1, cur.z2, cur.m0 + grp * 128 + r32, cur.n0 + wc * TN * 32, h);
+    }
     if (!has_nxt) break;
     if (grp == 1) PP_BARRIER();
     zero_acc();
@@ -834,6 +927,8 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
+  const char* le = getenv("MHADA_GEMM_LDSEPI");
+  p.lds_epi = !(le && le[0] == '0');
   const long long total = (long long)p.ntiles * nz;
   if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());

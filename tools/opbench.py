@@ -58,6 +58,8 @@ def gemm_suite():
             r = torch.randn(M, N, device=dev) if res else None
             fns = {"ours": lambda: ops.linear(x, w, b, out, residual=r, relu=relu),
                    "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
+            fns["epi_direct"] = lambda: with_env("MHADA_GEMM_LDSEPI", "0", ops.linear, x, w, b, out, residual=r,
+                                                 relu=relu)
             if dt == torch.bfloat16:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
@@ -68,6 +70,23 @@ def gemm_suite():
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
                   + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
+
+
+def gemm_k_suite():
+    """Main-loop rate vs K: the same M x N at growing K separates the per-tile prologue/epilogue
+    cost (fixed per tile) from the K-loop rate."""
+    dev = "cuda"
+    M, N = 65536, 1536
+    for K in (512, 1024, 2048, 4096):
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device=dev)
+        t = bench({"ours": lambda: ops.linear(x, w, b, torch.bfloat16),
+                   "epi_direct": lambda: with_env("MHADA_GEMM_LDSEPI", "0", ops.linear, x, w, b, torch.bfloat16),
+                   "torch": lambda: torch.addmm(b.to(torch.bfloat16), x, w.t())})
+        fl = 2 * M * N * K
+        print(f"gemmK bf16 M={M} N={N} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF"
+                                                             for k, v in t.items()))
 
 
 def out3_suite():
@@ -103,6 +122,8 @@ def conv_suite():
             if dt == torch.bfloat16 and 64 < Co <= 128:
                 fns["pp128_off"] = lambda: with_env("MHADA_GEMM_PP128", "0", ops.conv3x3, ops.upsample2x(x) if up else x,
                                                     w, bias, dt, upsample=False)
+            if Co > 128 and not (dt == torch.float32 and up):
+                fns["epi_direct"] = lambda: with_env("MHADA_GEMM_LDSEPI", "0", ops.conv3x3, x, w, bias, dt, upsample=up)
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
@@ -120,6 +141,8 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     if what in ("gemm", "all"):
         gemm_suite()
+    if what in ("gemmk",):
+        gemm_k_suite()
     if what in ("conv", "all"):
         conv_suite()
     if what in ("out3", "conv", "all"):
