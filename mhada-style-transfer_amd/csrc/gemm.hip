@@ -981,9 +981,14 @@ static bool pp_offsets_fit(const GemmP& p, int amode) {
 // under the ~34 TB/s L2 ceiling at MFMA rate.
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
-  // N <= 64: 8 waves of 32x64 (one 256x64 tile keeps 8 waves per CU at 92 KiB of LDS; a
-  // 4-wave 64x64-per-wave form with 2 workgroups per CU measured 1.3-2x slower)
-  if (p.N <= 64) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
+  // N <= 64: 128x64 tiles of 4 waves x (32x64), two workgroups per CU (55 KiB of LDS each), whose
+  // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (MHADA_GEMM_N64=256
+  // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
+  if (p.N <= 64) {
+    const char* e64 = getenv("MHADA_GEMM_N64");
+    if (e64 && e64[0] == '2') return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
+    return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
+  }
   if constexpr (sizeof(TC) == 4) {
     // persistent ping-pong (256x256 tiles) when there are at least as many tiles as CUs (below
     // that the 128x128 kernel keeps more of the chip busy); MHADA_GEMM_PP=0 / PERSIST=0 disable

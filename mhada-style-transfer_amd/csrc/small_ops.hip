@@ -562,6 +562,96 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
 }
 
 // ---------------------------------------------------------------------------------------
+// fp32 form of the last decoder layer: the same strip of 4-row x 64-pixel tiles, but VALU
+// (fp32 MFMA would spend 16/3 of the FLOPs on zero weight rows at 1/16 of the bf16 rate): the
+// reflect-padded 6 x 66-pixel halo is staged in LDS in CC-channel chunks (double buffered, the
+// next chunk in flight in registers during this chunk's FMAs); lane = output pixel, wave =
+// output row, weights wave-uniform (scalar operands).  The per-pixel kernel above reads every
+// input pixel 9x as lane-strided 16-B loads (one cache line per lane per load) and is
+// load-issue bound: 744 -> 219 us at 512^2 B8 with CC = 16 (63 KiB of LDS, two workgroups per
+// CU; CC = 32: 306 us at one workgroup per CU, CC = 8: 329 us).
+// ---------------------------------------------------------------------------------------
+template <int CIN, int CC>
+__global__ void __launch_bounds__(256) conv_out3_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            int H, int W, int tiles_x, int strips_y, int clamp255) {
+  constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2, LP = CC + 4, NCK = CIN / CC;
+  constexpr int Q = CC / 4, NQ = HR * HC * Q, PER = (NQ + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float tile[2][HR * HC * LP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bt = blockIdx.x, tx = bt % tiles_x, sy = (bt / tiles_x) % strips_y, b = bt / (tiles_x * strips_y);
+  const int x0 = tx * TC, ys = sy * TR * kOut3Rows;
+  const float* xb = x + (long long)b * H * W * CIN;
+  f32x4 st[PER];
+  // halo chunk (rows y0-1 .. y0+4, channels ck*CC ..), reflect-padded, clamped past the image
+  auto fetch = [&](int y0, int ck) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = min(tid + 256 * i, NQ - 1);
+      const int pix = c / Q, q = c - pix * Q;
+      const int r = pix / HC, cc = pix - r * HC;
+      int Y = y0 - 1 + r, X = x0 - 1 + cc;
+      Y = Y < 0 ? -Y : (Y >= H ? 2 * H - 2 - Y : Y);
+      X = X < 0 ? -X : (X >= W ? 2 * W - 2 - X : X);
+      Y = min(max(Y, 0), H - 1);
+      X = min(max(X, 0), W - 1);
+      st[i] = *reinterpret_cast<const f32x4*>(xb + ((long long)Y * W + X) * CIN + ck * CC + 4 * q);
+    }
+  };
+  auto commit = [&](float* t) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + 256 * i;
+      if (c < NQ) {
+        const int pix = c / Q, q = c - pix * Q;
+        *reinterpret_cast<f32x4*>(t + pix * LP + 4 * q) = st[i];
+      }
+    }
+  };
+  const int nt = min(kOut3Rows, (H - ys + TR - 1) / TR);
+  const int steps = nt * NCK;
+  fetch(ys, 0);
+  commit(tile[0]);
+  __syncthreads();
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int s = 0; s < steps; ++s) {
+    const int r = s / NCK, ck = s - r * NCK;
+    const float* t = tile[s & 1];
+    if (s + 1 < steps) fetch(ys + ((s + 1) / NCK) * TR, (s + 1) % NCK);
+    const float* wt = w + ck * CC * 3;  // [tap][cin][out]
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const float* px = t + ((wave + tap / 3) * HC + lane + tap % 3) * LP;
+      const float* wtap = wt + tap * CIN * 3;
+#pragma unroll
+      for (int c = 0; c < CC; c += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(px + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a0 = fmaf(v[e], wtap[(c + e) * 3 + 0], a0);
+          a1 = fmaf(v[e], wtap[(c + e) * 3 + 1], a1);
+          a2 = fmaf(v[e], wtap[(c + e) * 3 + 2], a2);
+        }
+      }
+    }
+    if (ck == NCK - 1) {
+      const int yy = ys + r * TR + wave, xx = x0 + lane;
+      if (yy < H && xx < W) {
+        float o[3] = {fmaxf(a0 + bias[0], 0.f), fmaxf(a1 + bias[1], 0.f), fmaxf(a2 + bias[2], 0.f)};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (clamp255) o[k] = fminf(o[k], 255.f);
+          y[(((long long)b * 3 + k) * H + yy) * W + xx] = o[k];
+        }
+      }
+      a0 = a1 = a2 = 0.f;
+    }
+    if (s + 1 < steps) commit(tile[(s + 1) & 1]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Bilinear x2 upsample on NHWC (F.interpolate(scale_factor=2, bilinear, align_corners=False),
 // conv.py:71): one thread per (output pixel, 8-channel group), fp32 blend in PyTorch's order.
 // ---------------------------------------------------------------------------------------
@@ -769,6 +859,21 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
       hipLaunchKernelGGL((conv_out3_mfma_kernel<64>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
     else
       hipLaunchKernelGGL((conv_out3_mfma_kernel<32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
+    return check_launch("mhada_conv3x3_out3");
+  }
+  // fp32, Cin 32/64: the LDS-tiled kernel (MHADA_OUT3_TILE=0 selects the per-pixel kernel)
+  const char* et = getenv("MHADA_OUT3_TILE");
+  if (dtype == MHADA_F32 && !(et && et[0] == '0') && (Cin == 32 || Cin == 64)) {
+    const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3Rows - 1) / (4 * kOut3Rows);
+    const long long nb = (long long)B * strips_y * tiles_x;
+    if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");
+    const dim3 g((unsigned)nb);
+    if (Cin == 64)
+      hipLaunchKernelGGL((conv_out3_f32_kernel<64, 16>), g, dim3(256), 0, s, (const float*)x, w, b, y, H, W, tiles_x,
+                         strips_y, clamp255);
+    else
+      hipLaunchKernelGGL((conv_out3_f32_kernel<32, 16>), g, dim3(256), 0, s, (const float*)x, w, b, y, H, W, tiles_x,
+                         strips_y, clamp255);
     return check_launch("mhada_conv3x3_out3");
   }
 #define OUT3_CASE(CI)                                                                                          \

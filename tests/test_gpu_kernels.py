@@ -117,13 +117,16 @@ def test_upsample2x(dt, H, W, C):
     assert rel(y.permute(0, 3, 1, 2), ref) < (1e-6 if dt == torch.float32 else 5e-3)
 
 
-@pytest.mark.parametrize("dt,mfma", [(torch.float32, "1"), (torch.bfloat16, "1"), (torch.bfloat16, "0")])
+@pytest.mark.parametrize("dt,mfma", [(torch.float32, "1"), (torch.float32, "0"), (torch.bfloat16, "1"),
+                                     (torch.bfloat16, "0")])
 @pytest.mark.parametrize("clamp", [False, True])
-@pytest.mark.parametrize("B,H,W,Ci", [(2, 20, 33, 64), (1, 64, 128, 64), (1, 7, 70, 32), (1, 9, 65, 128)])
+@pytest.mark.parametrize("B,H,W,Ci", [(2, 20, 33, 64), (1, 64, 128, 64), (1, 7, 70, 32), (1, 9, 65, 128),
+                                      (3, 37, 2, 64)])
 def test_conv_out3(dt, mfma, clamp, B, H, W, Ci, monkeypatch):
-    """Last decoder layer; bf16 runs the MFMA tile kernel (bf16 weights) or, with
-    MHADA_OUT3_MFMA=0, the per-pixel VALU kernel (fp32 weights)."""
+    """Last decoder layer; bf16 runs the MFMA tile kernel (bf16 weights), fp32 the LDS-tiled
+    VALU kernel, or, with mfma == "0", the per-pixel VALU kernel (fp32 weights)."""
     monkeypatch.setenv("MHADA_OUT3_MFMA", mfma)
+    monkeypatch.setenv("MHADA_OUT3_TILE", mfma)
     x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(9)).to(DEV).to(dt)
     w = rnd(3, Ci, 3, 3, scale=0.5, seed=2)
     b = rnd(3, seed=3) * 30

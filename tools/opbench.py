@@ -98,6 +98,8 @@ def out3_suite():
         fns = {"default": lambda: ops.conv3x3_out3(x, w, b)}
         if dt == torch.bfloat16:
             fns["valu"] = lambda: with_env("MHADA_OUT3_MFMA", "0", ops.conv3x3_out3, x, w, b)
+        else:
+            fns["per_pixel"] = lambda: with_env("MHADA_OUT3_TILE", "0", ops.conv3x3_out3, x, w, b)
         t = bench(fns)
         by = x.numel() * x.element_size() + B * 3 * res * res * 4
         print(f"out3 {str(dt)[6:]:8s} B={B} {res}^2: " + "  ".join(f"{k} {v * 1e3:8.1f} us {by / v / 1e6:7.1f} GB/s"
@@ -127,6 +129,9 @@ def conv_suite():
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
+            if Co <= 64:
+                fns["n64_256"] = lambda: with_env("MHADA_GEMM_N64", "256", ops.conv3x3, ops.upsample2x(x) if up else x, w,
+                                                  bias, dt, upsample=False)
             if up:
                 fns["sep"] = lambda: ops.conv3x3(ops.upsample2x(x), w, bias, dt, upsample=False)
                 fns["upsample_only"] = lambda: ops.upsample2x(x)
