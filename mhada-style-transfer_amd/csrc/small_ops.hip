@@ -477,12 +477,15 @@ __global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x,
 // ---------------------------------------------------------------------------------------
 constexpr int kOut3Rows = 8;  // row tiles per workgroup strip
 
-template <int CIN>
+template <int CIN, int CC>
 __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, float* __restrict__ y,
                                                              int H, int W, int tiles_x, int strips_y, int clamp255) {
-  constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2, LP = CIN + 8, NH = CIN / 32;
-  constexpr int CH = CIN / 8, NCH = HR * HC * CH, PER = (NCH + 255) / 256;
+  // the halo is staged in CC-channel chunks (CC = 32: 31 KiB per buffer, two workgroups per CU;
+  // the whole 64-channel halo double-buffered took 114 KiB, one workgroup per CU)
+  constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2, LP = CC + 8, NH = CIN / 32, NCK = CIN / CC;
+  constexpr int HPC = CC / 32;  // 32-channel MFMA steps per chunk
+  constexpr int CH = CC / 8, NCH = HR * HC * CH, PER = (NCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16 tile[2][HR * HC * LP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bt = blockIdx.x, tx = bt % tiles_x, sy = (bt / tiles_x) % strips_y, b = bt / (tiles_x * strips_y);
@@ -500,10 +503,10 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
       for (int j = 0; j < 8; ++j)
         wa[tap][hc][j] = (bf16)(n < 3 ? w[(tap * CIN + 32 * hc + 8 * kg + j) * 3 + n] : 0.f);
   const float bo[3] = {bias[0], bias[1], bias[2]};
-  // halo of row tile r (rows y0-1 .. y0+4, reflect-padded, clamped past the image edge) into
-  // registers; written to LDS after the previous tile's MFMAs
+  // halo chunk (rows y0-1 .. y0+4, channels ck*CC ..; reflect-padded, clamped past the image
+  // edge) into registers; written to LDS after the current chunk's MFMAs
   bf16x8 st[PER];
-  auto fetch = [&](int y0) {
+  auto fetch = [&](int y0, int ck) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = min(tid + 256 * i, NCH - 1);
@@ -514,7 +517,7 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
       X = X < 0 ? -X : (X >= W ? 2 * W - 2 - X : X);
       Y = min(max(Y, 0), H - 1);
       X = min(max(X, 0), W - 1);
-      st[i] = *reinterpret_cast<const bf16x8*>(xb + ((long long)Y * W + X) * CIN + ch * 8);
+      st[i] = *reinterpret_cast<const bf16x8*>(xb + ((long long)Y * W + X) * CIN + ck * CC + ch * 8);
     }
   };
   auto commit = [&](bf16* t) {
@@ -528,36 +531,50 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
     }
   };
   const int nt = min(kOut3Rows, (H - ys + TR - 1) / TR);
-  fetch(ys);
+  fetch(ys, 0);
   commit(tile[0]);
   __syncthreads();
+  int buf = 0;
   for (int r = 0; r < nt; ++r) {
-    const bf16* t = tile[r & 1];
-    if (r + 1 < nt) fetch(ys + (r + 1) * TR);
     const int yy = ys + r * TR + wave;
+    f32x4 acc[TC / 16];
 #pragma unroll
-    for (int g = 0; g < TC / 16; ++g) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < TC / 16; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const bf16* px = t + ((wave + tap / 3) * HC + 16 * g + (lane & 15) + tap % 3) * LP + 8 * kg;
+    for (int ck = 0; ck < NCK; ++ck) {
+      const bf16* t = tile[buf];
+      const bool more = ck + 1 < NCK || r + 1 < nt;
+      if (more) fetch(ck + 1 < NCK ? ys + r * TR : ys + (r + 1) * TR, (ck + 1) % NCK);
 #pragma unroll
-        for (int hc = 0; hc < NH; ++hc)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[tap][hc], *reinterpret_cast<const bf16x8*>(px + 32 * hc),
-                                                        acc, 0, 0, 0);
-      }
-      const int xx = x0 + 16 * g + lane;
-      if (lane < 16 && yy < H && xx < W) {
+      for (int g = 0; g < TC / 16; ++g) {
 #pragma unroll
-        for (int o = 0; o < 3; ++o) {
-          float v = fmaxf(acc[o] + bo[o], 0.f);
-          if (clamp255) v = fminf(v, 255.f);
-          y[(((long long)b * 3 + o) * H + yy) * W + xx] = v;
+        for (int tap = 0; tap < 9; ++tap) {
+          const bf16* px = t + ((wave + tap / 3) * HC + 16 * g + (lane & 15) + tap % 3) * LP + 8 * kg;
+#pragma unroll
+          for (int hc = 0; hc < HPC; ++hc)
+            acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[tap][ck * HPC + hc],
+                                                             *reinterpret_cast<const bf16x8*>(px + 32 * hc), acc[g],
+                                                             0, 0, 0);
         }
       }
+      if (ck == NCK - 1) {
+#pragma unroll
+        for (int g = 0; g < TC / 16; ++g) {
+          const int xx = x0 + 16 * g + lane;
+          if (lane < 16 && yy < H && xx < W) {
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+              float v = fmaxf(acc[g][o] + bo[o], 0.f);
+              if (clamp255) v = fminf(v, 255.f);
+              y[(((long long)b * 3 + o) * H + yy) * W + xx] = v;
+            }
+          }
+        }
+      }
+      if (more) commit(tile[buf ^ 1]);
+      __syncthreads();
+      buf ^= 1;
     }
-    if (r + 1 < nt) commit(tile[(r + 1) & 1]);
-    __syncthreads();
   }
 }
 
@@ -856,9 +873,9 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
     if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");
     const dim3 g((unsigned)nb);
     if (Cin == 64)
-      hipLaunchKernelGGL((conv_out3_mfma_kernel<64>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
+      hipLaunchKernelGGL((conv_out3_mfma_kernel<64, 32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
     else
-      hipLaunchKernelGGL((conv_out3_mfma_kernel<32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
+      hipLaunchKernelGGL((conv_out3_mfma_kernel<32, 32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
     return check_launch("mhada_conv3x3_out3");
   }
   // fp32, Cin 32/64: the LDS-tiled kernel (MHADA_OUT3_TILE=0 selects the per-pixel kernel)
