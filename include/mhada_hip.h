@@ -135,6 +135,20 @@ int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
                const float* fcs_mu, const float* fcs_rstd, const float* v_mu, void* out,
                int dtype, int B, int H, int Nc, int Ns, int activation, mhada_stream_t stream);
 
+/* MHAda attention for training (adaDecoder.py:186-198 under train_image.py:139 autograd), fp32,
+ * one (batch, head) per leading index, all rows of 64 (or 128) contiguous floats:
+ *   fwd: q [BH][Nc][64], k [BH][Ns][64], v [BH][Ns][64] (V' = V - mean_tokens(V)),
+ *        x [BH][Nc][64] (InstanceNorm(fcs)) -> out' = sqrt(max(E2'-M'^2,1e-6))*x + M' [BH][Nc][64],
+ *        mo = [M' | E2'] [BH][Nc][128], lse = log2(sum exp) row normaliser [BH][Nc].
+ *   bwd: dmo = [dM' | dE2'] [BH][Nc][128], dd = dM'.M' + dE2'.E2' [BH][Nc]
+ *        -> dq [BH][Nc][64], dk [BH][Ns][64], dv [BH][Ns][64] (gradient w.r.t. V').
+ * Replaces the autograd of adaDecoder.py:186-198 (bmm/softmax/bmm/sqrt); A is never stored. */
+int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const float* x, float* out,
+                         float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
+int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
+                         const float* dmo, const float* dd, float* dq, float* dk, float* dv,
+                         int BH, int Nc, int Ns, mhada_stream_t stream);
+
 /* Last decoder layer (conv.py:96, ConvReLU(64, 3)): ReflectionPad2d(1) + conv3x3 Cin->3 +
  * bias + ReLU on NHWC x [B][H][W][Cin] (dtype), written NCHW fp32 y [B][3][H][W] — the
  * module's output layout.  clamp255 != 0 also applies the caller's clamp(0,255)

@@ -1,0 +1,391 @@
+// MHAda attention for the training path: forward that keeps the softmax statistics, and the
+// backward (dual accumulator M / E2), fp32 on v_mfma_f32_32x32x2_f32.
+//
+// Reference: AdaAttnMultiHead.forward (MHAdaSTr/network/adaDecoder.py:186-198) under
+// train_image.py:93-144 autograd.  Per (batch, head), with Q [Nc][64], K [Ns][64], V' [Ns][64]
+// (V' = V - mean_tokens(V), centred by the caller under autograd: the variance is
+// shift-invariant and d(out)/dV = d(out)/dV' exactly, since the rows of A sum to one) and
+// X = InstanceNorm(fcs) [Nc][64]:
+//   A = softmax(Q K^T)   M' = A V'   E2' = A V'^2   var = E2' - M'^2
+//   out' = sqrt(max(var, 1e-6)) * X + M'            (the caller adds mean(V) back)
+// The forward writes out', [M' | E2'] and the log2 row normaliser lse2 = max + log2(sum).
+// The caller turns d(out') into dO = [dM' | dE2'] and D = dM'.M' + dE2'.E2' (elementwise,
+// O(Nc*64)); then with P = A (recomputed from lse2) and dA = dM'.V'^T + dE2'.(V'^2)^T:
+//   dS = P * (dA - D)            (gradient of the natural-unit logits)
+//   dQ = dS K       dK = dS^T Q       dV' = P^T dM' + 2 V' * (P^T dE2')
+// as two deterministic kernels (no atomics): key-stationary dK/dV', query-stationary dQ, each
+// recomputing P — the Nc x Ns matrices never reach HBM (the reference autograd keeps A, the
+// softmax output, and their gradients: 4 B x Nc x Ns per head each).
+//
+// MFMA 32x32x2 f32 layout (cdna_hip_programming.md §3): lane l gives A[l%32][l/32] and
+// B[l/32][l%32]; accumulator register r of lane l is D[acc_row(r, l/32)][l%32].  Every
+// product is arranged so that one operand is an accumulator of the previous product
+// (accumulator-as-operand), so no score or probability ever moves between lanes.
+#include "common.h"
+
+namespace mhada {
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int TT = 32;    // keys (fwd, dQ) or queries (dK/dV') staged per LDS tile
+constexpr int LP = 68;    // padded LDS row of 64 floats
+constexpr int LPO = 132;  // padded LDS row of 128 floats
+
+MHADA_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+MHADA_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+MHADA_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+MHADA_DEV f32x16 mfma(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+struct TrainP {
+  const float* q;    // [BH][Nc][64]
+  const float* k;    // [BH][Ns][64]
+  const float* v;    // [BH][Ns][64] centred V'
+  const float* x;    // [BH][Nc][64] InstanceNorm(fcs)
+  float* out;        // [BH][Nc][64]
+  float* mo;         // [BH][Nc][128]  M' | E2'
+  float* lse;        // [BH][Nc]       log2 units
+  const float* dmo;  // [BH][Nc][128]  dM' | dE2'
+  const float* dd;   // [BH][Nc]       D
+  float* dq;         // [BH][Nc][64]
+  float* dk;         // [BH][Ns][64]
+  float* dv;         // [BH][Ns][64]
+  int Nc, Ns, nb, nblk;  // nb = row blocks per (b, h)
+};
+
+// Stage rows [r0, r0+TT) of a [n][64] matrix into LDS (zero rows past n).
+template <int NT>
+MHADA_DEV void stage64(float* s, const float* g, int r0, int n, int tid) {
+#pragma unroll
+  for (int c = tid; c < TT * 16; c += NT) {
+    const int row = c >> 4, col = (c & 15) * 4;
+    const f32x4 t = r0 + row < n ? ld4(g + (long long)(r0 + row) * 64 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    st4(s + row * LP + col, t);
+  }
+}
+
+// Per-lane row of 64 floats split by lane half: reg[s] = g[row][32h + s] * scale.
+MHADA_DEV void load_half_row(float (&reg)[32], const float* g, int row, bool valid, int h, float scale) {
+  const float* p = g + (long long)(valid ? row : 0) * 64 + 32 * h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 t = ld4(p + 4 * i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) reg[4 * i + e] = valid ? t[e] * scale : 0.f;
+  }
+}
+
+// S^T (keys x queries) in log2 units from the staged K tile and the lane's query row
+// (qr pre-scaled by log2 e); keys past Ns masked to -inf.
+MHADA_DEV f32x16 scores_t(const float* sK, const float (&qr)[32], int k0, int Ns, int h, int r32) {
+  f32x16 S = {};
+  const float* kr = sK + r32 * LP + 32 * h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 kk = ld4(kr + 4 * i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) S = mfma(kk[e], qr[4 * i + e], S);
+  }
+  if (k0 + TT > Ns) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (k0 + acc_row(r, h) >= Ns) S[r] = -INFINITY;
+  }
+  return S;
+}
+
+// ---------------------------------------------------------------------------------------
+// forward: wave = 32 queries (one per lane column), online softmax over 32-key tiles
+// ---------------------------------------------------------------------------------------
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_train_fwd_kernel(const TrainP p) {
+  constexpr int NT = 64 * NW;
+  __shared__ __attribute__((aligned(16))) float sK[TT * LP];
+  __shared__ __attribute__((aligned(16))) float sV[TT * LP];
+  const int t = xcd_remap(blockIdx.x, p.nblk);
+  const long long bh = t / p.nb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = (t % p.nb) * 32 * NW + wave * 32 + r32;
+  const bool qv = q < p.Nc;
+  float qr[32];
+  load_half_row(qr, p.q + bh * p.Nc * 64, q, qv, h, kLog2e);
+  const float* kb = p.k + bh * p.Ns * 64;
+  const float* vb = p.v + bh * p.Ns * 64;
+
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) O[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < p.Ns; k0 += TT) {
+    __syncthreads();
+    stage64<NT>(sK, kb, k0, p.Ns, tid);
+    stage64<NT>(sV, vb, k0, p.Ns, tid);
+    __syncthreads();
+    f32x16 S = scores_t(sK, qr, k0, p.Ns, h, r32);
+    float mx = S[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, S[r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (__any(mx > m)) {  // exact online softmax: rescale whenever the running max moves
+      const float mn = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
+      m = mn;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      S[r] = __builtin_amdgcn_exp2f(S[r] - m);
+      l += S[r];
+    }
+    // O^T (c x queries) += V'^T (c x keys) . P^T (keys x queries); blocks 2,3 take V'^2
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* vr = sV + acc_row(r, h) * LP + r32;
+      const float v0 = vr[0], v1 = vr[32];
+      O[0] = mfma(v0, S[r], O[0]);
+      O[1] = mfma(v1, S[r], O[1]);
+      O[2] = mfma(v0 * v0, S[r], O[2]);
+      O[3] = mfma(v1 * v1, S[r], O[3]);
+    }
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  const float inv = 1.0f / l;
+  const long long row = bh * p.Nc + q;
+  const float* xr = p.x + row * 64;
+  float* orow = p.out + row * 64;
+  float* mrow = p.mo + row * 128;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * cb + 8 * g + 4 * h;
+      const f32x4 xx = ld4(xr + c0);
+      f32x4 o, mm, ee;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[cb][4 * g + e] * inv;
+        const float e2 = O[cb + 2][4 * g + e] * inv;
+        o[e] = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f)) * xx[e] + m1;
+        mm[e] = m1;
+        ee[e] = e2;
+      }
+      st4(orow + c0, o);
+      st4(mrow + c0, mm);
+      st4(mrow + 64 + c0, ee);
+    }
+  if (h == 0) p.lse[row] = m + __log2f(l);
+}
+
+// ---------------------------------------------------------------------------------------
+// dQ: wave = 32 queries; streams 32-key tiles of K, V'
+// ---------------------------------------------------------------------------------------
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) {
+  constexpr int NT = 64 * NW;
+  __shared__ __attribute__((aligned(16))) float sK[TT * LP];
+  __shared__ __attribute__((aligned(16))) float sV[TT * LP];
+  const int t = xcd_remap(blockIdx.x, p.nblk);
+  const long long bh = t / p.nb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = (t % p.nb) * 32 * NW + wave * 32 + r32;
+  const bool qv = q < p.Nc;
+  const long long row = bh * p.Nc + (qv ? q : 0);
+  float qr[32], dm[32], de[32];
+  load_half_row(qr, p.q + bh * p.Nc * 64, q, qv, h, kLog2e);
+  {
+    const float* o = p.dmo + row * 128 + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 a = ld4(o + 4 * i), b = ld4(o + 64 + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dm[4 * i + e] = qv ? a[e] : 0.f;
+        de[4 * i + e] = qv ? b[e] : 0.f;
+      }
+    }
+  }
+  const float L = qv ? p.lse[row] : INFINITY;  // invalid query: P = 0
+  const float D = qv ? p.dd[row] : 0.f;
+  const float* kb = p.k + bh * p.Ns * 64;
+  const float* vb = p.v + bh * p.Ns * 64;
+  f32x16 dQ[2] = {f32x16{}, f32x16{}};
+  for (int k0 = 0; k0 < p.Ns; k0 += TT) {
+    __syncthreads();
+    stage64<NT>(sK, kb, k0, p.Ns, tid);
+    stage64<NT>(sV, vb, k0, p.Ns, tid);
+    __syncthreads();
+    const f32x16 S = scores_t(sK, qr, k0, p.Ns, h, r32);
+    // dA^T (keys x queries) = [V' | V'^2] (keys x 128) . [dM' | dE2']^T
+    f32x16 dA = {};
+    const float* vr = sV + r32 * LP + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 vv = ld4(vr + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dA = mfma(vv[e], dm[4 * i + e], dA);
+        dA = mfma(vv[e] * vv[e], de[4 * i + e], dA);
+      }
+    }
+    f32x16 dS;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dS[r] = __builtin_amdgcn_exp2f(S[r] - L) * (dA[r] - D);
+    // dQ^T (d x queries) += K^T (d x keys) . dS^T (keys x queries)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* kr = sK + acc_row(r, h) * LP + r32;
+      dQ[0] = mfma(kr[0], dS[r], dQ[0]);
+      dQ[1] = mfma(kr[32], dS[r], dQ[1]);
+    }
+  }
+  if (!qv) return;
+  float* o = p.dq + row * 64;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      st4(o + 32 * db + 8 * g + 4 * h, f32x4{dQ[db][4 * g], dQ[db][4 * g + 1], dQ[db][4 * g + 2], dQ[db][4 * g + 3]});
+}
+
+// ---------------------------------------------------------------------------------------
+// dK, dV': wave = 32 keys (one per lane column); streams 32-query tiles of Q, dO, lse2, D
+// ---------------------------------------------------------------------------------------
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_train_dkv_kernel(const TrainP p) {
+  constexpr int NT = 64 * NW;
+  __shared__ __attribute__((aligned(16))) float sQ[TT * LP];
+  __shared__ __attribute__((aligned(16))) float sO[TT * LPO];
+  __shared__ float sL[TT], sD[TT];
+  const int t = xcd_remap(blockIdx.x, p.nblk);
+  const long long bh = t / p.nb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int key = (t % p.nb) * 32 * NW + wave * 32 + r32;
+  const bool kv = key < p.Ns;
+  float kr[32], vr[32];
+  load_half_row(kr, p.k + bh * p.Ns * 64, key, kv, h, kLog2e);
+  load_half_row(vr, p.v + bh * p.Ns * 64, key, kv, h, 1.0f);
+  const float* qb = p.q + bh * p.Nc * 64;
+  const float* ob = p.dmo + bh * p.Nc * 128;
+  const float* lb = p.lse + bh * p.Nc;
+  const float* db = p.dd + bh * p.Nc;
+  f32x16 G1[2] = {f32x16{}, f32x16{}}, G2[2] = {f32x16{}, f32x16{}}, dK[2] = {f32x16{}, f32x16{}};
+  for (int q0 = 0; q0 < p.Nc; q0 += TT) {
+    __syncthreads();
+    stage64<NT>(sQ, qb, q0, p.Nc, tid);
+#pragma unroll
+    for (int c = tid; c < TT * 32; c += NT) {
+      const int rr = c >> 5, col = (c & 31) * 4;
+      const f32x4 v = q0 + rr < p.Nc ? ld4(ob + (long long)(q0 + rr) * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      st4(sO + rr * LPO + col, v);
+    }
+    if (tid < TT) {
+      const bool ok = q0 + tid < p.Nc;
+      sL[tid] = ok ? lb[q0 + tid] : INFINITY;
+      sD[tid] = ok ? db[q0 + tid] : 0.f;
+    }
+    __syncthreads();
+    // S (queries x keys) = Q . K^T, dA (queries x keys) = [dM' | dE2'] . [V' | V'^2]^T
+    f32x16 S = {}, dA = {};
+    const float* qrow = sQ + r32 * LP + 32 * h;
+    const float* orow = sO + r32 * LPO + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 qq = ld4(qrow + 4 * i), o1 = ld4(orow + 4 * i), o2 = ld4(orow + 64 + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int s = 4 * i + e;
+        S = mfma(qq[e], kr[s], S);
+        dA = mfma(o1[e], vr[s], dA);
+        dA = mfma(o2[e], vr[s] * vr[s], dA);
+      }
+    }
+    f32x16 P, dS;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = acc_row(r, h);
+      P[r] = __builtin_amdgcn_exp2f(S[r] - sL[qi]);
+      dS[r] = P[r] * (dA[r] - sD[qi]);
+    }
+    // G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* o = sO + acc_row(r, h) * LPO + r32;
+      const float* qq = sQ + acc_row(r, h) * LP + r32;
+      G1[0] = mfma(o[0], P[r], G1[0]);
+      G1[1] = mfma(o[32], P[r], G1[1]);
+      G2[0] = mfma(o[64], P[r], G2[0]);
+      G2[1] = mfma(o[96], P[r], G2[1]);
+      dK[0] = mfma(qq[0], dS[r], dK[0]);
+      dK[1] = mfma(qq[32], dS[r], dK[1]);
+    }
+  }
+  if (!kv) return;
+  const long long row = bh * p.Ns + key;
+  const float* vg = p.v + row * 64;
+  float* dvr = p.dv + row * 64;
+  float* dkr = p.dk + row * 64;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * cb + 8 * g + 4 * h;
+      const f32x4 vv = ld4(vg + c0);
+      f32x4 a, b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = G1[cb][4 * g + e] + 2.0f * vv[e] * G2[cb][4 * g + e];
+        b[e] = dK[cb][4 * g + e];
+      }
+      st4(dvr + c0, a);
+      st4(dkr + c0, b);
+    }
+}
+
+constexpr int kNW = 4;
+
+bool set_grid(TrainP& p, long long BH, int n) {
+  p.nb = (n + 32 * kNW - 1) / (32 * kNW);
+  const long long nblk = BH * p.nb;
+  if (nblk > (1LL << 31) - 1) return false;
+  p.nblk = (int)nblk;
+  return true;
+}
+
+}  // namespace
+}  // namespace mhada
+
+using namespace mhada;
+
+extern "C" int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const float* x, float* out,
+                                    float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t s_) {
+  if (!q || !k || !v || !x || !out || !mo || !lse || BH <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_train_fwd: bad args");
+  TrainP p = {};
+  p.q = q; p.k = k; p.v = v; p.x = x; p.out = out; p.mo = mo; p.lse = lse; p.Nc = Nc; p.Ns = Ns;
+  if (!set_grid(p, BH, Nc)) return fail("mhada_attn_train_fwd: grid too large");
+  hipLaunchKernelGGL(attn_train_fwd_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
+  return check_launch("mhada_attn_train_fwd");
+}
+
+extern "C" int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
+                                    const float* dmo, const float* dd, float* dq, float* dk, float* dv, int BH,
+                                    int Nc, int Ns, mhada_stream_t s_) {
+  if (!q || !k || !v || !lse || !dmo || !dd || !dq || !dk || !dv || BH <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_train_bwd: bad args");
+  const hipStream_t s = (hipStream_t)s_;
+  TrainP p = {};
+  p.q = q; p.k = k; p.v = v; p.lse = const_cast<float*>(lse); p.dmo = dmo; p.dd = dd; p.dq = dq; p.dk = dk; p.dv = dv;
+  p.Nc = Nc; p.Ns = Ns;
+  if (!set_grid(p, BH, Nc)) return fail("mhada_attn_train_bwd: grid too large");
+  hipLaunchKernelGGL(attn_train_dq_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_bwd: grid too large");
+  hipLaunchKernelGGL(attn_train_dkv_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  return check_launch("mhada_attn_train_bwd");
+}

@@ -9,10 +9,13 @@ whose state_dict keys match the reference), so autograd reaches exactly those pa
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence
 
 import torch
 import torch.nn.functional as F
+
+from . import ops
 
 # decoder layers and whether bilinear x2 follows them (conv.py:78-94)
 DECODER_ORDER = (("conv1", 0, True), ("conv1", 1, False), ("conv1", 2, False), ("conv1", 3, False),
@@ -59,8 +62,70 @@ def _softmax_or_cosine(q, k, activation: str):
     return s / s.sum(dim=-1, keepdim=True)  # adaDecoder.py:24-34
 
 
+class MHAdaAttnFn(torch.autograd.Function):
+    """The attention core of adaDecoder.py:186-198 on the HIP training kernels
+    (csrc/attn_train.hip): out' = sqrt(max(E2' - M'^2, 1e-6)) * x + M' with M' = A V',
+    E2' = A V'^2, A = softmax(q k^T).  q, x (BH, Nc, 64); k, v (BH, Ns, 64), v centred.
+    A is never stored: the backward recomputes it from the saved row normaliser."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, x):
+        out, mo, lse = ops.attn_train_fwd(q, k, v, x)
+        ctx.save_for_backward(q, k, v, x, mo, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, x, mo, lse = ctx.saved_tensors
+        dout = dout.contiguous()
+        m, e2 = mo[..., :64], mo[..., 64:]
+        var = e2 - m * m
+        sd = var.clamp(min=1e-6).sqrt()
+        dx = dout * sd
+        dvar = (dout * x) * (0.5 / sd) * (var >= 1e-6)  # clamp passes the gradient where var >= min
+        dm = dout - 2.0 * m * dvar
+        dmo = torch.cat([dm, dvar], dim=-1)
+        dd = (dm * m + dvar * e2).sum(dim=-1)
+        dq, dk, dv = ops.attn_train_bwd(q, k, v, lse, dmo.contiguous(), dd.contiguous())
+        return dq, dk, dv, dx
+
+
+def _fused_train_attn(blk, fc) -> bool:
+    return (fc.is_cuda and fc.dtype == torch.float32 and blk.activation_name == "softmax"
+            and blk.head_dim == 64 and os.environ.get("MHADA_TRAIN_ATTN", "hip") != "torch")
+
+
+def _heads_rows(t: torch.Tensor, H: int) -> torch.Tensor:
+    """(B, 64H, h, w) -> (B*H, h*w, 64) contiguous."""
+    B, C, h, w = t.shape
+    return t.reshape(B, H, C // H, h * w).transpose(2, 3).reshape(B * H, h * w, C // H).contiguous()
+
+
+def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206) with the per-head 1x1 convs batched as
+    one grouped conv over the same parameter objects and the attention on MHAdaAttnFn."""
+    B, C, h, w = fc.shape
+    H = blk.num_heads
+
+    def grouped(mods, t):
+        wgt = torch.cat([m.weight for m in mods], 0)
+        bias = torch.cat([m.bias for m in mods], 0)
+        return F.conv2d(t, wgt, bias, groups=H)
+
+    q = _heads_rows(grouped(blk.f_list, F.instance_norm(fc)), H)
+    k = _heads_rows(grouped(blk.g_list, F.instance_norm(fs)), H)
+    v = _heads_rows(grouped(blk.h_list, fs), H)
+    vmu = v.mean(dim=1, keepdim=True)
+    x = _heads_rows(F.instance_norm(fcs), H)
+    o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
+    o = o.reshape(B, H, h * w, C // H).transpose(2, 3).reshape(B, C, h, w)
+    return blk.out_conv(o)
+
+
 def block_forward(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
     """AdaAttnMultiHead.forward (adaDecoder.py:162-206)."""
+    if _fused_train_attn(blk, fc):
+        return block_forward_fused(blk, fc, fs, fcs)
     B, _, h, w = fc.shape
     d = blk.head_dim
     outs = []

@@ -229,6 +229,49 @@ def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch
     return out
 
 
+def _rows64(*ts: torch.Tensor) -> None:
+    _need_gpu(*ts)
+    for t in ts:
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("training attention operands must be contiguous float32")
+
+
+def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.Tensor):
+    """``mhada_attn_train_fwd``: q, x (BH, Nc, 64); k, v (BH, Ns, 64) with v centred.
+    Returns out' (BH, Nc, 64), [M' | E2'] (BH, Nc, 128), lse2 (BH, Nc)."""
+    _rows64(q, k, v, x)
+    BH, Nc, d = q.shape
+    Ns = k.shape[1]
+    if d != 64 or k.shape != (BH, Ns, 64) or v.shape != k.shape or x.shape != q.shape:
+        raise ValueError(f"attn_train_fwd: bad shapes q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)} "
+                         f"x{tuple(x.shape)}")
+    out = torch.empty_like(q)
+    mo = torch.empty(BH, Nc, 128, device=q.device, dtype=torch.float32)
+    lse = torch.empty(BH, Nc, device=q.device, dtype=torch.float32)
+    rc = _lib.load().mhada_attn_train_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), x.data_ptr(), out.data_ptr(),
+                                          mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns, _stream())
+    _lib.check(rc, "mhada_attn_train_fwd")
+    return out, mo, lse
+
+
+def attn_train_bwd(q, k, v, lse, dmo, dd):
+    """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64)."""
+    _rows64(q, k, v, lse, dmo, dd)
+    BH, Nc, _ = q.shape
+    Ns = k.shape[1]
+    if lse.shape != (BH, Nc) or dmo.shape != (BH, Nc, 128) or dd.shape != (BH, Nc) or k.shape != (BH, Ns, 64) \
+            or v.shape != k.shape:
+        raise ValueError("attn_train_bwd: bad shapes")
+    dq = torch.empty_like(q)
+    dk = torch.empty_like(k)
+    dv = torch.empty_like(v)
+    rc = _lib.load().mhada_attn_train_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
+                                          dd.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), BH, Nc, Ns,
+                                          _stream())
+    _lib.check(rc, "mhada_attn_train_bwd")
+    return dq, dk, dv
+
+
 # ---- video path: optical-flow warping (NCHW fp32) ---------------------------------------
 _PADDING = {"zeros": 0, "border": 1}
 
