@@ -95,6 +95,17 @@ def _fused_train_attn(blk, fc) -> bool:
             and blk.head_dim == 64 and os.environ.get("MHADA_TRAIN_ATTN", "hip") != "torch")
 
 
+def _head_proj(mods, t: torch.Tensor, H: int) -> torch.Tensor:
+    """Per-head 1x1 convs (adaDecoder.py:188-190, f/g/h_list[i] on channel slice i) as one
+    head-batched matmul on the modules' own parameters: (B, 64H, h, w) -> (B*H, h*w, 64)."""
+    B, C, h, w = t.shape
+    d = C // H
+    wgt = torch.stack([m.weight.reshape(d, d) for m in mods], 0)  # (H, out, in)
+    bias = torch.stack([m.bias for m in mods], 0).unsqueeze(1)     # (H, 1, out)
+    y = torch.matmul(t.reshape(B, H, d, h * w).transpose(2, 3), wgt.transpose(1, 2)) + bias
+    return y.reshape(B * H, h * w, d)
+
+
 def _heads_rows(t: torch.Tensor, H: int) -> torch.Tensor:
     """(B, 64H, h, w) -> (B*H, h*w, 64) contiguous."""
     B, C, h, w = t.shape
@@ -102,19 +113,14 @@ def _heads_rows(t: torch.Tensor, H: int) -> torch.Tensor:
 
 
 def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
-    """AdaAttnMultiHead.forward (adaDecoder.py:162-206) with the per-head 1x1 convs batched as
-    one grouped conv over the same parameter objects and the attention on MHAdaAttnFn."""
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206) with the per-head 1x1 convs batched
+    over heads (hipBLASLt; a groups=8 conv2d took MIOpen's 4.5 ms CK weight-gradient kernel)
+    and the attention on MHAdaAttnFn."""
     B, C, h, w = fc.shape
     H = blk.num_heads
-
-    def grouped(mods, t):
-        wgt = torch.cat([m.weight for m in mods], 0)
-        bias = torch.cat([m.bias for m in mods], 0)
-        return F.conv2d(t, wgt, bias, groups=H)
-
-    q = _heads_rows(grouped(blk.f_list, F.instance_norm(fc)), H)
-    k = _heads_rows(grouped(blk.g_list, F.instance_norm(fs)), H)
-    v = _heads_rows(grouped(blk.h_list, fs), H)
+    q = _head_proj(blk.f_list, F.instance_norm(fc), H).contiguous()
+    k = _head_proj(blk.g_list, F.instance_norm(fs), H).contiguous()
+    v = _head_proj(blk.h_list, fs, H)
     vmu = v.mean(dim=1, keepdim=True)
     x = _heads_rows(F.instance_norm(fcs), H)
     o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
