@@ -23,6 +23,8 @@
 // (accumulator-as-operand), so no score or probability ever moves between lanes.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace mhada {
 namespace {
 
@@ -55,16 +57,31 @@ struct TrainP {
   int Nc, Ns, nb, nblk;  // nb = row blocks per (b, h)
 };
 
-// Stage rows [r0, r0+TT) of a [n][64] matrix into LDS (zero rows past n).
-template <int NT>
-MHADA_DEV void stage64(float* s, const float* g, int r0, int n, int tid) {
+// Register-staged copy of rows [r0, r0+TT) of a [n][W] matrix (zero rows past n) into a padded
+// LDS tile: load() issues the global reads one tile ahead, store() writes them after the
+// current tile's math (one barrier per tile, two LDS buffers).
+template <int NT, int W>
+struct Stager {
+  static constexpr int CPR = W / 4;             // 16-B chunks per row
+  static constexpr int N = TT * CPR / NT;       // chunks per thread
+  static constexpr int LD = W == 64 ? LP : LPO;
+  static_assert(N * NT == TT * CPR, "tile must divide evenly");
+  f32x4 r[N];
+  MHADA_DEV void load(const float* g, int r0, int n, int tid) {
 #pragma unroll
-  for (int c = tid; c < TT * 16; c += NT) {
-    const int row = c >> 4, col = (c & 15) * 4;
-    const f32x4 t = r0 + row < n ? ld4(g + (long long)(r0 + row) * 64 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-    st4(s + row * LP + col, t);
+    for (int i = 0; i < N; ++i) {
+      const int c = tid + NT * i, row = c / CPR, col = (c % CPR) * 4;
+      r[i] = r0 + row < n ? ld4(g + (long long)(r0 + row) * W + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
-}
+  MHADA_DEV void store(float* s, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int c = tid + NT * i, row = c / CPR, col = (c % CPR) * 4;
+      st4(s + row * LD + col, r[i]);
+    }
+  }
+};
 
 // Per-lane row of 64 floats split by lane half: reg[s] = g[row][32h + s] * scale.
 MHADA_DEV void load_half_row(float (&reg)[32], const float* g, int row, bool valid, int h, float scale) {
@@ -102,8 +119,8 @@ MHADA_DEV f32x16 scores_t(const float* sK, const float (&qr)[32], int k0, int Ns
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) attn_train_fwd_kernel(const TrainP p) {
   constexpr int NT = 64 * NW;
-  __shared__ __attribute__((aligned(16))) float sK[TT * LP];
-  __shared__ __attribute__((aligned(16))) float sV[TT * LP];
+  __shared__ __attribute__((aligned(16))) float sK[2][TT * LP];
+  __shared__ __attribute__((aligned(16))) float sV[2][TT * LP];
   const int t = xcd_remap(blockIdx.x, p.nblk);
   const long long bh = t / p.nb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
@@ -118,12 +135,21 @@ __global__ void __launch_bounds__(64 * NW) attn_train_fwd_kernel(const TrainP p)
 #pragma unroll
   for (int i = 0; i < 4; ++i) O[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
-  for (int k0 = 0; k0 < p.Ns; k0 += TT) {
-    __syncthreads();
-    stage64<NT>(sK, kb, k0, p.Ns, tid);
-    stage64<NT>(sV, vb, k0, p.Ns, tid);
-    __syncthreads();
-    f32x16 S = scores_t(sK, qr, k0, p.Ns, h, r32);
+  Stager<NT, 64> gk, gv;
+  gk.load(kb, 0, p.Ns, tid);
+  gv.load(vb, 0, p.Ns, tid);
+  gk.store(sK[0], tid);
+  gv.store(sV[0], tid);
+  __syncthreads();
+  const int nt = (p.Ns + TT - 1) / TT;
+  for (int t = 0; t < nt; ++t) {
+    const int k0 = t * TT, cb = t & 1;
+    const bool nxt = t + 1 < nt;
+    if (nxt) {
+      gk.load(kb, k0 + TT, p.Ns, tid);
+      gv.load(vb, k0 + TT, p.Ns, tid);
+    }
+    f32x16 S = scores_t(sK[cb], qr, k0, p.Ns, h, r32);
     float mx = S[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, S[r]);
@@ -146,13 +172,18 @@ __global__ void __launch_bounds__(64 * NW) attn_train_fwd_kernel(const TrainP p)
     // O^T (c x queries) += V'^T (c x keys) . P^T (keys x queries); blocks 2,3 take V'^2
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float* vr = sV + acc_row(r, h) * LP + r32;
+      const float* vr = sV[cb] + acc_row(r, h) * LP + r32;
       const float v0 = vr[0], v1 = vr[32];
       O[0] = mfma(v0, S[r], O[0]);
       O[1] = mfma(v1, S[r], O[1]);
       O[2] = mfma(v0 * v0, S[r], O[2]);
       O[3] = mfma(v1 * v1, S[r], O[3]);
     }
+    if (nxt) {
+      gk.store(sK[cb ^ 1], tid);
+      gv.store(sV[cb ^ 1], tid);
+    }
+    __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
   if (!qv) return;
@@ -189,8 +220,8 @@ __global__ void __launch_bounds__(64 * NW) attn_train_fwd_kernel(const TrainP p)
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) {
   constexpr int NT = 64 * NW;
-  __shared__ __attribute__((aligned(16))) float sK[TT * LP];
-  __shared__ __attribute__((aligned(16))) float sV[TT * LP];
+  __shared__ __attribute__((aligned(16))) float sK[2][TT * LP];
+  __shared__ __attribute__((aligned(16))) float sV[2][TT * LP];
   const int t = xcd_remap(blockIdx.x, p.nblk);
   const long long bh = t / p.nb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
@@ -216,15 +247,24 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) 
   const float* kb = p.k + bh * p.Ns * 64;
   const float* vb = p.v + bh * p.Ns * 64;
   f32x16 dQ[2] = {f32x16{}, f32x16{}};
-  for (int k0 = 0; k0 < p.Ns; k0 += TT) {
-    __syncthreads();
-    stage64<NT>(sK, kb, k0, p.Ns, tid);
-    stage64<NT>(sV, vb, k0, p.Ns, tid);
-    __syncthreads();
-    const f32x16 S = scores_t(sK, qr, k0, p.Ns, h, r32);
+  Stager<NT, 64> gk, gv;
+  gk.load(kb, 0, p.Ns, tid);
+  gv.load(vb, 0, p.Ns, tid);
+  gk.store(sK[0], tid);
+  gv.store(sV[0], tid);
+  __syncthreads();
+  const int nt = (p.Ns + TT - 1) / TT;
+  for (int t = 0; t < nt; ++t) {
+    const int k0 = t * TT, cb = t & 1;
+    const bool nxt = t + 1 < nt;
+    if (nxt) {
+      gk.load(kb, k0 + TT, p.Ns, tid);
+      gv.load(vb, k0 + TT, p.Ns, tid);
+    }
+    const f32x16 S = scores_t(sK[cb], qr, k0, p.Ns, h, r32);
     // dA^T (keys x queries) = [V' | V'^2] (keys x 128) . [dM' | dE2']^T
     f32x16 dA = {};
-    const float* vr = sV + r32 * LP + 32 * h;
+    const float* vr = sV[cb] + r32 * LP + 32 * h;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const f32x4 vv = ld4(vr + 4 * i);
@@ -240,10 +280,15 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) 
     // dQ^T (d x queries) += K^T (d x keys) . dS^T (keys x queries)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float* kr = sK + acc_row(r, h) * LP + r32;
+      const float* kr = sK[cb] + acc_row(r, h) * LP + r32;
       dQ[0] = mfma(kr[0], dS[r], dQ[0]);
       dQ[1] = mfma(kr[32], dS[r], dQ[1]);
     }
+    if (nxt) {
+      gk.store(sK[cb ^ 1], tid);
+      gv.store(sV[cb ^ 1], tid);
+    }
+    __syncthreads();
   }
   if (!qv) return;
   float* o = p.dq + row * 64;
@@ -257,12 +302,12 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) 
 // ---------------------------------------------------------------------------------------
 // dK, dV': wave = 32 keys (one per lane column); streams 32-query tiles of Q, dO, lse2, D
 // ---------------------------------------------------------------------------------------
-template <int NW>
-__global__ void __launch_bounds__(64 * NW) attn_train_dkv_kernel(const TrainP p) {
+template <int NW, int OCC>
+__global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const TrainP p) {
   constexpr int NT = 64 * NW;
-  __shared__ __attribute__((aligned(16))) float sQ[TT * LP];
-  __shared__ __attribute__((aligned(16))) float sO[TT * LPO];
-  __shared__ float sL[TT], sD[TT];
+  __shared__ __attribute__((aligned(16))) float sQ[2][TT * LP];
+  __shared__ __attribute__((aligned(16))) float sO[2][TT * LPO];
+  __shared__ float sL[2][TT], sD[2][TT];
   const int t = xcd_remap(blockIdx.x, p.nblk);
   const long long bh = t / p.nb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
@@ -276,25 +321,40 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dkv_kernel(const TrainP p)
   const float* lb = p.lse + bh * p.Nc;
   const float* db = p.dd + bh * p.Nc;
   f32x16 G1[2] = {f32x16{}, f32x16{}}, G2[2] = {f32x16{}, f32x16{}}, dK[2] = {f32x16{}, f32x16{}};
-  for (int q0 = 0; q0 < p.Nc; q0 += TT) {
-    __syncthreads();
-    stage64<NT>(sQ, qb, q0, p.Nc, tid);
-#pragma unroll
-    for (int c = tid; c < TT * 32; c += NT) {
-      const int rr = c >> 5, col = (c & 31) * 4;
-      const f32x4 v = q0 + rr < p.Nc ? ld4(ob + (long long)(q0 + rr) * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-      st4(sO + rr * LPO + col, v);
+  Stager<NT, 64> gq;
+  Stager<NT, 128> go;
+  float gl = INFINITY, gd = 0.f;
+  auto load = [&](int q0) {
+    gq.load(qb, q0, p.Nc, tid);
+    go.load(ob, q0, p.Nc, tid);
+    if (tid < TT && q0 + tid < p.Nc) {
+      gl = lb[q0 + tid];
+      gd = db[q0 + tid];
+    } else {
+      gl = INFINITY;  // padded query: P = 0
+      gd = 0.f;
     }
+  };
+  auto store = [&](int buf) {
+    gq.store(sQ[buf], tid);
+    go.store(sO[buf], tid);
     if (tid < TT) {
-      const bool ok = q0 + tid < p.Nc;
-      sL[tid] = ok ? lb[q0 + tid] : INFINITY;
-      sD[tid] = ok ? db[q0 + tid] : 0.f;
+      sL[buf][tid] = gl;
+      sD[buf][tid] = gd;
     }
-    __syncthreads();
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  const int nt = (p.Nc + TT - 1) / TT;
+  for (int t = 0; t < nt; ++t) {
+    const int cb = t & 1;
+    const bool nxt = t + 1 < nt;
+    if (nxt) load((t + 1) * TT);
     // S (queries x keys) = Q . K^T, dA (queries x keys) = [dM' | dE2'] . [V' | V'^2]^T
     f32x16 S = {}, dA = {};
-    const float* qrow = sQ + r32 * LP + 32 * h;
-    const float* orow = sO + r32 * LPO + 32 * h;
+    const float* qrow = sQ[cb] + r32 * LP + 32 * h;
+    const float* orow = sO[cb] + r32 * LPO + 32 * h;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const f32x4 qq = ld4(qrow + 4 * i), o1 = ld4(orow + 4 * i), o2 = ld4(orow + 64 + 4 * i);
@@ -310,14 +370,14 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dkv_kernel(const TrainP p)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = acc_row(r, h);
-      P[r] = __builtin_amdgcn_exp2f(S[r] - sL[qi]);
-      dS[r] = P[r] * (dA[r] - sD[qi]);
+      P[r] = __builtin_amdgcn_exp2f(S[r] - sL[cb][qi]);
+      dS[r] = P[r] * (dA[r] - sD[cb][qi]);
     }
     // G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float* o = sO + acc_row(r, h) * LPO + r32;
-      const float* qq = sQ + acc_row(r, h) * LP + r32;
+      const float* o = sO[cb] + acc_row(r, h) * LPO + r32;
+      const float* qq = sQ[cb] + acc_row(r, h) * LP + r32;
       G1[0] = mfma(o[0], P[r], G1[0]);
       G1[1] = mfma(o[32], P[r], G1[1]);
       G2[0] = mfma(o[64], P[r], G2[0]);
@@ -325,6 +385,8 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dkv_kernel(const TrainP p)
       dK[0] = mfma(qq[0], dS[r], dK[0]);
       dK[1] = mfma(qq[32], dS[r], dK[1]);
     }
+    if (nxt) store(cb ^ 1);
+    __syncthreads();
   }
   if (!kv) return;
   const long long row = bh * p.Ns + key;
@@ -386,6 +448,12 @@ extern "C" int mhada_attn_train_bwd(const float* q, const float* k, const float*
   if (!set_grid(p, BH, Nc)) return fail("mhada_attn_train_bwd: grid too large");
   hipLaunchKernelGGL(attn_train_dq_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_bwd: grid too large");
-  hipLaunchKernelGGL(attn_train_dkv_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  // default: 288 registers, one wave per SIMD, no spills.  MHADA_TRAIN_DKV_OCC=2 forces two
+  // waves per SIMD at 256 registers (18 spilled): measured the same (tools/train_attn_bench.py)
+  const char* e = getenv("MHADA_TRAIN_DKV_OCC");
+  if (e && e[0] == '2')
+    hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 2>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  else
+    hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   return check_launch("mhada_attn_train_bwd");
 }

@@ -1,0 +1,38 @@
+"""Time the training attention kernels at the train_image.py 512^2 B8 block shape
+(BH = 64, Nc = Ns = 4096): forward, backward (dQ + dK/dV'), per-kernel averages via HIP events.
+usage: python tools/train_attn_bench.py [reps]"""
+import os
+import sys
+
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "mhada-style-transfer_amd")]
+import torch  # noqa: E402
+
+from mhada_hip import ops  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+BH, N = 64, 4096
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, x = (torch.randn(BH, N, 64, device="cuda", generator=g) * 0.3 for _ in range(3))
+v = torch.randn(BH, N, 64, device="cuda", generator=g)
+out, mo, lse = ops.attn_train_fwd(q, k, v, x)
+dmo = torch.randn(BH, N, 128, device="cuda", generator=g)
+dd = torch.randn(BH, N, device="cuda", generator=g)
+pairs = BH * N * N
+
+
+def timeit(fn):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+tf = timeit(lambda: ops.attn_train_fwd(q, k, v, x))
+tb = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd))
+print(f"occ={os.environ.get('MHADA_TRAIN_DKV_OCC', '1')} fwd {tf:.3f} ms ({384 * pairs / tf / 1e9:.1f} TF)  "
+      f"bwd {tb:.3f} ms ({1280 * pairs / tb / 1e9:.1f} TF)")
