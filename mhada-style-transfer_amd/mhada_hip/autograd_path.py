@@ -1,8 +1,10 @@
-"""Differentiable forward passes for the training path (v1: PyTorch-ROCm autograd).
+"""Differentiable forward passes for the training path.
 
 When a forward needs gradients (``torch.is_grad_enabled()`` and a parameter or input requires
 grad — ``train_image.py:93-144``, feature-inversion scripts), the ``network`` modules route
-here instead of to the inference HIP kernels, which have no backward yet.
+here instead of to the inference engine.  The MHAda attention core runs on the HIP training
+kernels (``MHAdaAttnFn``: csrc/attn_train.hip forward + backward); the remaining ops use
+PyTorch-ROCm autograd.
 Each function evaluates the reference algorithm on the module's own parameter containers
 (the same ``nn.Conv2d`` / ``nn.MultiheadAttention`` / ``nn.Linear`` / ``nn.LayerNorm`` objects
 whose state_dict keys match the reference), so autograd reaches exactly those parameters.
