@@ -56,19 +56,35 @@ def flops_per_frame(res: int, style_res: int) -> dict:
     return {"total": vit(nc) + vit(ns) + mhada + dec, "attn_per_block": 6 * nc * ns * C}
 
 
+ATTN_SOURCES = ("mhada-style-transfer_amd/csrc/attn.hip", "mhada-style-transfer_amd/csrc/attn_common.h",
+                "mhada-style-transfer_amd/csrc/common.h")
+
+
+def attn_source_sha() -> str:
+    """sha256 (16 hex) of the attention kernel's sources: ties a PMC measurement to this build."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ATTN_SOURCES:
+        with open(os.path.join(REPO, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(cfg_key):
     """HBM bytes per mhada_attn launch from the latest committed rocprofv3 PMC pass
     (profiles/rNN_pmc_traffic.json, produced by tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE
     per the gfx950 corrections).  PMC counters need their own profiler run, so the bench reads
-    the measured value rather than collecting it live."""
+    the measured value rather than collecting it live — and only when that pass measured THIS
+    attention kernel source (attn_src_sha recorded by tools/pmc_traffic.py); otherwise null."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        d = json.load(f).get(cfg_key)
-    if not d:
-        return None, None
+        doc = json.load(f)
+    d = doc.get(cfg_key)
+    if not d or doc.get("attn_src_sha") != attn_source_sha():
+        return None, f"{os.path.relpath(files[-1], REPO)} (stale: other attention source)" if d else None
     return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
@@ -236,8 +252,22 @@ def run_train(steps, warmup, rank, world):
             "last_losses": last}
 
 
-def cpu_baseline(seconds_budget=30.0):
-    """numpy oracle (restatement of the reference CPU path) on one 512x512 frame."""
+def cpu_model() -> str:
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def cpu_baseline():
+    """numpy oracle (oracle/mhada_oracle.py, restatement of the reference CPU path) timed on the
+    box's host cores at B=1: 3 frames at 256^2, 2 at 512^2 (the headline value) and one 1024^2
+    frame."""
     import numpy as np
     from mhada_hip.recipe import recipe_state_dict, seeded_image
     from oracle import mhada_oracle as O
@@ -251,19 +281,21 @@ def cpu_baseline(seconds_budget=30.0):
     p_vc = O.to_numpy_params(recipe_state_dict("vit_c", shapes(network.VisionTransformer(pos_embedding=True))))
     p_vs = O.to_numpy_params(recipe_state_dict("vit_s", shapes(network.VisionTransformer(pos_embedding=False))))
     p_ada = O.to_numpy_params(recipe_state_dict("ada", shapes(network.AdaAttnTransformerMultiHead())))
-    c = seeded_image(1, 512, 512, 11).numpy()
-    s = seeded_image(1, 512, 512, 12).numpy()
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        O.stylize(c, s, p_vc, p_vs, p_ada)
-        n += 1
-        if time.perf_counter() - t0 > seconds_budget / 3 or n >= 3:
-            break
-    el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frame(s) of 512x512 B=1 through oracle/mhada_oracle.py (numpy fp32, "
-                      f"{threads} BLAS threads), same recipe weights; {el:.1f} s"}
+    per_res = {}
+    for res, n in ((256, 3), (512, 2), (1024, 1)):
+        c = seeded_image(1, res, res, 11).numpy()
+        s = seeded_image(1, res, res, 12).numpy()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            O.stylize(c, s, p_vc, p_vs, p_ada)
+        el = time.perf_counter() - t0
+        per_res[f"{res}x{res}_b1"] = {"frames_per_s": round(n / el, 5), "frames": n, "seconds": round(el, 2)}
+    v = per_res["512x512_b1"]
+    return {"value": v["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "per_resolution": per_res,
+            "sample": f"oracle/mhada_oracle.py (numpy fp32, {threads} BLAS threads, same recipe weights) at B=1: "
+                      + ", ".join(f"{k} {d['frames']} frame(s) in {d['seconds']} s" for k, d in per_res.items())
+                      + "; value = the 512x512 rate"}
 
 
 def main():
@@ -274,7 +306,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the 1024^2 bf16 config")
     ap.add_argument("--only-secondary", action="store_true", help="run only the 1024^2 bf16 config (profiling)")
-    ap.add_argument("--train", action="store_true", help="BASELINE configs[3]: DP training step at 512^2")
+    ap.add_argument("--train", action="store_true", help="only BASELINE configs[3]: DP training step at 512^2")
+    ap.add_argument("--no-train", action="store_true", help="skip the training config in the default line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -309,6 +342,7 @@ def main():
     videos = {} if args.no_secondary else {
         f"video_1080p_s256_{'f32' if dt == torch.float32 else 'bf16'}": run_video(dt, args.steps, args.warmup, rank, world)
         for dt in (torch.float32, torch.bfloat16)}
+    train = None if (args.no_secondary or args.no_train) else run_train(args.steps, args.warmup, rank, world)
 
     if rank == 0:
         line = {
@@ -334,6 +368,9 @@ def main():
                                                      "tflops_whole_step", "roofline", "config")}}
         if videos:
             line.setdefault("configs", {}).update(videos)
+        if train is not None:
+            line.setdefault("configs", {})["train_512_b8_f32"] = {
+                k: train[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "last_losses")}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

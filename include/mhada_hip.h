@@ -36,8 +36,20 @@ enum {
   MHADA_A_CONV3X3_UP2 = 3  /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
 };
 
-int mhada_abi_version(void);  /* 2 (mhada_fold_block gained kscale) */
+int mhada_abi_version(void);  /* 3 (mhada_set_tuning / mhada_get_tuning) */
 const char* mhada_last_error(void);
+
+/* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
+ * measurements and tests that force a rare path.  Initialised ONCE, at the first call into the
+ * library, from MHADA_<NAME> environment variables (NAME upper-cased); afterwards only these
+ * calls change it (not thread-safe against concurrent launches: set knobs between launches).
+ * Knobs (value range): attn_fixed_shift (0|1), attn_waves (4|8), attn_tk (64|128),
+ * attn_prio (0|1), vit_attn_vec (0|1), out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1),
+ * gemm_persist (0|1), gemm_pp128 (0|1), gemm_ldsepi (0|1), gemm_n64 (128|256).
+ * Returns MHADA_ERR_ARG for an unknown knob or an out-of-range value.  No reference
+ * counterpart (the reference has no kernels). */
+int mhada_set_tuning(const char* name, int value);
+int mhada_get_tuning(const char* name, int* value);
 
 /*
  * Batched NT GEMM with fused epilogue:

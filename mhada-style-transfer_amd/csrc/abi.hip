@@ -1,5 +1,10 @@
-// C-ABI plumbing shared by every entry point: thread-local error message, launch checks.
+// C-ABI plumbing shared by every entry point: thread-local error message, launch checks, the
+// kernel-variant table (read once at the first launch, see Tuning in common.h).
 #include "common.h"
+
+#include <mutex>
+#include <stdlib.h>
+#include <string.h>
 
 namespace mhada {
 
@@ -21,8 +26,75 @@ int check_launch(const char* what) {
   return MHADA_OK;
 }
 
+namespace {
+struct Knob {
+  const char* name;  // mhada_set_tuning name; env variable MHADA_<NAME upper-cased>
+  int Tuning::*field;
+};
+const Knob kKnobs[] = {
+    {"attn_fixed_shift", &Tuning::attn_fixed_shift}, {"attn_waves", &Tuning::attn_waves},
+    {"attn_tk", &Tuning::attn_tk},                   {"attn_prio", &Tuning::attn_prio},
+    {"vit_attn_vec", &Tuning::vit_attn_vec},         {"out3_mfma", &Tuning::out3_mfma},
+    {"out3_tile", &Tuning::out3_tile},               {"gemm_pp", &Tuning::gemm_pp},
+    {"gemm_persist", &Tuning::gemm_persist},         {"gemm_pp128", &Tuning::gemm_pp128},
+    {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
+};
+
+Tuning g_tuning;
+std::once_flag g_tuning_once;
+
+void read_env_once() {
+  std::call_once(g_tuning_once, [] {
+    for (const Knob& k : kKnobs) {
+      std::string env = "MHADA_";
+      for (const char* c = k.name; *c; ++c) env += (char)(*c >= 'a' && *c <= 'z' ? *c - 32 : *c);
+      if (const char* v = getenv(env.c_str())) g_tuning.*k.field = atoi(v);
+    }
+  });
+}
+
+bool valid(const char* name, int v) {
+  if (!strcmp(name, "attn_waves")) return v == 4 || v == 8;
+  if (!strcmp(name, "attn_tk")) return v == 64 || v == 128;
+  if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
+  return v == 0 || v == 1;
+}
+}  // namespace
+
+const Tuning& tuning() {
+  read_env_once();
+  return g_tuning;
+}
+
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 2; }  // 2: mhada_fold_block takes kscale
+extern "C" int mhada_abi_version(void) { return 3; }  // 3: mhada_set_tuning / mhada_get_tuning
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }
+
+extern "C" int mhada_set_tuning(const char* name, int value) {
+  using namespace mhada;
+  read_env_once();
+  if (!name) return fail("mhada_set_tuning: null name");
+  for (const Knob& k : kKnobs) {
+    if (!strcmp(k.name, name)) {
+      if (!valid(name, value)) return fail(std::string("mhada_set_tuning: bad value for ") + name);
+      g_tuning.*k.field = value;
+      return MHADA_OK;
+    }
+  }
+  return fail(std::string("mhada_set_tuning: unknown knob ") + name);
+}
+
+extern "C" int mhada_get_tuning(const char* name, int* value) {
+  using namespace mhada;
+  read_env_once();
+  if (!name || !value) return fail("mhada_get_tuning: null argument");
+  for (const Knob& k : kKnobs) {
+    if (!strcmp(k.name, name)) {
+      *value = g_tuning.*k.field;
+      return MHADA_OK;
+    }
+  }
+  return fail(std::string("mhada_get_tuning: unknown knob ") + name);
+}

@@ -31,8 +31,6 @@
 // onto one XCD so they share K/V in its L2.
 #include "attn_common.h"
 
-#include <stdio.h>
-#include <stdlib.h>
 #include <type_traits>
 
 namespace mhada {
@@ -557,7 +555,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
     __syncthreads();
   }
   // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD"
-  // item 4: waves 4-7 lose every arbitration otherwise); MHADA_ATTN_PRIO=0 disables (A/B)
+  // item 4: waves 4-7 lose every arbitration otherwise); tuning attn_prio = 0 disables (A/B)
   if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   // full tiles 1 .. NFULL-1: no max, no branch
   for (int t = 1; t < NFULL; ++t) {
@@ -581,27 +579,11 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
 }
 
-// bf16 softmax: the fixed-shift kernel (default) or, with MHADA_ATTN_KERNEL=w8, the online-max
-// 8-wave kernel (read per call, for A/B measurements; cosine always uses the latter).
-static bool attn_bf16_fixed_shift() {
-  const char* e = getenv("MHADA_ATTN_KERNEL");
-  return !(e && e[0] == 'w');
-}
-
-// Waves per workgroup (32 queries each).  Default per dtype; MHADA_ATTN_WAVES=4|8 overrides
-// (read per call, for in-process A/B measurements).
-static int attn_waves(int dtype) {
-  const char* e = getenv("MHADA_ATTN_WAVES");
-  if (e && (atoi(e) == 4 || atoi(e) == 8)) return atoi(e);
-  return 8;
-}
-
-// Keys per bf16 tile (64 | 128): MHADA_ATTN_TK overrides the default (read per call).
-static int attn_tk() {
-  const char* e = getenv("MHADA_ATTN_TK");
-  if (e && atoi(e) == 64) return 64;
-  return 128;
-}
+// Variant selection (Tuning, common.h): the fixed-shift kernel is the bf16 softmax default; the
+// online-max kernel serves the cosine activation and, through attn_fixed_shift = 0, tests / A-B.
+static bool attn_bf16_fixed_shift() { return tuning().attn_fixed_shift != 0; }
+static int attn_waves(int) { return tuning().attn_waves; }
+static int attn_tk() { return tuning().attn_tk; }
 
 template <int NW>
 static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s) {
@@ -645,7 +627,7 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   AttnP p;
   p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
   p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
-  p.prio = !(getenv("MHADA_ATTN_PRIO") && getenv("MHADA_ATTN_PRIO")[0] == '0');
+  p.prio = tuning().attn_prio;
   p.ldt = (Ns + 63) / 64 * 64;
   const int nw = attn_waves(dtype);
   p.nqb = (Nc + 32 * nw - 1) / (32 * nw);

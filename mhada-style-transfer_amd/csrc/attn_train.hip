@@ -448,12 +448,8 @@ extern "C" int mhada_attn_train_bwd(const float* q, const float* k, const float*
   if (!set_grid(p, BH, Nc)) return fail("mhada_attn_train_bwd: grid too large");
   hipLaunchKernelGGL(attn_train_dq_kernel<kNW>, dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_bwd: grid too large");
-  // default: 288 registers, one wave per SIMD, no spills.  MHADA_TRAIN_DKV_OCC=2 forces two
-  // waves per SIMD at 256 registers (18 spilled): measured the same (tools/train_attn_bench.py)
-  const char* e = getenv("MHADA_TRAIN_DKV_OCC");
-  if (e && e[0] == '2')
-    hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 2>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
-  else
-    hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  // 288 registers, one wave per SIMD, no spills (two waves per SIMD at 256 registers spilled 18
+  // and measured the same, tools/train_attn_bench.py)
+  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   return check_launch("mhada_attn_train_bwd");
 }

@@ -22,6 +22,27 @@ void set_error(const std::string& msg);
 int fail(const std::string& msg);  // sets message, returns MHADA_ERR_ARG
 int check_launch(const char* what);  // hipGetLastError -> MHADA_ERR_LAUNCH
 
+// ---- kernel-variant selection -------------------------------------------------------------
+// The defaults are the measured winners.  The non-default variants exist for A/B measurements
+// and for tests that force a rare path (e.g. the online-max bf16 attention).  The values are
+// read ONCE, at the first launch, from MHADA_* environment variables, and can be changed only
+// through mhada_set_tuning() (include/mhada_hip.h) — never per launch from the environment.
+struct Tuning {
+  int attn_fixed_shift = 1;  // bf16 softmax attention: fixed-shift kernel (0: online-max kernel)
+  int attn_waves = 8;        // attention waves per workgroup (4 | 8)
+  int attn_tk = 128;         // bf16 attention keys per tile (64 | 128)
+  int attn_prio = 1;         // fixed-shift kernel: s_setprio(1) for the younger wave half
+  int vit_attn_vec = 1;      // bf16 batch-axis attention: vectorised form
+  int out3_mfma = 1;         // bf16 last decoder layer: MFMA tile kernel (0: per-pixel VALU)
+  int out3_tile = 1;         // fp32 last decoder layer: LDS-tiled kernel (0: per-pixel)
+  int gemm_pp = 1;           // ping-pong GEMM kernels
+  int gemm_persist = 1;      // persistent form of the ping-pong GEMM
+  int gemm_pp128 = 1;        // 256x128 persistent ping-pong form for 65..128 columns
+  int gemm_ldsepi = 1;       // ping-pong epilogue staged through LDS
+  int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
+};
+const Tuning& tuning();
+
 // ---- scalar conversions -----------------------------------------------------------------
 template <typename T> MHADA_DEV float to_f32(T x);
 template <> MHADA_DEV float to_f32<float>(float x) { return x; }

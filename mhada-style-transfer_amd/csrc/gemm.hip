@@ -30,7 +30,7 @@ struct GemmP {
   const void* r; long long ldr, sr1, sr2;
   void* c; long long ldc, sc1, sc2;
   int relu, tiles_n, ntiles;
-  int lds_epi;  // ping-pong kernels: stage the output through LDS (MHADA_GEMM_LDSEPI=0: direct stores)
+  int lds_epi;  // ping-pong kernels: stage the output through LDS (tuning gemm_ldsepi = 0: direct stores)
 };
 
 template <typename TC> struct Cfg {
@@ -916,19 +916,15 @@ static int num_cus() {
   return n;
 }
 
-// MHADA_GEMM_PERSIST=0 selects the one-shot ping-pong kernel (A/B runs; read per call).
-static bool persist_enabled() {
-  const char* e = getenv("MHADA_GEMM_PERSIST");
-  return !(e && e[0] == '0');
-}
+// tuning gemm_persist = 0 selects the one-shot ping-pong kernel (A/B runs)
+static bool persist_enabled() { return tuning().gemm_persist != 0; }
 
 template <typename TC, typename TO, int AMODE, int BN = 256>
 static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
-  const char* le = getenv("MHADA_GEMM_LDSEPI");
-  p.lds_epi = !(le && le[0] == '0');
+  p.lds_epi = tuning().gemm_ldsepi;
   const long long total = (long long)p.ntiles * nz;
   if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
@@ -943,11 +939,8 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
 }
 
 // The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
-// spans addressable with 32-bit element offsets.  MHADA_GEMM_PP=0 disables it (A/B runs).
-static bool pp_enabled() {
-  const char* e = getenv("MHADA_GEMM_PP");
-  return !(e && e[0] == '0');
-}
+// spans addressable with 32-bit element offsets.  tuning gemm_pp = 0 disables it (A/B runs).
+static bool pp_enabled() { return tuning().gemm_pp != 0; }
 
 template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN, int WM, int WN>
 static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
@@ -982,16 +975,15 @@ static bool pp_offsets_fit(const GemmP& p, int amode) {
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // N <= 64: 128x64 tiles of 4 waves x (32x64), two workgroups per CU (55 KiB of LDS each), whose
-  // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (MHADA_GEMM_N64=256
+  // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (tuning gemm_n64 = 256
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
   if (p.N <= 64) {
-    const char* e64 = getenv("MHADA_GEMM_N64");
-    if (e64 && e64[0] == '2') return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
+    if (tuning().gemm_n64 == 256) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
   }
   if constexpr (sizeof(TC) == 4) {
     // persistent ping-pong (256x256 tiles) when there are at least as many tiles as CUs (below
-    // that the 128x128 kernel keeps more of the chip busy); MHADA_GEMM_PP=0 / PERSIST=0 disable
+    // that the 128x128 kernel keeps more of the chip busy); tuning gemm_pp / gemm_persist = 0 disable
     if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && t256 >= num_cus() && pp_enabled() && persist_enabled() &&
@@ -1007,9 +999,8 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       if constexpr (sizeof(TA) == 2 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
         if (p.N > 128 && p.K % 64 == 0 && pp_enabled() && pp_offsets_fit(p, AMODE))
           return launch_gemm_pp<bf16, TO, AMODE>(p, nz, s);
-        // 65..128 columns: the 256x128 persistent ping-pong form (MHADA_GEMM_PP128=0 disables)
-        const char* e128 = getenv("MHADA_GEMM_PP128");
-        if (p.N > 64 && p.N <= 128 && p.K % 64 == 0 && p.K >= 128 && !(e128 && e128[0] == '0') && pp_enabled() &&
+        // 65..128 columns: the 256x128 persistent ping-pong form (tuning gemm_pp128 = 0 disables)
+        if (p.N > 64 && p.N <= 128 && p.K % 64 == 0 && p.K >= 128 && tuning().gemm_pp128 && pp_enabled() &&
             pp_offsets_fit(p, AMODE))
           return launch_gemm_pp<bf16, TO, AMODE, 128>(p, nz, s);
       }

@@ -757,9 +757,8 @@ extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L
   if (L <= 8) {
     // bf16: the vectorised form (16-byte aligned rows in qkv and out; 97 -> 67 us at 1024^2 B4).
     // fp32 keeps the per-lane form: its vectorised instance needs ~214 VGPRs and measured
-    // 54.8 vs 51.4 us at 512^2 B8. MHADA_VIT_ATTN_VEC=0 selects the per-lane form (A/B).
-    const char* e = getenv("MHADA_VIT_ATTN_VEC");
-    if (dtype != MHADA_F32 && !(e && e[0] == '0') && aligned16(qkv) && aligned16(out)) {
+    // 54.8 vs 51.4 us at 512^2 B8. tuning vit_attn_vec = 0 selects the per-lane form (A/B).
+    if (dtype != MHADA_F32 && tuning().vit_attn_vec && aligned16(qkv) && aligned16(out)) {
       const dim3 g32((unsigned)((pairs + 31) / 32));
       hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
                          ntok, heads);
@@ -865,9 +864,8 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
   const long long pix = (long long)B * H * W;
   const dim3 grid((unsigned)((pix + 255) / 256));
   hipStream_t s = (hipStream_t)s_;
-  // bf16, Cin 32/64: the MFMA tile kernel (MHADA_OUT3_MFMA=0 selects the per-pixel VALU kernel)
-  const char* e = getenv("MHADA_OUT3_MFMA");
-  if (dtype == MHADA_BF16 && !(e && e[0] == '0') && (Cin == 32 || Cin == 64)) {
+  // bf16, Cin 32/64: the MFMA tile kernel (tuning out3_mfma = 0 selects the per-pixel VALU kernel)
+  if (dtype == MHADA_BF16 && tuning().out3_mfma && (Cin == 32 || Cin == 64)) {
     const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3Rows - 1) / (4 * kOut3Rows);
     const long long nb = (long long)B * strips_y * tiles_x;
     if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");
@@ -878,9 +876,8 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
       hipLaunchKernelGGL((conv_out3_mfma_kernel<32, 32>), g, dim3(256), 0, s, (const bf16*)x, w, b, y, H, W, tiles_x, strips_y, clamp255);
     return check_launch("mhada_conv3x3_out3");
   }
-  // fp32, Cin 32/64: the LDS-tiled kernel (MHADA_OUT3_TILE=0 selects the per-pixel kernel)
-  const char* et = getenv("MHADA_OUT3_TILE");
-  if (dtype == MHADA_F32 && !(et && et[0] == '0') && (Cin == 32 || Cin == 64)) {
+  // fp32, Cin 32/64: the LDS-tiled kernel (tuning out3_tile = 0 selects the per-pixel kernel)
+  if (dtype == MHADA_F32 && tuning().out3_tile && (Cin == 32 || Cin == 64)) {
     const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3Rows - 1) / (4 * kOut3Rows);
     const long long nb = (long long)B * strips_y * tiles_x;
     if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");

@@ -42,6 +42,8 @@ _I, _F = ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "mhada_abi_version": (_I, []),
     "mhada_last_error": (ctypes.c_char_p, []),
+    "mhada_set_tuning": (_I, [ctypes.c_char_p, _I]),
+    "mhada_get_tuning": (_I, [ctypes.c_char_p, ctypes.POINTER(_I)]),
     "mhada_gemm": (_I, [ctypes.POINTER(GemmArgs), _vp]),
     "mhada_layernorm": (_I, [_vp, _vp, _I, _vp, _vp, _I, _I, _F, _vp]),
     "mhada_vit_batch_attn": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
@@ -85,6 +87,39 @@ def load(path: str | None = None) -> ctypes.CDLL:
         if path is None:
             _lib = lib
         return lib
+
+
+ABI_VERSION = 3
+
+
+def get_tuning(name: str) -> int:
+    v = ctypes.c_int()
+    check(load().mhada_get_tuning(name.encode(), ctypes.byref(v)), "mhada_get_tuning")
+    return v.value
+
+
+def set_tuning(name: str, value: int) -> None:
+    """Select a kernel variant (include/mhada_hip.h: A/B measurements and rare-path tests)."""
+    check(load().mhada_set_tuning(name.encode(), int(value)), "mhada_set_tuning")
+
+
+class tuning:
+    """Context manager: ``with tuning(attn_fixed_shift=0): ...`` restores the previous values."""
+
+    def __init__(self, **knobs: int):
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.saved[k] = get_tuning(k)
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_tuning(k, v)
+        return False
 
 
 def check(rc: int, what: str) -> None:

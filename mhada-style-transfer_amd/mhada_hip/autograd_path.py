@@ -11,13 +11,15 @@ whose state_dict keys match the reference), so autograd reaches exactly those pa
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Sequence
 
 import torch
 import torch.nn.functional as F
 
 from . import ops
+
+# "hip": the MHAda attention core trains on the HIP kernels; "torch": plain autograd (A/B, tests)
+TRAIN_ATTN = "hip"
 
 # decoder layers and whether bilinear x2 follows them (conv.py:78-94)
 DECODER_ORDER = (("conv1", 0, True), ("conv1", 1, False), ("conv1", 2, False), ("conv1", 3, False),
@@ -71,12 +73,15 @@ class MHAdaAttnFn(torch.autograd.Function):
     A is never stored: the backward recomputes it from the saved row normaliser."""
 
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, q, k, v, x):
+        q, k, v, x = (t.contiguous() for t in (q, k, v, x))
         out, mo, lse = ops.attn_train_fwd(q, k, v, x)
         ctx.save_for_backward(q, k, v, x, mo, lse)
         return out
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dout):
         q, k, v, x, mo, lse = ctx.saved_tensors
         dout = dout.contiguous()
@@ -93,8 +98,10 @@ class MHAdaAttnFn(torch.autograd.Function):
 
 
 def _fused_train_attn(blk, fc) -> bool:
-    return (fc.is_cuda and fc.dtype == torch.float32 and blk.activation_name == "softmax"
-            and blk.head_dim == 64 and os.environ.get("MHADA_TRAIN_ATTN", "hip") != "torch")
+    """The HIP training kernels compute in fp32; under autocast MHAdaAttnFn casts its operands to
+    fp32 (custom_fwd), so a bf16/fp16 projection output still takes this path."""
+    return (fc.is_cuda and fc.is_floating_point() and blk.activation_name == "softmax"
+            and blk.head_dim == 64 and TRAIN_ATTN != "torch")
 
 
 def _head_proj(mods, t: torch.Tensor, H: int) -> torch.Tensor:

@@ -1,11 +1,14 @@
 """Tensor-level wrappers over the C-ABI (one function per entry point of include/mhada_hip.h).
 
-Every wrapper takes ROCm device tensors, validates shapes/dtypes on the host, launches on
-``torch.cuda.current_stream()`` and allocates outputs through the torch caching allocator
-(the library itself never allocates).  No wrapper has a CPU or aten fallback.
+Every wrapper takes ROCm device tensors, validates shapes/dtypes on the host, launches on the
+current stream of the operands' device (with that device made current for the call, so modules
+moved with ``.to('cuda:1')`` work without ``set_device``) and allocates outputs through the
+torch caching allocator (the library itself never allocates).  No wrapper has a CPU or aten
+fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Optional
 
@@ -24,18 +27,32 @@ def dt_code(dtype: torch.dtype) -> int:
         raise ValueError(f"unsupported dtype {dtype}; the HIP path computes in float32 or bfloat16")
 
 
-def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
-
-
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
 def _need_gpu(*ts: Optional[torch.Tensor]) -> None:
+    dev = None
     for t in ts:
-        if t is not None and not t.is_cuda:
+        if t is None:
+            continue
+        if not t.is_cuda:
             raise RuntimeError("mhada_hip ops need ROCm device tensors (the MI355X path has no CPU fallback)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"mhada_hip ops need all operands on one device, got {dev} and {t.device}")
+
+
+def _call(name: str, dev_tensor: torch.Tensor, *args) -> None:
+    """Launch entry point ``name`` with ``dev_tensor``'s device current, on that device's current
+    stream (appended as the last argument); raise on a non-zero status."""
+    idx = dev_tensor.device.index
+    guard = contextlib.nullcontext() if idx is None or idx == torch.cuda.current_device() \
+        else torch.cuda.device(idx)
+    with guard:
+        rc = getattr(_lib.load(), name)(*args, torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc, name)
 
 
 def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K: int,
@@ -74,7 +91,7 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     args.c, args.c_dtype, args.ldc = c.data_ptr(), dt_code(c.dtype), ldc
     args.sc1, args.sc2 = sc
     args.relu = int(relu)
-    _lib.check(_lib.load().mhada_gemm(ctypes.byref(args), _stream()), "mhada_gemm")
+    _call("mhada_gemm", c, ctypes.byref(args))
     return c
 
 
@@ -120,8 +137,7 @@ def upsample2x(x: torch.Tensor) -> torch.Tensor:
     _need_gpu(x)
     B, H, W, C = x.shape
     y = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=x.dtype)
-    rc = _lib.load().mhada_upsample2x(x.data_ptr(), y.data_ptr(), dt_code(x.dtype), B, H, W, C, _stream())
-    _lib.check(rc, "mhada_upsample2x")
+    _call("mhada_upsample2x", x, x.data_ptr(), y.data_ptr(), dt_code(x.dtype), B, H, W, C)
     return y
 
 
@@ -129,9 +145,8 @@ def conv3x3_out3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, clamp255:
     B, H, W, Ci = x.shape
     _need_gpu(x, w, bias)
     y = torch.empty(B, 3, H, W, device=x.device, dtype=torch.float32)
-    rc = _lib.load().mhada_conv3x3_out3(x.data_ptr(), dt_code(x.dtype), w.data_ptr(), bias.data_ptr(),
-                                        y.data_ptr(), B, H, W, Ci, int(clamp255), _stream())
-    _lib.check(rc, "mhada_conv3x3_out3")
+    _call("mhada_conv3x3_out3", x, x.data_ptr(), dt_code(x.dtype), w.data_ptr(), bias.data_ptr(),
+                                        y.data_ptr(), B, H, W, Ci, int(clamp255))
     return y
 
 
@@ -139,9 +154,8 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, out_dtype: torc
     _need_gpu(x, g, b)
     rows, cols = x.shape
     y = torch.empty(rows, cols, device=x.device, dtype=out_dtype)
-    rc = _lib.load().mhada_layernorm(x.data_ptr(), y.data_ptr(), dt_code(out_dtype), g.data_ptr(), b.data_ptr(),
-                                     rows, cols, eps, _stream())
-    _lib.check(rc, "mhada_layernorm")
+    _call("mhada_layernorm", x, x.data_ptr(), y.data_ptr(), dt_code(out_dtype), g.data_ptr(), b.data_ptr(),
+                                     rows, cols, eps)
     return y
 
 
@@ -149,9 +163,8 @@ def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int) -> torch.Te
     _need_gpu(qkv)
     C = qkv.shape[-1] // 3
     out = torch.empty(L, ntok, C, device=qkv.device, dtype=qkv.dtype)
-    rc = _lib.load().mhada_vit_batch_attn(qkv.data_ptr(), out.data_ptr(), dt_code(qkv.dtype), L, ntok, heads,
-                                          C // heads, _stream())
-    _lib.check(rc, "mhada_vit_batch_attn")
+    _call("mhada_vit_batch_attn", qkv, qkv.data_ptr(), out.data_ptr(), dt_code(qkv.dtype), L, ntok, heads,
+                                          C // heads)
     return out
 
 
@@ -159,8 +172,7 @@ def pos_embed(pos: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
     _need_gpu(pos)
     _, C, bh, bw = pos.shape
     out = torch.empty(oh * ow, C, device=pos.device, dtype=torch.float32)
-    rc = _lib.load().mhada_pos_embed(pos.data_ptr(), out.data_ptr(), C, bh, bw, oh, ow, _stream())
-    _lib.check(rc, "mhada_pos_embed")
+    _call("mhada_pos_embed", pos, pos.data_ptr(), out.data_ptr(), C, bh, bw, oh, ow)
     return out
 
 
@@ -172,9 +184,8 @@ def instnorm_stats(x: torch.Tensor, eps: float = 1e-5):
     mu = torch.empty(B, C, device=x.device, dtype=torch.float32)
     rstd = torch.empty(B, C, device=x.device, dtype=torch.float32)
     work = torch.empty(splits, B, C, 2, device=x.device, dtype=torch.float64)
-    rc = _lib.load().mhada_instnorm_stats(x.data_ptr(), mu.data_ptr(), rstd.data_ptr(), work.data_ptr(), B, N, C,
-                                          splits, eps, _stream())
-    _lib.check(rc, "mhada_instnorm_stats")
+    _call("mhada_instnorm_stats", x, x.data_ptr(), mu.data_ptr(), rstd.data_ptr(), work.data_ptr(), B, N, C,
+                                          splits, eps)
     return mu, rstd
 
 
@@ -191,41 +202,40 @@ def fold_block(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s, dtype: torch.dtype, ksc
     wkv = torch.empty(B, H, 128, 64, device=dev, dtype=dtype)
     bkv = torch.empty(H, 128, device=dev, dtype=torch.float32)
     v_mu = torch.empty(B, C, device=dev, dtype=torch.float32)
-    rc = _lib.load().mhada_fold_block(wf.data_ptr(), wg.data_ptr(), wh.data_ptr(), bg.data_ptr(), bh.data_ptr(),
-                                      rstd_c.data_ptr(), mu_s.data_ptr(), rstd_s.data_ptr(), wq.data_ptr(),
-                                      wkv.data_ptr(), bkv.data_ptr(), v_mu.data_ptr(), kscale, dt_code(dtype), B, H,
-                                      _stream())
-    _lib.check(rc, "mhada_fold_block")
+    _need_gpu(wf, wg, wh, bg, bh, rstd_c, mu_s, rstd_s)
+    _call("mhada_fold_block", wf, wf.data_ptr(), wg.data_ptr(), wh.data_ptr(), bg.data_ptr(), bh.data_ptr(),
+          rstd_c.data_ptr(), mu_s.data_ptr(), rstd_s.data_ptr(), wq.data_ptr(), wkv.data_ptr(), bkv.data_ptr(),
+          v_mu.data_ptr(), kscale, dt_code(dtype), B, H)
     return wq, wkv, bkv, v_mu
 
 
 def transpose_v(kv: torch.Tensor) -> torch.Tensor:
+    _need_gpu(kv)
     B, H, Ns, _ = kv.shape
     ldt = (Ns + 63) // 64 * 64
     vt = torch.empty(B, H, 128, ldt, device=kv.device, dtype=kv.dtype)
-    rc = _lib.load().mhada_transpose_v(kv.data_ptr(), vt.data_ptr(), dt_code(kv.dtype), B, H, Ns, _stream())
-    _lib.check(rc, "mhada_transpose_v")
+    _call("mhada_transpose_v", kv, kv.data_ptr(), vt.data_ptr(), dt_code(kv.dtype), B, H, Ns)
     return vt
 
 
 def cosine_prep(q: Optional[torch.Tensor], kv: Optional[torch.Tensor]) -> None:
     """L2-normalise Q rows and/or the K half of KV rows in place (either may be None)."""
+    _need_gpu(q, kv)
     ref = q if q is not None else kv
     B, H = ref.shape[0], ref.shape[1]
     Nc = q.shape[2] if q is not None else 0
     Ns = kv.shape[2] if kv is not None else 0
-    rc = _lib.load().mhada_cosine_prep(_ptr(q), _ptr(kv), dt_code(ref.dtype), B, H, Nc, Ns, _stream())
-    _lib.check(rc, "mhada_cosine_prep")
+    _call("mhada_cosine_prep", ref, _ptr(q), _ptr(kv), dt_code(ref.dtype), B, H, Nc, Ns)
 
 
 def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch.Tensor:
+    _need_gpu(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu)
     B, H, Nc, _ = q.shape
     Ns = kv.shape[2]
     out = torch.empty(B, Nc, H * 64, device=q.device, dtype=q.dtype)
-    rc = _lib.load().mhada_attn(q.data_ptr(), kv.data_ptr(), _ptr(vt), fcs.data_ptr(), fcs_mu.data_ptr(),
+    _call("mhada_attn", q, q.data_ptr(), kv.data_ptr(), _ptr(vt), fcs.data_ptr(), fcs_mu.data_ptr(),
                                 fcs_rstd.data_ptr(), v_mu.data_ptr(), out.data_ptr(), dt_code(q.dtype), B, H, Nc,
-                                Ns, activation, _stream())
-    _lib.check(rc, "mhada_attn")
+                                Ns, activation)
     return out
 
 
@@ -248,9 +258,8 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     out = torch.empty_like(q)
     mo = torch.empty(BH, Nc, 128, device=q.device, dtype=torch.float32)
     lse = torch.empty(BH, Nc, device=q.device, dtype=torch.float32)
-    rc = _lib.load().mhada_attn_train_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), x.data_ptr(), out.data_ptr(),
-                                          mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns, _stream())
-    _lib.check(rc, "mhada_attn_train_fwd")
+    _call("mhada_attn_train_fwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), x.data_ptr(), out.data_ptr(),
+                                          mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns)
     return out, mo, lse
 
 
@@ -265,10 +274,8 @@ def attn_train_bwd(q, k, v, lse, dmo, dd):
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)
-    rc = _lib.load().mhada_attn_train_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
-                                          dd.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), BH, Nc, Ns,
-                                          _stream())
-    _lib.check(rc, "mhada_attn_train_bwd")
+    _call("mhada_attn_train_bwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
+          dd.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), BH, Nc, Ns)
     return dq, dk, dv
 
 
@@ -297,9 +304,8 @@ def warp(x: torch.Tensor, flow: torch.Tensor, padding_mode: str = "zeros") -> to
     if tuple(flow.shape) != (B, 2, H, W):
         raise ValueError(f"flow must be [B,2,H,W] = {[B, 2, H, W]}, got {list(flow.shape)}")
     y = torch.empty_like(x)
-    rc = _lib.load().mhada_warp(x.data_ptr(), flow.data_ptr(), y.data_ptr(), B, C, H, W,
-                                _padding_code(padding_mode), _stream())
-    _lib.check(rc, "mhada_warp")
+    _call("mhada_warp", x, x.data_ptr(), flow.data_ptr(), y.data_ptr(), B, C, H, W,
+                                _padding_code(padding_mode))
     return y
 
 
@@ -312,9 +318,8 @@ def flow_warp_mask(flo01: torch.Tensor, flo10: torch.Tensor, padding_mode: str =
         raise ValueError("flows must both be [2,H,W]")
     H, W = flo01.shape[1:]
     mask = torch.empty(H, W, device=flo01.device, dtype=torch.float32)
-    rc = _lib.load().mhada_flow_warp_mask(flo01.data_ptr(), flo10.data_ptr(), mask.data_ptr(), H, W,
-                                          float(threshold), _padding_code(padding_mode), _stream())
-    _lib.check(rc, "mhada_flow_warp_mask")
+    _call("mhada_flow_warp_mask", flo01, flo01.data_ptr(), flo10.data_ptr(), mask.data_ptr(), H, W,
+                                          float(threshold), _padding_code(padding_mode))
     return mask
 
 
@@ -327,7 +332,6 @@ def warp_l1(cs1: torch.Tensor, cs2: torch.Tensor, flow: torch.Tensor, mask: torc
         raise ValueError("warp_l1: cs1/cs2 [B,C,H,W], flow [B,2,H,W], mask [B,H,W]")
     work = torch.empty(B * ((H * W + 255) // 256), device=cs1.device, dtype=torch.float64)
     out = torch.empty(B, device=cs1.device, dtype=torch.float32)
-    rc = _lib.load().mhada_warp_l1(cs1.data_ptr(), cs2.data_ptr(), flow.data_ptr(), mask.data_ptr(),
-                                   work.data_ptr(), out.data_ptr(), B, C, H, W, _stream())
-    _lib.check(rc, "mhada_warp_l1")
+    _call("mhada_warp_l1", cs1, cs1.data_ptr(), cs2.data_ptr(), flow.data_ptr(), mask.data_ptr(),
+                                   work.data_ptr(), out.data_ptr(), B, C, H, W)
     return out

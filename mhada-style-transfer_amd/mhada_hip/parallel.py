@@ -69,7 +69,9 @@ class GradAllReducer:
 
     def finish(self) -> None:
         """Wait for every bucket (launching those whose parameters got no gradient this step),
-        average, and write the reduced values back into .grad."""
+        average, and write the reduced values back into .grad.  A parameter that got no gradient
+        (grad None: unused by this step's graph, the same on every rank) contributes zeros to its
+        bucket and KEEPS grad None, so Adam skips it exactly as in the single-GPU reference."""
         for bi in range(len(self.buckets)):
             if self._handles[bi] is None:
                 self._launch(bi)
@@ -80,14 +82,14 @@ class GradAllReducer:
             off = 0
             for p in ps:
                 n = p.numel()
-                g = flat[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
+                if p.grad is not None:
+                    p.grad.copy_(flat[off:off + n].view_as(p))
                 off += n
         self.reset()
 
     def remove(self) -> None:
+        """Detach the gradient hooks (Trainer.close): a later reducer on the same parameters must
+        not share them, or extra all-reduces would mismatch the collectives across ranks."""
         for h in self._hooks:
             h.remove()
+        self._hooks = []

@@ -47,6 +47,19 @@ class Trainer:
             params = list(vit_c.parameters()) + list(vit_s.parameters()) + list(ada.parameters())
             self.reducer = GradAllReducer(params, bucket_bytes=bucket_mb << 20)
 
+    def close(self) -> None:
+        """Remove the all-reduce hooks from the parameters (a new Trainer on the same modules
+        installs its own)."""
+        if self.reducer is not None:
+            self.reducer.remove()
+            self.reducer = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
     def losses(self, content: torch.Tensor, style: torch.Tensor) -> Dict[str, torch.Tensor]:
         """Forward + weighted losses (train_image.py:103-136)."""
         fc_vc = self.vit_c(content)

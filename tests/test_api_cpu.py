@@ -88,7 +88,26 @@ def test_library_loads_and_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
-    assert lib.mhada_abi_version() == 2
+    assert lib.mhada_abi_version() == 3
+
+
+def test_tuning_table_read_once_and_settable():
+    """Kernel-variant knobs: read once at library init, changed only through mhada_set_tuning."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmhada_hip.so not built")
+    assert _lib.get_tuning("attn_fixed_shift") == 1
+    with _lib.tuning(attn_fixed_shift=0, attn_tk=64):
+        assert _lib.get_tuning("attn_fixed_shift") == 0 and _lib.get_tuning("attn_tk") == 64
+        os.environ["MHADA_ATTN_FIXED_SHIFT"] = "1"  # the environment is not re-read per call
+        try:
+            assert _lib.get_tuning("attn_fixed_shift") == 0
+        finally:
+            del os.environ["MHADA_ATTN_FIXED_SHIFT"]
+    assert _lib.get_tuning("attn_fixed_shift") == 1 and _lib.get_tuning("attn_tk") == 128
+    with pytest.raises(ValueError):
+        _lib.set_tuning("no_such_knob", 1)
+    with pytest.raises(ValueError):
+        _lib.set_tuning("attn_tk", 96)
 
 
 def test_abi_argument_errors_without_gpu():

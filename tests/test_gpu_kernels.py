@@ -29,7 +29,7 @@ TOL = {torch.float32: 2e-5, torch.bfloat16: 1e-2}
 
 def test_library_is_the_native_one():
     lib = _lib.load()
-    assert lib.mhada_abi_version() == 2
+    assert lib.mhada_abi_version() == 3
     assert _lib.LIB_PATH.endswith("libmhada_hip.so")
 
 
@@ -122,15 +122,14 @@ def test_upsample2x(dt, H, W, C):
 @pytest.mark.parametrize("clamp", [False, True])
 @pytest.mark.parametrize("B,H,W,Ci", [(2, 20, 33, 64), (1, 64, 128, 64), (1, 7, 70, 32), (1, 9, 65, 128),
                                       (3, 37, 2, 64)])
-def test_conv_out3(dt, mfma, clamp, B, H, W, Ci, monkeypatch):
+def test_conv_out3(dt, mfma, clamp, B, H, W, Ci):
     """Last decoder layer; bf16 runs the MFMA tile kernel (bf16 weights), fp32 the LDS-tiled
     VALU kernel, or, with mfma == "0", the per-pixel VALU kernel (fp32 weights)."""
-    monkeypatch.setenv("MHADA_OUT3_MFMA", mfma)
-    monkeypatch.setenv("MHADA_OUT3_TILE", mfma)
     x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(9)).to(DEV).to(dt)
     w = rnd(3, Ci, 3, 3, scale=0.5, seed=2)
     b = rnd(3, seed=3) * 30
-    y = ops.conv3x3_out3(x, w.permute(2, 3, 1, 0).contiguous(), b, clamp255=clamp)
+    with _lib.tuning(out3_mfma=int(mfma), out3_tile=int(mfma)):
+        y = ops.conv3x3_out3(x, w.permute(2, 3, 1, 0).contiguous(), b, clamp255=clamp)
     ref = torch.relu(F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
                               w.double(), b.double()))
     if clamp:
@@ -150,15 +149,15 @@ def test_layernorm(dt):
 
 @pytest.mark.parametrize("dt,vec", [(torch.float32, "1"), (torch.bfloat16, "1"), (torch.bfloat16, "0")])
 @pytest.mark.parametrize("L", [1, 2, 3, 8, 11])
-def test_vit_batch_attention_matches_nn_mha(dt, vec, L, monkeypatch):
-    monkeypatch.setenv("MHADA_VIT_ATTN_VEC", vec)  # bf16 L <= 8: vectorised form unless "0"
+def test_vit_batch_attention_matches_nn_mha(dt, vec, L):
     N, C, heads = 300, 512, 8
     mha = torch.nn.MultiheadAttention(C, heads).to(DEV).double()
     x = rnd(L, N, C, seed=L).double()
     with torch.no_grad():
         ref, _ = mha(x, x, x, need_weights=False)  # batch_first=False on (B, N, C): attends over B
         qkv = F.linear(x, mha.in_proj_weight, mha.in_proj_bias).to(dt)
-        att = ops.vit_batch_attn(qkv.contiguous(), L, N, heads)
+        with _lib.tuning(vit_attn_vec=int(vec)):  # bf16 L <= 8: vectorised form unless 0
+            att = ops.vit_batch_attn(qkv.contiguous(), L, N, heads)
         y = F.linear(att.double(), mha.out_proj.weight, mha.out_proj.bias)
     assert rel(y, ref) < (1e-6 if dt == torch.float32 else 1e-2)
 
@@ -264,11 +263,10 @@ def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
 
 @pytest.mark.parametrize("kernel", ["fs", "w8"])
 @pytest.mark.parametrize("Nc,Ns", [(300, 700), (256, 128), (97, 33)])
-def test_mhada_attn_late_max_jump(kernel, Nc, Ns, monkeypatch):
+def test_mhada_attn_late_max_jump(kernel, Nc, Ns):
     """A key far beyond the first tile's scores (> 2^64 in P against the first tile's max): the
     fixed-shift kernel ("fs", attn.hip) must take its exact-recompute path, the online-max
     kernel ("w8") its rescale branch; both against fp64 torch on the same bf16 operands."""
-    monkeypatch.setenv("MHADA_ATTN_KERNEL", kernel)
     B, H = 1, 8
     q = rnd(B, H, Nc, 64, seed=11)
     q = q / q.norm(dim=-1, keepdim=True) * 4.0
@@ -281,7 +279,8 @@ def test_mhada_attn_late_max_jump(kernel, Nc, Ns, monkeypatch):
     fcs = rnd(B, Nc, 512, seed=13)
     mu, rs = ops.instnorm_stats(fcs)
     vmu = rnd(B, 512, seed=14)
-    y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+    with _lib.tuning(attn_fixed_shift=int(kernel == "fs")):
+        y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
     ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
     assert torch.isfinite(y.float()).all()
     assert rel(y.float(), ref) < 1.5e-2

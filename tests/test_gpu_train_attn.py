@@ -80,7 +80,7 @@ def test_fused_block_grads_match_autograd_block():
     dout = torch.randn(2, 512, 12, 10, device="cuda")
     results = []
     for mode in ("hip", "torch"):
-        os.environ["MHADA_TRAIN_ATTN"] = mode
+        autograd_path.TRAIN_ATTN = mode
         try:
             for t in (fc, fs, fcs, *blk.parameters()):
                 t.grad = None
@@ -88,7 +88,7 @@ def test_fused_block_grads_match_autograd_block():
             y.backward(dout)
             results.append([y.detach().clone()] + [t.grad.clone() for t in (fc, fs, fcs, *blk.parameters())])
         finally:
-            os.environ.pop("MHADA_TRAIN_ATTN", None)
+            autograd_path.TRAIN_ATTN = "hip"
     # K-bias gradients are zero in exact arithmetic (a per-query constant logit shift): those
     # are held to an absolute floor of 1e-5 of the largest gradient
     gmax = max(b.abs().max().item() for b in results[1])

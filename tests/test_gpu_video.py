@@ -170,3 +170,74 @@ def test_video_stylizer_loop():
     # align_corners=False, so it reads x*W/(W-1) - 1/2 (reproduced, not corrected)
     ref = torch.abs(f2 / 255 - L.warp(f1 / 255, flow)).mean()
     assert abs(float(e[0]) - float(ref)) < 1e-5 * float(ref) + 1e-7
+
+
+# ---- BASELINE configs[4] at full size: one 1080x1920 frame against a cached 256^2 style ----------
+def _smooth_frame(seed, H=1080, W=1920):
+    """Synthetic video frame: seeded low-frequency noise (what bench.py's video config streams)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lo = torch.rand(1, 3, H // 8 + 2, W // 8 + 2, generator=g) * 255
+    return torch.nn.functional.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False).contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_video_1080p_frame_matches_torch_fp32(dtype):
+    """infer_video.py:58-61,91-92 at 1080p (Nc = 135*240 = 32400 content tokens, ragged against
+    the 256-query attention tile; Ns = 1024 style tokens): the VideoStylizer path (style encoded
+    once, K/V cached by the AdaFormer) against the plain-PyTorch fp32 restatement on the device
+    (SURVEY §8c contract: MSE on clamp/255 < 1e-4; raw 0-255 MSE < 1e-4 for fp32), and the cached
+    call bit-identical to a cache-off call."""
+    import numpy as np
+    import torch_ref
+    vc, vs, ada = models("softmax", dtype)
+    style = seeded_image(1, 256, 256, 12).to(DEV)
+    frame = _smooth_frame(500).to(DEV)
+    st = video.VideoStylizer(vc, vs, ada)
+    st.set_style(style)
+    with torch.no_grad():
+        out1 = st(frame)                       # fills the per-style cache
+        fc = vc(frame)
+        _, cs = ada(fc, st.fs)                 # cache hit
+        _, cs_fresh = fresh(ada, fc, st.fs)    # everything recomputed
+    assert "_mhada_style" in ada.__dict__
+    assert torch.equal(cs, cs_fresh)
+    assert torch.equal(out1, cs.clamp(0, 255))
+    sds = [{k: v.float() for k, v in m.state_dict().items()} for m in (vc, vs, ada)]
+    with torch.no_grad():
+        _, _, _, ref = torch_ref.stylize(frame, style, *sds)
+    a, b = cs.double().cpu().numpy(), ref.double().cpu().numpy()
+    assert a.shape == (1, 3, 1080, 1920)
+    mse01 = float(((np.clip(a, 0, 255) / 255 - np.clip(b, 0, 255) / 255) ** 2).mean())
+    assert mse01 < 1e-4, mse01
+    if dtype == torch.float32:
+        assert float(((a - b) ** 2).mean()) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mhada_attn_1080p_shape_rows_against_fp64(dt):
+    """mhada_attn at the video shape (B 1, 8 heads, Nc 32400, Ns 1024) against fp64 on a strided
+    subset of query rows (every 37th, plus the last, ragged tile's rows)."""
+    import math
+    from mhada_hip import ops
+    B, H, Nc, Ns = 1, 8, 32400, 1024
+    g = torch.Generator(device="cpu").manual_seed(77)
+    q = (torch.randn(B, H, Nc, 64, generator=g) * 0.25).to(DEV, dt)
+    kv = (torch.randn(B, H, Ns, 128, generator=g) * 0.5).to(DEV, dt)
+    fcs = torch.randn(B, Nc, 512, generator=g).to(DEV)
+    vmu = torch.randn(B, 512, generator=g).to(DEV)
+    with torch.no_grad():
+        mu, rs = ops.instnorm_stats(fcs)
+        vt = ops.transpose_v(kv)
+        y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0).float()
+    rows = torch.cat([torch.arange(0, Nc, 37), torch.arange(Nc - 144, Nc)]).unique().to(DEV)
+    qd, kd, vd = q[:, :, rows].double(), kv[..., :64].double(), kv[..., 64:].double()
+    a = torch.softmax(qd @ kd.transpose(-1, -2) * math.log(2.0), dim=-1)  # K carries log2(e)
+    m = a @ vd
+    s = torch.sqrt(torch.clamp(a @ (vd * vd) - m * m, min=1e-6))
+    f = (fcs[:, rows].double() - mu.double()[:, None]) * rs.double()[:, None]
+    ref = s.permute(0, 2, 1, 3).reshape(B, -1, 512) * f + m.permute(0, 2, 1, 3).reshape(B, -1, 512) \
+        + vmu.double()[:, None]
+    got = y[:, rows].double()
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert torch.isfinite(y).all()
+    assert err < (1e-5 if dt == torch.float32 else 1.5e-2), err

@@ -99,3 +99,44 @@ def test_data_parallel_allreduce_equals_accumulation(tmp_path):
     torch.set_num_threads(8)
     for n, g in acc.items():
         torch.testing.assert_close(dp[n], g, rtol=1e-4, atol=1e-5 * float(g.abs().max()))
+
+
+def _reducer_worker(rank, world, port, out_dir):
+    from mhada_hip.parallel import GradAllReducer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    used, unused = torch.nn.Linear(4, 3), torch.nn.Linear(4, 3)
+    params = list(used.parameters()) + list(unused.parameters())
+    red = GradAllReducer(params, bucket_bytes=16)  # one small bucket per parameter or two
+    x = torch.full((2, 4), float(rank + 1))
+    used(x).sum().backward()
+    red.finish()
+    res = {"w": used.weight.grad.clone(), "unused_none": unused.weight.grad is None}
+    red.remove()
+    # a second reducer on the same parameters: the first one's hooks must not fire any more
+    red2 = GradAllReducer(params, bucket_bytes=1 << 20)
+    for p in params:
+        p.grad = None
+    used(x).sum().backward()
+    red2.finish()
+    res["w2"] = used.weight.grad.clone()
+    res["n_hooks_first"] = len(red._hooks)
+    red2.remove()
+    torch.save(res, os.path.join(out_dir, f"red_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reducer_keeps_unused_grads_none_and_removes_hooks(tmp_path):
+    """a parameter no loss reaches keeps grad None (Adam skips it, as in the single-GPU
+    reference), and remove() detaches the hooks so a second reducer runs exactly one all-reduce
+    per bucket (a stale hook would desynchronise the collectives across ranks)."""
+    world = 2
+    mp.spawn(_reducer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        res = torch.load(tmp_path / f"red_{r}.pt", weights_only=True)
+        # d sum(W x) / dW = 2 rows of x (value rank+1) -> mean over ranks of 2*(r+1) = 3
+        torch.testing.assert_close(res["w"], torch.full((3, 4), 3.0))
+        torch.testing.assert_close(res["w2"], torch.full((3, 4), 3.0))
+        assert res["unused_none"] and res["n_hooks_first"] == 0

@@ -1,4 +1,4 @@
-"""A/B of the bf16 MHAda attention kernel variants (MHADA_ATTN_* switches, attn.hip) in one process:
+"""A/B of the bf16 MHAda attention kernel variants (attn_* tuning knobs, attn.hip) in one process:
 agreement on the same operands and interleaved timing (median of rounds) at the bench shapes.
 
     python tools/attn_ab.py
@@ -17,14 +17,15 @@ SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1
           ("ragged", 2, 1000, 777)]
 
 
-VARIANTS = {"fs": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "128"},
-            "fs64": {"MHADA_ATTN_KERNEL": "fs", "MHADA_ATTN_TK": "64"},
-            "w8": {"MHADA_ATTN_KERNEL": "w8", "MHADA_ATTN_TK": "128"}}
+VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128},
+            "fs64": {"attn_fixed_shift": 1, "attn_tk": 64},
+            "w8": {"attn_fixed_shift": 0, "attn_tk": 128}}
 
 
 def run(variant, args):
-    os.environ.update(VARIANTS[variant])
-    return ops.mhada_attn(*args, 0)
+    from mhada_hip import _lib
+    with _lib.tuning(**VARIANTS[variant]):
+        return ops.mhada_attn(*args, 0)
 
 
 def main():
@@ -54,8 +55,6 @@ def main():
         fl = 6.0 * nc * ns * 512 * B
         print(f"{name:18s} " + "   ".join(f"{v} {med[v]:.3f} ms {fl / med[v] / 1e9:.0f} TF (err {errs[v]:.1e})"
                                            for v in VARIANTS), flush=True)
-    for k in ("MHADA_ATTN_KERNEL", "MHADA_ATTN_PRIO", "MHADA_ATTN_TK"):
-        os.environ.pop(k, None)
     # fp32 (one kernel; compare with the launch averages in profiles/r01_attn_launch_stats.txt)
     for name, B, nc, ns in SHAPES[1:]:
         q = torch.randn(B, H, nc, 64, device="cuda") * 0.35

@@ -35,15 +35,10 @@ def bench(fns, rounds=7, iters=10):
 
 
 def with_env(key, val, fn, *a, **k):
-    old = os.environ.get(key)
-    os.environ[key] = val
-    try:
+    """Run fn with one kernel-variant knob changed (MHADA_<KNOB> naming, see include/mhada_hip.h)."""
+    from mhada_hip import _lib
+    with _lib.tuning(**{key[len("MHADA_"):].lower(): int(val)}):
         return fn(*a, **k)
-    finally:
-        if old is None:
-            del os.environ[key]
-        else:
-            os.environ[key] = old
 
 
 def gemm_suite():

@@ -9,7 +9,11 @@ counters come from separate passes (they cannot share one).  Keyed by bench conf
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import attn_source_sha  # noqa: E402
 
 # grid size (threads) of mhada_attn per bench config: blocks = B*H*ceil(Nc/256), 512 threads each
 CONFIGS = {"512x512_b8_f32": 8 * 8 * (4096 // 256) * 512, "1024x1024_b4_bf16": 4 * 8 * (16384 // 256) * 512}
@@ -26,7 +30,7 @@ def load(fn, counter):
 def main():
     f = load(sys.argv[1], "FETCH_SIZE")
     w = load(sys.argv[2], "WRITE_SIZE")
-    out = {}
+    out = {"attn_src_sha": attn_source_sha()}
     for name, grid in CONFIGS.items():
         if grid not in f or grid not in w:
             continue

@@ -34,5 +34,5 @@ def timeit(fn):
 
 tf = timeit(lambda: ops.attn_train_fwd(q, k, v, x))
 tb = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd))
-print(f"occ={os.environ.get('MHADA_TRAIN_DKV_OCC', '1')} fwd {tf:.3f} ms ({384 * pairs / tf / 1e9:.1f} TF)  "
+print(f"fwd {tf:.3f} ms ({384 * pairs / tf / 1e9:.1f} TF)  "
       f"bwd {tb:.3f} ms ({1280 * pairs / tb / 1e9:.1f} TF)")
