@@ -3,8 +3,9 @@
 A "step" is one full style-transfer forward — vit_c(content), vit_s(style),
 adaFormer(fc, fs) (infer_image.py:83-85 / infer_time.py:74-77) — over one synthetic batch
 already resident in HBM.  Headline workload = BASELINE configs[1]: 512x512, batch 8, fp32.
-The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path) and configs[4] (1080p
-video frames against a cached 256^2 style + warping error, fp32 and bf16) under "configs".
+The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path), configs[3] (the
+train_image.py step at 512x512, 8 images per GPU) and configs[4] (1080p u8 video frames ingested,
+stylised against a cached 256^2 style + warping error, fp32 and bf16) under "configs".
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -160,7 +161,7 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
 
 
 def run_video(dtype, steps, warmup, rank, world):
-    """BASELINE configs[4]: infer_video.py per-frame stylisation at 1080x1920 with a 256^2
+    """BASELINE configs[4]: infer_video.py per-frame ingest + stylisation at 1080x1920 with a 256^2
     style encoded once (its K/V cached by the AdaFormer, engine.style_cache) plus the temporal
     warping-error metric of the new frame against the previous one (exps_sintel.py:101-109,
     HIP warp kernel).  Synthetic smooth video: seeded low-frequency noise translating by a known
@@ -176,14 +177,19 @@ def run_video(dtype, steps, warmup, rank, world):
     frames = [base[:, :, 1 * t: 1 * t + H, 3 * t: 3 * t + W].contiguous().to(dev) for t in range(n)]
     flow = torch.empty(1, 2, H, W, device=dev)
     flow[:, 0], flow[:, 1] = 3.0, 1.0  # frame t+1 at p equals frame t at p + (3, 1)
+    # the stream arrives as cv2 frames: u8 BGR HWC (device-resident, like every bench input);
+    # each step ingests one (utilities.cv2_to_tensor: BGR->RGB, toTensor255; HIP frame ingest),
+    # stylises it against the cached style and scores the warping error against the previous one
+    frames_u8 = [f[0].permute(1, 2, 0).flip(-1).round().clamp(0, 255).to(torch.uint8).contiguous() for f in frames]
+    del frames
     st = video.VideoStylizer(vc, vs, ada)
     with torch.no_grad():
         st.set_style(seeded_image(1, 256, 256, 12 + 1000 * rank).to(dev))
         mask = video.flow_warp_mask(flow[0], -flow[0])
-        st(frames[0])
+        st(video.cv2_to_tensor(frames_u8[0]).unsqueeze(0))
 
         def step(t):
-            st(frames[t])
+            st(video.cv2_to_tensor(frames_u8[t]).unsqueeze(0))
             return st.warping_error(flow, mask)
 
         for t in range(1, warmup + 1):
@@ -209,7 +215,8 @@ def run_video(dtype, steps, warmup, rank, world):
     dts = "f32" if dtype == torch.float32 else "bf16"
     return {"value": steps * world / elapsed, "unit": "frames/s", "ms_per_frame": elapsed / steps * 1e3,
             "dtype": dts, "tflops": fl * steps / elapsed / 1e12, "warping_error_last": float(err[0]),
-            "config": {"workload": "infer_video.py: 1080x1920 frames, 256x256 style cached, + warping error",
+            "config": {"workload": "infer_video.py: 1080x1920 u8 BGR frames -> ingest (cv2_to_tensor) -> stylise "
+                                   "against a cached 256x256 style, + warping error",
                        "batch_per_gpu": 1, "compute_dtype": dts, "parallelism": f"replicas x{world}"}}
 
 

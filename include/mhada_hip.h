@@ -33,10 +33,13 @@ enum {
   MHADA_A_ROWS = 0,        /* A[m*lda + k], row-major                                     */
   MHADA_A_PATCH8 = 1,      /* A = im2col of an NCHW fp32 image, 8x8 patches, stride 8     */
   MHADA_A_CONV3X3 = 2,     /* A = im2col of NHWC input, 3x3 taps, ReflectionPad2d(1)      */
-  MHADA_A_CONV3X3_UP2 = 3  /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
+  MHADA_A_CONV3X3_UP2 = 3, /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
+  MHADA_A_CONV3X3_ZERO = 4 /* 3x3 taps with ZERO padding `pad` (1: same size, as VGG19's
+                              nn.Conv2d(padding=1); 2: the full correlation, out = in + 2 —
+                              the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 3 (mhada_set_tuning / mhada_get_tuning) */
+int mhada_abi_version(void);  /* 4 (training: CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -75,13 +78,15 @@ typedef struct mhada_gemm_args {
   const float* a_mu; long long smu1, smu2;
   /* PATCH8: img_c/h/w of the NCHW image (a_dtype must be F32).
      CONV*: img_c = Cin, img_h/img_w = spatial size of the NHWC INPUT tensor; the output grid
-     is img_h x img_w (CONV3X3) or 2*img_h x 2*img_w (CONV3X3_UP2); M = batch*out_h*out_w. */
+     is img_h x img_w (CONV3X3), 2*img_h x 2*img_w (CONV3X3_UP2) or img + 2*(pad-1)
+     (CONV3X3_ZERO); M = batch*out_h*out_w. */
   int img_c, img_h, img_w;
   const void* w; long long ldw, sw1, sw2;
   const float* bias; long long sb1, sb2;
   const void* r; int r_dtype; long long ldr, sr1, sr2;
   void* c; int c_dtype; long long ldc, sc1, sc2;
   int relu;
+  int pad;      /* CONV3X3_ZERO only: 1 or 2 (0 = 1) */
 } mhada_gemm_args;
 
 int mhada_gemm(const mhada_gemm_args* args, mhada_stream_t stream);
@@ -193,6 +198,70 @@ int mhada_flow_warp_mask(const float* flo01, const float* flo10, float* mask, in
  * work: fp64 scratch of B * ceil(H*W/256) entries (fixed-order partial sums). */
 int mhada_warp_l1(const float* cs1, const float* cs2, const float* flow, const float* mask,
                   double* work, float* out, int B, int C, int H, int W, mhada_stream_t stream);
+
+/* ---- training path (train_image.py:139 loss.backward(), fp32, NHWC activations) ---------- */
+
+/* Weight-gradient contraction C[M][N] = sum_k A[k][m] * B[k][n] (C row stride ldc), fp32:
+ *   conv wgrad: A = dY' [pixels][Cout] (lda = Cout), B = im2col of the layer input in b_mode
+ *     MHADA_A_CONV3X3 (reflect pad 1) or MHADA_A_CONV3X3_ZERO (zero pad `pad`): k = output pixel,
+ *     n = tap*Cin + ci (N = 9*Cin; img_* = the NHWC input), C = dW [Cout][ky][kx][Cin];
+ *   linear dW = dY^T X: A = dY [rows][out], B = X [rows][in] (b_mode MHADA_A_ROWS, ldb).
+ * Replaces the weight-gradient half of conv2d / addmm backward (conv.py:27-32, vgg19 convs,
+ * vit.py:49-63 Linear layers).  K is split into partial slabs in `work` (>= M*N floats; up to
+ * mhada_gemm_tn_splits(M,N,K)*M*N are used) summed in a fixed order: deterministic.  N % 4 == 0. */
+typedef struct mhada_gemm_tn_args {
+  int M, N, K;
+  const float* a; long long lda;
+  const float* b; long long ldb;
+  int b_mode;
+  int img_c, img_h, img_w, pad;
+  float* c; long long ldc;
+} mhada_gemm_tn_args;
+int mhada_gemm_tn_splits(int M, int N, int K);
+int mhada_gemm_tn(const mhada_gemm_tn_args* args, float* work, long long work_floats, mhada_stream_t stream);
+
+/* Bias gradients: out[c] = sum_r x[r][c] (x [rows][C] fp32, C % 4 == 0); work >= C floats
+ * (up to 1024*C used), fixed-order reduction. */
+int mhada_colsum(const float* x, float* out, long long rows, int C, float* work, long long work_floats,
+                 mhada_stream_t stream);
+/* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */
+int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t stream);
+/* Adjoint of ReflectionPad2d(1) (conv.py:27,31): dxp [B][H+2][W+2][C] (the full-correlation
+ * input gradient on the padded grid) -> dx [B][H][W][C]. */
+int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t stream);
+/* MaxPool2d(2, 2) on NHWC (vgg19.py slices, torchvision cfg E) and its backward (the gradient
+ * goes to the first maximum of each window in row-major order, as ATen keeps it). */
+int mhada_maxpool2(const float* x, float* y, int B, int H, int W, int C, mhada_stream_t stream);
+int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+                       mhada_stream_t stream);
+/* Adjoint of the bilinear x2 upsample (conv.py:71): dy [B][2H][2W][C] -> dx [B][H][W][C]. */
+int mhada_upsample2x_bwd(const float* dy, float* dx, int B, int H, int W, int C, mhada_stream_t stream);
+/* imageNet1k_normalize (vgg19.py:6-12): img [B][3][H][W] fp32 0..255 -> NHWC [B][H][W][Cp]
+ * ((x/255 - mean)/std, channels 3..Cp-1 zero), and the adjoint of that map. */
+int mhada_vgg_input(const float* img, float* out, int B, int H, int W, int Cp, mhada_stream_t stream);
+int mhada_vgg_input_bwd(const float* dout, float* dimg, int B, int H, int W, int Cp, mhada_stream_t stream);
+
+/* AdaAttnForLoss (adaDecoder.py:52-81, the local-feature-loss target of lossfn.py:26-34), fp32,
+ * flash-style (A never stored): out = sqrt(max(A V^2 - (A V)^2, 1e-6)) * IN(c_x) + A V with
+ * A = softmax(Q K^T) or the cosine form.  q [B][Nq][Dqk] = IN(c_1x), k [B][Ns][Dqk] = IN(s_1x)
+ * (mhada_rows_normalize; for cosine with unit = 1, i.e. rows divided by their L2 norm), v
+ * [B][Ns][Dv] = s_x, x [B][Nq][Dv] = c_x with its IN statistics x_mu / x_rs [B][Dv].
+ * Dqk % 4 == 0; Dv in {64, 128, 256, 512}. */
+int mhada_loss_attn(const float* q, const float* k, const float* v, const float* x, const float* x_mu,
+                    const float* x_rs, float* out, int B, int Nq, int Ns, int Dqk, int Dv, int activation,
+                    mhada_stream_t stream);
+/* InstanceNorm of token rows: out = (x - mu[b]) * rs[b] on x [B][N][C] (C % 4 == 0); unit != 0
+ * also divides each normalised row by its L2 norm (CosineSimilarity, adaDecoder.py:30-32). */
+int mhada_rows_normalize(const float* x, const float* mu, const float* rs, float* out, int unit,
+                         int B, int N, int C, mhada_stream_t stream);
+
+/* Frame ingest (utilities.py:43-52 cv2_to_tensor, used per frame at infer_video.py:80):
+ * BGR->RGB (bgr != 0; bgr == 0 keeps the channel order), INTER_AREA resize to Ho x Wo (area
+ * average rounded to u8; Ho <= H, Wo <= W — upscaling is rejected), then toTensor255
+ * (utilities.py:11-16: /255 then *255 in fp32).  frames: [B][H][W][3] u8, rows of row_bytes;
+ * out: [B][3][Ho][Wo] fp32. */
+int mhada_frame_ingest(const void* frames, int B, int H, int W, long long row_bytes, int bgr, float* out,
+                       int Ho, int Wo, mhada_stream_t stream);
 
 #ifdef __cplusplus
 }

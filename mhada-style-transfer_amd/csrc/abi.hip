@@ -68,7 +68,7 @@ const Tuning& tuning() {
 
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 3; }  // 3: mhada_set_tuning / mhada_get_tuning
+extern "C" int mhada_abi_version(void) { return 4; }  // 4: CONV3X3_ZERO, gemm_tn, backward helpers
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }
 

@@ -25,6 +25,7 @@ struct GemmP {
   const void* a; long long lda, sa1, sa2;
   const float* a_mu; long long smu1, smu2;
   int img_c, img_h, img_w, out_h, out_w;
+  int pad;  // CONV3X3_ZERO: input coordinate = output + tap - pad (zero outside the image)
   const void* w; long long ldw, sw1, sw2;
   const float* bias; long long sb1, sb2;
   const void* r; long long ldr, sr1, sr2;
@@ -90,6 +91,25 @@ MHADA_DEV void store_chunk(TC* dst, const float (&f)[Cfg<TC>::E]) {
 
 MHADA_DEV int reflect1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
+// 16 zero bytes per lane for LDS-DMA staging of zero-padding taps (a glds cannot write zeros)
+__device__ __attribute__((aligned(16))) float g_zero16[4];
+
+// Source pixel of output (y, x) under 3x3 tap offset (dy, dx) in {-1,0,1}: reflect modes fold
+// the coordinate back into the (output) grid (ReflectionPad2d(1)); CONV3X3_ZERO shifts by
+// 1 - pad and reports taps outside the input as zero padding (returns false).
+template <int AMODE>
+MHADA_DEV bool conv_src(const GemmP& p, int y, int x, int dy, int dx, int& Y, int& X) {
+  if constexpr (AMODE == MHADA_A_CONV3X3_ZERO) {
+    Y = y + dy + 1 - p.pad;
+    X = x + dx + 1 - p.pad;
+    return Y >= 0 && Y < p.img_h && X >= 0 && X < p.img_w;
+  } else {
+    Y = reflect1(y + dy, p.out_h);
+    X = reflect1(x + dx, p.out_w);
+    return true;
+  }
+}
+
 // Internal A mode: ROWS with per-column centring (a_mu != NULL), a separate instantiation so
 // the plain ROWS path stages raw chunks with no per-element work.
 constexpr int kRowsCentred = 100;
@@ -145,10 +165,10 @@ MHADA_DEV void issue_a(AStage<TA, TC, AMODE, A_CH>& st, const GemmP& p, const TA
     const int dy = tap / 3 - 1, dx = tap % 3 - 1;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int Y = reflect1(ri[i].y + dy, p.out_h);
-      const int X = reflect1(ri[i].x + dx, p.out_w);
-      const bool ok = ri[i].valid && kvalid;
-      if constexpr (AMODE == MHADA_A_CONV3X3) {
+      int Y, X;
+      const bool inside = conv_src<AMODE>(p, ri[i].y, ri[i].x, dy, dx, Y, X);
+      const bool ok = ri[i].valid && kvalid && inside;
+      if constexpr (AMODE == MHADA_A_CONV3X3 || AMODE == MHADA_A_CONV3X3_ZERO) {
         const TA* src = abase + (((long long)ri[i].b * p.img_h + Y) * p.img_w + X) * cin_n + cin;
         st.raw[i][0] = ok ? load_raw<TA, TC>(src) : zero_raw<TA, TC>();
         st.wt[i][0] = 1.f;
@@ -757,9 +777,10 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int Y = reflect1(s.y[hh][i] + dy, p.out_h), X = reflect1(s.x[hh][i] + dx, p.out_w);
+        int Y, X;
+        const bool inside = conv_src<AMODE>(p, s.y[hh][i], s.x[hh][i], dy, dx, Y, X);
         const unsigned off = (unsigned)(((s.b[hh][i] * p.img_h + Y) * p.img_w + X) * cin_n + cin0 + cofs[i]);
-        glds16(s.ab + off, dst + PE * i);
+        glds16(inside ? (const void*)(s.ab + off) : (const void*)g_zero16, dst + PE * i);
       }
     }
   };
@@ -984,7 +1005,7 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   if constexpr (sizeof(TC) == 4) {
     // persistent ping-pong (256x256 tiles) when there are at least as many tiles as CUs (below
     // that the 128x128 kernel keeps more of the chip busy); tuning gemm_pp / gemm_persist = 0 disable
-    if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3)) {
+    if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3 || AMODE == MHADA_A_CONV3X3_ZERO)) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && t256 >= num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE))
@@ -1018,6 +1039,7 @@ static int dispatch_mode(int mode, const GemmP& p, int nz, hipStream_t s) {
       return dispatch_tile<TC, TA, TO, MHADA_A_ROWS>(p, nz, s);
     case MHADA_A_CONV3X3: return dispatch_tile<TC, TA, TO, MHADA_A_CONV3X3>(p, nz, s);
     case MHADA_A_CONV3X3_UP2: return dispatch_tile<TC, TA, TO, MHADA_A_CONV3X3_UP2>(p, nz, s);
+    case MHADA_A_CONV3X3_ZERO: return dispatch_tile<TC, TA, TO, MHADA_A_CONV3X3_ZERO>(p, nz, s);
     case MHADA_A_PATCH8:
       if constexpr (sizeof(TA) == 4) return dispatch_tile<TC, TA, TO, MHADA_A_PATCH8>(p, nz, s);
       return fail("mhada_gemm: PATCH8 needs an fp32 image");
@@ -1080,6 +1102,18 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
       if (a->M != p.out_h * p.out_w) return fail("mhada_gemm: PATCH8 needs M == (H/8)*(W/8)");
       if (a->a_mu) return fail("mhada_gemm: centring only in ROWS mode");
       break;
+    case MHADA_A_CONV3X3_ZERO: {
+      const int pad = a->pad ? a->pad : 1;
+      if (pad < 1 || pad > 2) return fail("mhada_gemm: CONV3X3_ZERO needs pad 1 or 2");
+      if (a->img_c % bk) return fail("mhada_gemm: CONV needs Cin % (128 bytes of compute type) == 0");
+      if (a->K != 9 * a->img_c) return fail("mhada_gemm: CONV needs K == 9*Cin");
+      p.pad = pad;
+      p.out_h = a->img_h + 2 * (pad - 1); p.out_w = a->img_w + 2 * (pad - 1);
+      if (a->M % (p.out_h * p.out_w)) return fail("mhada_gemm: CONV needs M == batch*out_h*out_w");
+      if (a->nb1 * a->nb2 != 1) return fail("mhada_gemm: CONV is not z-batched (batch lives in M)");
+      if (a->a_mu) return fail("mhada_gemm: centring only in ROWS mode");
+      break;
+    }
     case MHADA_A_CONV3X3:
     case MHADA_A_CONV3X3_UP2: {
       const int up = a->a_mode == MHADA_A_CONV3X3_UP2 ? 2 : 1;

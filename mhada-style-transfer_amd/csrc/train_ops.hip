@@ -1,0 +1,523 @@
+// Training-path kernels (train_image.py:139 loss.backward(), fp32): the pieces autograd needs
+// around the forward GEMM/conv kernels of gemm.hip.
+//
+//   mhada_gemm_tn     C[M][N] = sum_k A[k][m] B[k][n] — the weight-gradient contraction: conv
+//                     wgrad (B = im2col of the layer input, reflect or zero padding) and linear
+//                     dW = dY^T X.  fp32 MFMA (v_mfma_f32_32x32x2_f32), split over K into
+//                     partial slabs that a second pass sums in a FIXED order (deterministic;
+//                     no float atomics).
+//   mhada_colsum      bias gradients: column sums of dY rows (split rows + the same reduction).
+//   mhada_relu_bwd    dY * (Y > 0) (threshold_backward on the saved ReLU output).
+//   mhada_reflect_fold  the adjoint of ReflectionPad2d(1): folds the full-correlation input
+//                     gradient on the padded grid (H+2)x(W+2) back onto H x W.
+//   mhada_maxpool2 / mhada_maxpool2_bwd  MaxPool2d(2, 2) (vgg19.py, torchvision cfg E) forward and
+//                     backward (gradient to the FIRST maximum of each window in row-major scan
+//                     order, as ATen's max_pool2d keeps it).
+//   mhada_upsample2x_bwd  adjoint of the bilinear x2 upsample (conv.py:71, align_corners=False).
+//   mhada_vgg_input / mhada_vgg_input_bwd  imageNet1k_normalize (vgg19.py:6-12) fused with the
+//                     NCHW -> NHWC layout change (channels zero padded to a multiple of 32 so the
+//                     first conv runs on the implicit-GEMM kernel), and its adjoint.
+// Layouts: activations NHWC fp32 (token-major, as the inference engine).
+#include "common.h"
+
+#include <algorithm>
+
+namespace mhada {
+
+// ======================================================================================
+// TN GEMM with split-K partial slabs
+// ======================================================================================
+struct TnP {
+  int M, N, K;
+  const float* a; long long lda;          // A[k * lda + m]
+  const float* b; long long ldb;          // ROWS: B[k * ldb + n]
+  int img_c, img_h, img_w, out_h, out_w, pad;  // CONV: k = output pixel (b, oy, ox), n = tap*Cin + ci
+  float* slab;                            // [splits][M][N]
+  int kchunk, tiles_n;
+};
+
+constexpr int kTnBM = 128, kTnBN = 128, kTnBK = 32;
+
+MHADA_DEV int tn_reflect(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
+
+// BMODE: MHADA_A_ROWS, MHADA_A_CONV3X3 (reflect pad 1), MHADA_A_CONV3X3_ZERO (zero pad `pad`).
+// VEC_A: A rows are 16-B aligned with M % 4 == 0 (else element loads, e.g. the 3-channel layer).
+template <int BMODE, bool VEC_A>
+__global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kTnBK][kTnBM];
+  __shared__ __attribute__((aligned(16))) float sB[2][kTnBK][kTnBN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves of 64 x 64
+  const int h = lane >> 5, r32 = lane & 31;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
+  const int m0 = tm * kTnBM, n0 = tn * kTnBN;
+  const int kbeg = blockIdx.y * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+
+  // staging: chunk c = tid + 256 i (i < 4) -> tile row c >> 5 = (tid >> 5) + 8 i, 4 columns at 4 (c & 31)
+  const int col = 4 * (tid & 31), row0 = tid >> 5;
+  // B gather: the column quad of this thread is fixed for the whole K loop (tap, channel)
+  int tap_dy = 0, tap_dx = 0, ci = 0;
+  const bool bcol_ok = n0 + col < p.N;  // N % 4 == 0 for every B mode (checked on the host)
+  if constexpr (BMODE != MHADA_A_ROWS) {
+    const int n = min(n0 + col, p.N - 4);
+    const int tap = n / p.img_c;
+    ci = n - tap * p.img_c;
+    tap_dy = tap / 3 - 1;
+    tap_dx = tap - (tap / 3) * 3 - 1;
+  }
+  f32x4 ra[4], rb[4];
+  auto issue = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + row0 + 8 * i;
+      const bool kok = k < kend;
+      // A
+      const int m = m0 + col;
+      if constexpr (VEC_A) {
+        ra[i] = (kok && m < p.M) ? *reinterpret_cast<const f32x4*>(p.a + (long long)k * p.lda + m) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ra[i][e] = (kok && m + e < p.M) ? p.a[(long long)k * p.lda + m + e] : 0.f;
+      }
+      // B
+      if constexpr (BMODE == MHADA_A_ROWS) {
+        rb[i] = (kok && bcol_ok) ? *reinterpret_cast<const f32x4*>(p.b + (long long)k * p.ldb + n0 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        bool ok = kok && bcol_ok;
+        long long src = 0;
+        if (ok) {
+          const int hw = p.out_h * p.out_w;
+          const int bb = k / hw, rem = k - bb * hw;
+          const int oy = rem / p.out_w, ox = rem - oy * p.out_w;
+          int Y, X;
+          if constexpr (BMODE == MHADA_A_CONV3X3_ZERO) {
+            Y = oy + tap_dy + 1 - p.pad;
+            X = ox + tap_dx + 1 - p.pad;
+            ok = Y >= 0 && Y < p.img_h && X >= 0 && X < p.img_w;
+          } else {
+            Y = tn_reflect(oy + tap_dy, p.img_h);
+            X = tn_reflect(ox + tap_dx, p.img_w);
+          }
+          src = (((long long)bb * p.img_h + Y) * p.img_w + X) * p.img_c + ci;
+        }
+        rb[i] = ok ? *reinterpret_cast<const f32x4*>(p.b + src) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<f32x4*>(&sA[buf][row0 + 8 * i][col]) = ra[i];
+      *reinterpret_cast<f32x4*>(&sB[buf][row0 + 8 * i][col]) = rb[i];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nst = (kend - kbeg + kTnBK - 1) / kTnBK;
+  if (nst > 0) {
+    issue(kbeg);
+    commit(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    const bool more = st + 1 < nst;
+    if (more) issue(kbeg + (st + 1) * kTnBK);
+#pragma unroll
+    for (int kk = 0; kk < kTnBK; kk += 2) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) av[mi] = sA[buf][kk + h][wm * 64 + mi * 32 + r32];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bv[ni] = sB[buf][kk + h][wn * 64 + ni * 32 + r32];
+      // D[n][m]: B is the MFMA A operand, so the lane owns output row m = ... + r32 and the
+      // registers 4g..4g+3 hold 4 consecutive columns n (16-B slab stores)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[ni], av[mi], acc[mi][ni], 0, 0, 0);
+    }
+    if (more) commit(buf ^ 1);
+    __syncthreads();
+  }
+
+  float* slab = p.slab + (long long)blockIdx.y * p.M * p.N;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int m = m0 + wm * 64 + mi * 32 + r32;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 64 + ni * 32 + 8 * g + 4 * h;
+        if (n < p.N)  // N % 4 == 0
+          *reinterpret_cast<f32x4*>(slab + (long long)m * p.N + n) =
+              f32x4{acc[mi][ni][4 * g], acc[mi][ni][4 * g + 1], acc[mi][ni][4 * g + 2], acc[mi][ni][4 * g + 3]};
+      }
+  }
+}
+
+// out[i] = sum_{s < S} slab[s][i], fixed order; out may have a row stride (ld >= ncol)
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          long long rows, int ncol, long long ld, int S) {
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;  // quad index
+  const long long n4 = rows * ncol / 4;
+  if (q >= n4) return;
+  const long long total = rows * ncol;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(slab + 4 * q);
+  for (int s = 1; s < S; ++s) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(slab + (long long)s * total + 4 * q);
+    acc += v;
+  }
+  const long long i = 4 * q, r = i / ncol, c = i - r * ncol;
+  if (ld == ncol) {
+    *reinterpret_cast<f32x4*>(out + i) = acc;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[r * ld + c + e] = acc[e];
+  }
+}
+
+int tn_splits(int M, int N, int K) {
+  const int tiles = ((M + kTnBM - 1) / kTnBM) * ((N + kTnBN - 1) / kTnBN);
+  const int target = 1024;  // blocks: 2 per CU resident, 2 waves of them
+  int s = (target + tiles - 1) / tiles;
+  const int maxs = (K + kTnBK * 8 - 1) / (kTnBK * 8);  // at least 8 K-stages per split
+  return std::max(1, std::min(s, maxs));
+}
+
+// ======================================================================================
+// column sums (bias gradients): slab[chunk][c] = sum of rows in the chunk
+// ======================================================================================
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x, float* __restrict__ slab, long long rows,
+                                                     int C, long long rows_per_chunk) {
+  const int c = 4 * (blockIdx.y * 256 + threadIdx.x);
+  if (c >= C) return;
+  const long long r0 = (long long)blockIdx.x * rows_per_chunk, r1 = std::min(rows, r0 + rows_per_chunk);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  long long r = r0;
+  for (; r + 1 < r1; r += 2) {
+    a += *reinterpret_cast<const f32x4*>(x + r * C + c);
+    b += *reinterpret_cast<const f32x4*>(x + (r + 1) * C + c);
+  }
+  if (r < r1) a += *reinterpret_cast<const f32x4*>(x + r * C + c);
+  *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * C + c) = a + b;
+}
+
+// ======================================================================================
+// elementwise / layout kernels
+// ======================================================================================
+__global__ void __launch_bounds__(256) relu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                       float* __restrict__ dx, long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const f32x4 g = reinterpret_cast<const f32x4*>(dy)[i];
+  const f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = v[e] > 0.f ? g[e] : 0.f;
+  reinterpret_cast<f32x4*>(dx)[i] = o;
+}
+
+// dX[b][y][x] = sum of dXp[b][py][px] over the padded positions whose reflection is (y, x):
+// py = y + 1, plus py = 0 when y == 1 and py = H + 1 when y == H - 2 (same in x).
+__global__ void __launch_bounds__(256) reflect_fold_kernel(const float* __restrict__ dxp, float* __restrict__ dx, int B,
+                                                           int H, int W, int C) {
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int C4 = C / 4;
+  const long long total = (long long)B * H * W * C4;
+  if (q >= total) return;
+  const int c4 = (int)(q % C4);
+  long long pix = q / C4;
+  const int x = (int)(pix % W);
+  pix /= W;
+  const int y = (int)(pix % H);
+  const int b = (int)(pix / H);
+  // padded rows folding onto y: y + 1 always; 0 (reflect(-1) = 1) when y == 1; H + 1
+  // (reflect(H) = H - 2) when y == H - 2 — both extra ones at H == 3, y == 1
+  int ys[3], xs[3], ny = 0, nx = 0;
+  ys[ny++] = y + 1;
+  if (y == 1) ys[ny++] = 0;
+  if (y == H - 2) ys[ny++] = H + 1;
+  xs[nx++] = x + 1;
+  if (x == 1) xs[nx++] = 0;
+  if (x == W - 2) xs[nx++] = W + 1;
+  const int Hp = H + 2, Wp = W + 2;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < ny; ++i)
+    for (int j = 0; j < nx; ++j)
+      acc += *reinterpret_cast<const f32x4*>(dxp + (((long long)b * Hp + ys[i]) * Wp + xs[j]) * C + 4 * c4);
+  *reinterpret_cast<f32x4*>(dx + (((long long)b * H + y) * W + x) * C + 4 * c4) = acc;
+}
+
+__global__ void __launch_bounds__(256) maxpool2_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H,
+                                                       int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (long long)B * Ho * Wo * C4) return;
+  const int c4 = (int)(q % C4);
+  long long pix = q / C4;
+  const int ox = (int)(pix % Wo);
+  pix /= Wo;
+  const int oy = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  const float* base = x + (((long long)b * H + 2 * oy) * W + 2 * ox) * C + 4 * c4;
+  const f32x4 v00 = *reinterpret_cast<const f32x4*>(base), v01 = *reinterpret_cast<const f32x4*>(base + C);
+  const f32x4 v10 = *reinterpret_cast<const f32x4*>(base + (long long)W * C),
+              v11 = *reinterpret_cast<const f32x4*>(base + (long long)W * C + C);
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = fmaxf(fmaxf(v00[e], v01[e]), fmaxf(v10[e], v11[e]));
+  *reinterpret_cast<f32x4*>(y + (((long long)b * Ho + oy) * Wo + ox) * C + 4 * c4) = o;
+}
+
+// one thread per output window x 4 channels: the whole window's dX (4 positions) is written,
+// the gradient to the first maximum in the scan order (0,0), (0,1), (1,0), (1,1); rows / columns
+// beyond 2*Ho, 2*Wo (odd sizes) are zeroed by the caller
+__global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                           float* __restrict__ dx, int B, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (long long)B * Ho * Wo * C4) return;
+  const int c4 = (int)(q % C4);
+  long long pix = q / C4;
+  const int ox = (int)(pix % Wo);
+  pix /= Wo;
+  const int oy = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  const long long o00 = (((long long)b * H + 2 * oy) * W + 2 * ox) * C + 4 * c4;
+  const long long offs[4] = {o00, o00 + C, o00 + (long long)W * C, o00 + (long long)W * C + C};
+  f32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(x + offs[j]);
+  const f32x4 g = *reinterpret_cast<const f32x4*>(dy + (((long long)b * Ho + oy) * Wo + ox) * C + 4 * c4);
+  f32x4 out[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int arg = 0;
+    float mx = v[0][e];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (v[j][e] > mx || (v[j][e] != v[j][e] && mx == mx)) {  // first max; a NaN wins (ATen)
+        mx = v[j][e];
+        arg = j;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j][e] = j == arg ? g[e] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(dx + offs[j]) = out[j];
+}
+
+// adjoint of upsample2x (bilinear, align_corners=False, scale 2): input row y receives from
+// output rows 2y-1 .. 2y+2 with the forward's own weights (recomputed, so border clamps agree)
+MHADA_DEV float up2_weight(int o, int i, int n) {
+  const float s = fmaxf(((float)o + 0.5f) * 0.5f - 0.5f, 0.f);
+  const int i0 = (int)s;
+  const int i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  const float l1 = s - (float)i0, l0 = 1.f - l1;
+  return (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+__global__ void __launch_bounds__(256) upsample2x_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, int B,
+                                                             int H, int W, int C) {
+  const int C4 = C / 4;
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (long long)B * H * W * C4) return;
+  const int c4 = (int)(q % C4);
+  long long pix = q / C4;
+  const int x = (int)(pix % W);
+  pix /= W;
+  const int y = (int)(pix % H);
+  const int b = (int)(pix / H);
+  const int Ho = 2 * H, Wo = 2 * W;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int oy = max(0, 2 * y - 1); oy <= min(Ho - 1, 2 * y + 2); ++oy) {
+    const float wy = up2_weight(oy, y, H);
+    if (wy == 0.f) continue;
+    for (int ox = max(0, 2 * x - 1); ox <= min(Wo - 1, 2 * x + 2); ++ox) {
+      const float wx = up2_weight(ox, x, W);
+      if (wx == 0.f) continue;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(dy + (((long long)b * Ho + oy) * Wo + ox) * C + 4 * c4);
+      acc += (wy * wx) * g;
+    }
+  }
+  *reinterpret_cast<f32x4*>(dx + (((long long)b * H + y) * W + x) * C + 4 * c4) = acc;
+}
+
+__constant__ float c_in_mean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float c_in_std[3] = {0.229f, 0.224f, 0.225f};
+
+// (x / 255 - mean) / std, three fp32 roundings as vgg19.py:11; NCHW [B][3][H][W] -> NHWC [B][H][W][Cp]
+__global__ void __launch_bounds__(256) vgg_input_kernel(const float* __restrict__ img, float* __restrict__ out, int B,
+                                                        int H, int W, int Cp) {
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)H * W;
+  if (pix >= (long long)B * plane) return;
+  const long long b = pix / plane, r = pix - b * plane;
+  float* o = out + pix * Cp;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float v = img[(b * 3 + c) * plane + r];
+    v = v / 255.0f;
+    v = v - c_in_mean[c];
+    o[c] = v / c_in_std[c];
+  }
+  for (int c = 3; c < Cp; c += 1) o[c] = 0.f;
+}
+
+// adjoint: d img[b][c][y][x] = d out[b][y][x][c] / std_c / 255 (the chain of the three ops)
+__global__ void __launch_bounds__(256) vgg_input_bwd_kernel(const float* __restrict__ dout, float* __restrict__ dimg,
+                                                            int B, int H, int W, int Cp) {
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)H * W;
+  if (pix >= (long long)B * plane) return;
+  const long long b = pix / plane, r = pix - b * plane;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dimg[(b * 3 + c) * plane + r] = dout[pix * Cp + c] / c_in_std[c] / 255.0f;
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static dim3 grid1(long long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace mhada
+
+using namespace mhada;
+
+extern "C" int mhada_gemm_tn_splits(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  return tn_splits(M, N, K);
+}
+
+extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long work_floats, mhada_stream_t s_) {
+  if (!a || !a->a || !a->b || !a->c || !work) return fail("mhada_gemm_tn: null argument");
+  const hipStream_t s = (hipStream_t)s_;
+  if (a->M <= 0 || a->N <= 0 || a->K <= 0) return fail("mhada_gemm_tn: bad sizes");
+  if (a->N % 4) return fail("mhada_gemm_tn: N must be a multiple of 4");
+  if (!al16(work) || !al16(a->b)) return fail("mhada_gemm_tn: B and the workspace must be 16-byte aligned");
+  if (a->ldc < a->N) return fail("mhada_gemm_tn: ldc < N");
+  TnP p{};
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.a = a->a; p.lda = a->lda; p.b = a->b; p.ldb = a->ldb;
+  const bool vec_a = al16(a->a) && a->lda % 4 == 0 && a->M % 4 == 0;
+  switch (a->b_mode) {
+    case MHADA_A_ROWS:
+      if (a->ldb % 4) return fail("mhada_gemm_tn: ldb must be a multiple of 4");
+      break;
+    case MHADA_A_CONV3X3:
+    case MHADA_A_CONV3X3_ZERO: {
+      const int pad = a->b_mode == MHADA_A_CONV3X3 ? 1 : (a->pad ? a->pad : 1);
+      if (pad < 1 || pad > 2) return fail("mhada_gemm_tn: pad 1 or 2");
+      if (a->img_c % 4 || a->N != 9 * a->img_c) return fail("mhada_gemm_tn: CONV needs N == 9*Cin, Cin % 4 == 0");
+      p.img_c = a->img_c; p.img_h = a->img_h; p.img_w = a->img_w; p.pad = pad;
+      p.out_h = a->img_h + 2 * (pad - 1); p.out_w = a->img_w + 2 * (pad - 1);
+      if (a->b_mode == MHADA_A_CONV3X3 && (a->img_h < 2 || a->img_w < 2)) return fail("mhada_gemm_tn: reflect needs H, W >= 2");
+      if (a->K % (p.out_h * p.out_w)) return fail("mhada_gemm_tn: CONV needs K == batch*out_h*out_w");
+      break;
+    }
+    default:
+      return fail("mhada_gemm_tn: bad b_mode");
+  }
+  int S = tn_splits(p.M, p.N, p.K);
+  const long long per = (long long)p.M * p.N;
+  if (work_floats < per) return fail("mhada_gemm_tn: workspace smaller than M*N floats");
+  S = (int)std::min<long long>(S, work_floats / per);
+  p.kchunk = ((p.K + S - 1) / S + kTnBK - 1) / kTnBK * kTnBK;
+  S = (p.K + p.kchunk - 1) / p.kchunk;
+  p.tiles_n = (p.N + kTnBN - 1) / kTnBN;
+  const int tiles = ((p.M + kTnBM - 1) / kTnBM) * p.tiles_n;
+  p.slab = work;
+  if (S > 65535) return fail("mhada_gemm_tn: too many splits");
+  const dim3 grid((unsigned)tiles, (unsigned)S);
+#define TN_LAUNCH(MODE)                                                                   \
+  do {                                                                                    \
+    if (vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true>), grid, dim3(256), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_tn_kernel<MODE, false>), grid, dim3(256), 0, s, p);      \
+  } while (0)
+  if (a->b_mode == MHADA_A_ROWS) TN_LAUNCH(MHADA_A_ROWS);
+  else if (a->b_mode == MHADA_A_CONV3X3) TN_LAUNCH(MHADA_A_CONV3X3);
+  else TN_LAUNCH(MHADA_A_CONV3X3_ZERO);
+#undef TN_LAUNCH
+  if (int rc = check_launch("mhada_gemm_tn")) return rc;
+  hipLaunchKernelGGL(slab_reduce_kernel, grid1(per / 4), dim3(256), 0, s, work, a->c, (long long)p.M, p.N, a->ldc, S);
+  return check_launch("mhada_gemm_tn(reduce)");
+}
+
+extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, float* work, long long work_floats,
+                            mhada_stream_t s_) {
+  if (!x || !out || !work || rows <= 0 || C <= 0) return fail("mhada_colsum: bad args");
+  if (C % 4 || !al16(x) || !al16(work)) return fail("mhada_colsum: C % 4 == 0 and 16-byte aligned x, work");
+  long long chunks = std::min<long long>(std::max<long long>(1, rows / 256), 1024);
+  chunks = std::min<long long>(chunks, work_floats / C);
+  if (chunks < 1) return fail("mhada_colsum: workspace smaller than C floats");
+  const long long rpc = (rows + chunks - 1) / chunks;
+  chunks = (rows + rpc - 1) / rpc;
+  const dim3 grid((unsigned)chunks, (unsigned)((C / 4 + 255) / 256));
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)s_, x, work, rows, C, rpc);
+  if (int rc = check_launch("mhada_colsum")) return rc;
+  hipLaunchKernelGGL(slab_reduce_kernel, grid1(C / 4), dim3(256), 0, (hipStream_t)s_, work, out, 1LL, C, (long long)C,
+                     (int)chunks);
+  return check_launch("mhada_colsum(reduce)");
+}
+
+extern "C" int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t s_) {
+  if (!dy || !y || !dx || n <= 0 || n % 4 || !al16(dy) || !al16(y) || !al16(dx))
+    return fail("mhada_relu_bwd: bad args (n % 4 == 0, 16-byte aligned)");
+  hipLaunchKernelGGL(relu_bwd_kernel, grid1(n / 4), dim3(256), 0, (hipStream_t)s_, dy, y, dx, n / 4);
+  return check_launch("mhada_relu_bwd");
+}
+
+extern "C" int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t s_) {
+  if (!dxp || !dx || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(dxp) || !al16(dx))
+    return fail("mhada_reflect_fold: bad args");
+  hipLaunchKernelGGL(reflect_fold_kernel, grid1((long long)B * H * W * (C / 4)), dim3(256), 0, (hipStream_t)s_, dxp, dx,
+                     B, H, W, C);
+  return check_launch("mhada_reflect_fold");
+}
+
+extern "C" int mhada_maxpool2(const float* x, float* y, int B, int H, int W, int C, mhada_stream_t s_) {
+  if (!x || !y || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(x) || !al16(y)) return fail("mhada_maxpool2: bad args");
+  hipLaunchKernelGGL(maxpool2_kernel, grid1((long long)B * (H / 2) * (W / 2) * (C / 4)), dim3(256), 0, (hipStream_t)s_,
+                     x, y, B, H, W, C);
+  return check_launch("mhada_maxpool2");
+}
+
+extern "C" int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+                                  mhada_stream_t s_) {
+  if (!x || !dy || !dx || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(x) || !al16(dy) || !al16(dx))
+    return fail("mhada_maxpool2_bwd: bad args");
+  if (H % 2 || W % 2) (void)hipMemsetAsync(dx, 0, (size_t)B * H * W * C * sizeof(float), (hipStream_t)s_);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, grid1((long long)B * (H / 2) * (W / 2) * (C / 4)), dim3(256), 0,
+                     (hipStream_t)s_, x, dy, dx, B, H, W, C);
+  return check_launch("mhada_maxpool2_bwd");
+}
+
+extern "C" int mhada_upsample2x_bwd(const float* dy, float* dx, int B, int H, int W, int C, mhada_stream_t s_) {
+  if (!dy || !dx || B <= 0 || H <= 0 || W <= 0 || C % 4 || !al16(dy) || !al16(dx))
+    return fail("mhada_upsample2x_bwd: bad args");
+  hipLaunchKernelGGL(upsample2x_bwd_kernel, grid1((long long)B * H * W * (C / 4)), dim3(256), 0, (hipStream_t)s_, dy, dx,
+                     B, H, W, C);
+  return check_launch("mhada_upsample2x_bwd");
+}
+
+extern "C" int mhada_vgg_input(const float* img, float* out, int B, int H, int W, int Cp, mhada_stream_t s_) {
+  if (!img || !out || B <= 0 || H <= 0 || W <= 0 || Cp < 3) return fail("mhada_vgg_input: bad args");
+  hipLaunchKernelGGL(vgg_input_kernel, grid1((long long)B * H * W), dim3(256), 0, (hipStream_t)s_, img, out, B, H, W, Cp);
+  return check_launch("mhada_vgg_input");
+}
+
+extern "C" int mhada_vgg_input_bwd(const float* dout, float* dimg, int B, int H, int W, int Cp, mhada_stream_t s_) {
+  if (!dout || !dimg || B <= 0 || H <= 0 || W <= 0 || Cp < 3) return fail("mhada_vgg_input_bwd: bad args");
+  hipLaunchKernelGGL(vgg_input_bwd_kernel, grid1((long long)B * H * W), dim3(256), 0, (hipStream_t)s_, dout, dimg, B, H,
+                     W, Cp);
+  return check_launch("mhada_vgg_input_bwd");
+}

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmhada_hi
 
 F32, BF16 = 0, 1
 ACT_SOFTMAX, ACT_COSINE = 0, 1
-A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2 = 0, 1, 2, 3
+A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO = 0, 1, 2, 3, 4
 
 _c_ll = ctypes.c_longlong
 _vp = ctypes.c_void_p
@@ -33,7 +33,17 @@ class GemmArgs(ctypes.Structure):
         ("bias", _vp), ("sb1", _c_ll), ("sb2", _c_ll),
         ("r", _vp), ("r_dtype", ctypes.c_int), ("ldr", _c_ll), ("sr1", _c_ll), ("sr2", _c_ll),
         ("c", _vp), ("c_dtype", ctypes.c_int), ("ldc", _c_ll), ("sc1", _c_ll), ("sc2", _c_ll),
-        ("relu", ctypes.c_int),
+        ("relu", ctypes.c_int), ("pad", ctypes.c_int),
+    ]
+
+
+class GemmTnArgs(ctypes.Structure):
+    """mirror of ``mhada_gemm_tn_args``"""
+    _fields_ = [
+        ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+        ("a", _vp), ("lda", _c_ll), ("b", _vp), ("ldb", _c_ll), ("b_mode", ctypes.c_int),
+        ("img_c", ctypes.c_int), ("img_h", ctypes.c_int), ("img_w", ctypes.c_int), ("pad", ctypes.c_int),
+        ("c", _vp), ("ldc", _c_ll),
     ]
 
 
@@ -60,6 +70,19 @@ SIGNATURES = {
     "mhada_warp": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_flow_warp_mask": (_I, [_vp, _vp, _vp, _I, _I, _F, _I, _vp]),
     "mhada_warp_l1": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_frame_ingest": (_I, [_vp, _I, _I, _I, _c_ll, _I, _vp, _I, _I, _vp]),
+    "mhada_gemm_tn_splits": (_I, [_I, _I, _I]),
+    "mhada_loss_attn": (_I, [_vp] * 7 + [_I, _I, _I, _I, _I, _I, _vp]),
+    "mhada_rows_normalize": (_I, [_vp] * 4 + [_I, _I, _I, _I, _vp]),
+    "mhada_gemm_tn": (_I, [ctypes.POINTER(GemmTnArgs), _vp, _c_ll, _vp]),
+    "mhada_colsum": (_I, [_vp, _vp, _c_ll, _I, _vp, _c_ll, _vp]),
+    "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
+    "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_upsample2x_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_vgg_input": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_vgg_input_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
 }
 
 _lib = None
@@ -89,7 +112,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 def get_tuning(name: str) -> int:

@@ -160,7 +160,12 @@ def block_forward(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) ->
 
 
 def decoder_forward(dec, x: torch.Tensor) -> torch.Tensor:
-    """Decoder.forward (conv.py:96-100)."""
+    """Decoder.forward (conv.py:96-100): on a ROCm device the HIP training kernels
+    (train_fns: implicit-GEMM conv fwd / dgrad / wgrad, upsample and its adjoint); the CPU
+    (test plumbing) evaluates the same expression with aten ops."""
+    if x.is_cuda:
+        from . import train_fns
+        return train_fns.decoder_forward(dec, x, DECODER_ORDER)
     for seq, idx, up in DECODER_ORDER:
         conv = getattr(dec, seq)[idx].conv.conv
         x = F.relu(conv(F.pad(x, (1, 1, 1, 1), mode="reflect")))
@@ -187,7 +192,13 @@ def imagenet_normalize(x: torch.Tensor) -> torch.Tensor:
 
 
 def vgg19_forward(vgg, x: torch.Tensor) -> Dict[str, torch.Tensor]:
-    """VGG19.forward (vgg19.py:42-70): relu1_1 .. relu5_1."""
+    """VGG19.forward (vgg19.py:42-70): relu1_1 .. relu5_1.  On a ROCm device: the HIP kernels
+    (train_fns: zero-padded implicit-GEMM convs with fused ReLU, max-pool, fused normalise;
+    features are NCHW views of NHWC storage); on the CPU: aten."""
+    if x.is_cuda:
+        from network.vgg19 import _CONVS, _POOLS, _SLICES
+        from . import train_fns
+        return train_fns.vgg19_forward(vgg, x, {i for i, _, _ in _CONVS}, set(_POOLS), _SLICES)
     x = imagenet_normalize(x)
     feats = {}
     for i in range(1, 6):
@@ -196,9 +207,30 @@ def vgg19_forward(vgg, x: torch.Tensor) -> Dict[str, torch.Tensor]:
     return feats
 
 
+def _tokens(x: torch.Tensor) -> torch.Tensor:
+    """NCHW (any strides; free for channels-last views) -> contiguous fp32 [B][H*W][C]."""
+    B, C, h, w = x.shape
+    return x.permute(0, 2, 3, 1).float().contiguous().view(B, h * w, C)
+
+
 def ada_attn_for_loss(c_x, s_x, c_1x, s_1x, activation: str = "softmax", chunk: int = 4096) -> torch.Tensor:
-    """AdaAttnForLoss.forward (adaDecoder.py:52-81), query-chunked so the Nc x Ns attention
-    matrix is never whole (relu3_1 at 512^2 is 16384 x 16384 per image)."""
+    """AdaAttnForLoss.forward (adaDecoder.py:52-81).  The training step needs it without gradients
+    (its inputs are VGG features of the content and style images, lossfn.py:26-34): on a ROCm
+    device that runs the wide-head HIP kernel (mhada_loss_attn: flash-style, A never stored,
+    fp32 MFMA); the result is an NCHW view of token-major storage.  When a gradient is required
+    (a caller differentiating through the target) or on the CPU, the reference expression is
+    evaluated with aten ops, query-chunked so the Nc x Ns matrix is never whole."""
+    grad = torch.is_grad_enabled() and any(t.requires_grad for t in (c_x, s_x, c_1x, s_1x))
+    if c_x.is_cuda and not grad:
+        from ._lib import ACT_COSINE, ACT_SOFTMAX
+        unit = activation == "cosine"
+        qt, kt, vt, xt = _tokens(c_1x), _tokens(s_1x), _tokens(s_x), _tokens(c_x)
+        qn = ops.rows_normalize(qt, *ops.instnorm_stats(qt), unit=unit)
+        kn = ops.rows_normalize(kt, *ops.instnorm_stats(kt), unit=unit)
+        x_mu, x_rs = ops.instnorm_stats(xt)
+        out = ops.loss_attn(qn, kn, vt, xt, x_mu, x_rs, ACT_COSINE if unit else ACT_SOFTMAX)
+        B, C, h, w = c_x.shape
+        return out.view(B, h, w, C).permute(0, 3, 1, 2)
     b, _, h, w = c_1x.shape
     q = F.instance_norm(c_1x).reshape(b, -1, h * w).permute(0, 2, 1)
     k = F.instance_norm(s_1x).reshape(b, s_1x.shape[1], -1)

@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import A_CONV3X3, A_CONV3X3_UP2, A_PATCH8, A_ROWS, BF16, F32, GemmArgs
+from ._lib import A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO, A_PATCH8, A_ROWS, BF16, F32, GemmArgs, GemmTnArgs
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -60,7 +60,7 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
          a_mu: Optional[torch.Tensor] = None, smu=(0, 0), img=(0, 0, 0),
          ldw: int = 0, sw=(0, 0), bias: Optional[torch.Tensor] = None, sb=(0, 0),
          r: Optional[torch.Tensor] = None, ldr: int = 0, sr=(0, 0),
-         ldc: int = 0, sc=(0, 0), relu: bool = False) -> torch.Tensor:
+         ldc: int = 0, sc=(0, 0), relu: bool = False, pad: int = 0) -> torch.Tensor:
     """``mhada_gemm``: C[z] = act(A[z] W[z]^T + bias[z]) + R[z]; strides in elements."""
     _need_gpu(a, w, c, a_mu, bias, r)
     if w.dtype != compute:
@@ -91,6 +91,7 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     args.c, args.c_dtype, args.ldc = c.data_ptr(), dt_code(c.dtype), ldc
     args.sc1, args.sc2 = sc
     args.relu = int(relu)
+    args.pad = int(pad)
     _call("mhada_gemm", c, ctypes.byref(args))
     return c
 
@@ -119,17 +120,29 @@ def patch_embed(img: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, pos: Opt
                 r=pos, ldr=C, sr=(0, 0), ldc=C, sc=(N * C, 0))
 
 
-def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out_dtype: torch.dtype,
-            upsample: bool, relu: bool = True) -> torch.Tensor:
+def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
+            upsample: bool, relu: bool = True, pad_mode: str = "reflect", pad: int = 1,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NHWC x [B][H][W][Cin] -> NHWC [B][H'][W'][Cout]; ReflectionPad2d(1)+conv3x3(+ReLU),
-    optionally on bilinear-x2(x).  w packed [Cout][9*Cin] in the compute dtype."""
+    optionally on bilinear-x2(x), or (pad_mode "zero") a zero-padded conv with padding `pad`
+    (1: same size, 2: the full correlation, H' = H + 2).  w packed [Cout][9*Cin] in the compute
+    dtype.  ``out`` may be a preallocated [B][H'][W'][ldc >= Cout] buffer (channel padding)."""
     B, H, W, Ci = x.shape
     Co = w.shape[0]
-    Ho, Wo = (2 * H, 2 * W) if upsample else (H, W)
-    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=out_dtype)
-    return gemm(a=x, w=w, c=y, M=B * Ho * Wo, N=Co, K=9 * Ci, compute=w.dtype,
-                a_mode=A_CONV3X3_UP2 if upsample else A_CONV3X3, img=(Ci, H, W), ldw=w.stride(0),
-                bias=bias, ldc=Co, relu=relu)
+    if pad_mode == "zero":
+        if upsample:
+            raise ValueError("zero-padded conv3x3 has no fused upsample")
+        Ho, Wo = H + 2 * (pad - 1), W + 2 * (pad - 1)
+        mode = A_CONV3X3_ZERO
+    elif pad_mode == "reflect":
+        Ho, Wo = (2 * H, 2 * W) if upsample else (H, W)
+        mode = A_CONV3X3_UP2 if upsample else A_CONV3X3
+        pad = 0
+    else:
+        raise ValueError(f"pad_mode {pad_mode!r}")
+    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=out_dtype) if out is None else out
+    return gemm(a=x, w=w, c=y, M=B * Ho * Wo, N=Co, K=9 * Ci, compute=w.dtype, a_mode=mode, img=(Ci, H, W),
+                ldw=w.stride(0), bias=bias, ldc=y.shape[-1], relu=relu, pad=pad)
 
 
 def upsample2x(x: torch.Tensor) -> torch.Tensor:
@@ -334,4 +347,137 @@ def warp_l1(cs1: torch.Tensor, cs2: torch.Tensor, flow: torch.Tensor, mask: torc
     out = torch.empty(B, device=cs1.device, dtype=torch.float32)
     _call("mhada_warp_l1", cs1, cs1.data_ptr(), cs2.data_ptr(), flow.data_ptr(), mask.data_ptr(),
                                    work.data_ptr(), out.data_ptr(), B, C, H, W)
+    return out
+
+
+def frame_ingest(frames: torch.Tensor, out_hw=None, bgr: bool = True) -> torch.Tensor:
+    """``mhada_frame_ingest``: u8 frames [B][H][W][3] (or one [H][W][3]; rows may be padded) ->
+    fp32 [B][3][Ho][Wo] (BGR->RGB, INTER_AREA to out_hw = (Ho, Wo), toTensor255)."""
+    _need_gpu(frames)
+    if frames.dtype != torch.uint8:
+        raise ValueError("frames must be uint8 (H, W, 3) images")
+    if frames.dim() == 3:
+        frames = frames.unsqueeze(0)
+    if frames.dim() != 4 or frames.shape[3] != 3 or frames.stride(3) != 1 or frames.stride(2) != 3:
+        raise ValueError(f"frames must be [B][H][W][3] with packed pixels, got {tuple(frames.shape)}")
+    B, H, W, _ = frames.shape
+    if B > 1 and frames.stride(0) != H * frames.stride(1):
+        frames = frames.contiguous()
+    Ho, Wo = (H, W) if out_hw is None else out_hw
+    out = torch.empty(B, 3, Ho, Wo, device=frames.device, dtype=torch.float32)
+    _call("mhada_frame_ingest", frames, frames.data_ptr(), B, H, W, frames.stride(1), int(bgr), out.data_ptr(), Ho, Wo)
+    return out
+
+
+# ---- training path (fp32, NHWC): backward helpers (include/mhada_hip.h) ------------------
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int = 0,
+            b_mode: int = A_ROWS, img=(0, 0, 0), pad: int = 0) -> torch.Tensor:
+    """``mhada_gemm_tn``: C[M][N] = sum_k A[k][m] B[k][n] (fp32), deterministic split-K."""
+    _need_gpu(a, b)
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise ValueError("gemm_tn is fp32")
+    lib = _lib.load()
+    splits = lib.mhada_gemm_tn_splits(M, N, K)
+    work = torch.empty(max(1, splits) * M * N, device=a.device, dtype=torch.float32)
+    c = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    args = GemmTnArgs()
+    args.M, args.N, args.K = M, N, K
+    args.a, args.lda, args.b, args.ldb, args.b_mode = a.data_ptr(), lda, b.data_ptr(), ldb, b_mode
+    args.img_c, args.img_h, args.img_w = img
+    args.pad = pad
+    args.c, args.ldc = c.data_ptr(), N
+    _call("mhada_gemm_tn", a, ctypes.byref(args), work.data_ptr(), work.numel())
+    return c
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """``mhada_colsum`` over the rows of a contiguous [..., C] fp32 tensor -> [C]."""
+    _need_gpu(x)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    out = torch.empty(C, device=x.device, dtype=torch.float32)
+    work = torch.empty(min(1024, max(1, rows // 256)) * C, device=x.device, dtype=torch.float32)
+    _call("mhada_colsum", x, x.data_ptr(), out.data_ptr(), rows, C, work.data_ptr(), work.numel())
+    return out
+
+
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    _need_gpu(dy, y)
+    dx = torch.empty_like(y)
+    _call("mhada_relu_bwd", y, dy.data_ptr(), y.data_ptr(), dx.data_ptr(), y.numel())
+    return dx
+
+
+def reflect_fold(dxp: torch.Tensor) -> torch.Tensor:
+    _need_gpu(dxp)
+    B, Hp, Wp, C = dxp.shape
+    dx = torch.empty(B, Hp - 2, Wp - 2, C, device=dxp.device, dtype=torch.float32)
+    _call("mhada_reflect_fold", dxp, dxp.data_ptr(), dx.data_ptr(), B, Hp - 2, Wp - 2, C)
+    return dx
+
+
+def maxpool2(x: torch.Tensor) -> torch.Tensor:
+    _need_gpu(x)
+    B, H, W, C = x.shape
+    y = torch.empty(B, H // 2, W // 2, C, device=x.device, dtype=torch.float32)
+    _call("mhada_maxpool2", x, x.data_ptr(), y.data_ptr(), B, H, W, C)
+    return y
+
+
+def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    _need_gpu(x, dy)
+    B, H, W, C = x.shape
+    dx = torch.empty_like(x)
+    _call("mhada_maxpool2_bwd", x, x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C)
+    return dx
+
+
+def upsample2x_bwd(dy: torch.Tensor) -> torch.Tensor:
+    _need_gpu(dy)
+    B, Ho, Wo, C = dy.shape
+    dx = torch.empty(B, Ho // 2, Wo // 2, C, device=dy.device, dtype=torch.float32)
+    _call("mhada_upsample2x_bwd", dy, dy.data_ptr(), dx.data_ptr(), B, Ho // 2, Wo // 2, C)
+    return dx
+
+
+def vgg_input(img: torch.Tensor, cp: int = 32) -> torch.Tensor:
+    _need_gpu(img)
+    B, _, H, W = img.shape
+    out = torch.empty(B, H, W, cp, device=img.device, dtype=torch.float32)
+    _call("mhada_vgg_input", img, img.data_ptr(), out.data_ptr(), B, H, W, cp)
+    return out
+
+
+def vgg_input_bwd(dout: torch.Tensor) -> torch.Tensor:
+    _need_gpu(dout)
+    B, H, W, cp = dout.shape
+    dimg = torch.empty(B, 3, H, W, device=dout.device, dtype=torch.float32)
+    _call("mhada_vgg_input_bwd", dout, dout.data_ptr(), dimg.data_ptr(), B, H, W, cp)
+    return dimg
+
+
+def rows_normalize(x: torch.Tensor, mu: torch.Tensor, rs: torch.Tensor, unit: bool = False) -> torch.Tensor:
+    """``mhada_rows_normalize``: (x - mu) * rs on token rows [B][N][C] (and / |row| if unit)."""
+    _need_gpu(x, mu, rs)
+    B, N, C = x.shape
+    out = torch.empty_like(x)
+    _call("mhada_rows_normalize", x, x.data_ptr(), mu.data_ptr(), rs.data_ptr(), out.data_ptr(), int(unit), B, N, C)
+    return out
+
+
+def loss_attn(qn: torch.Tensor, kn: torch.Tensor, v: torch.Tensor, x: torch.Tensor, x_mu: torch.Tensor,
+              x_rs: torch.Tensor, activation: int) -> torch.Tensor:
+    """``mhada_loss_attn``: AdaAttnForLoss on token rows; returns [B][Nq][Dv] fp32."""
+    _need_gpu(qn, kn, v, x, x_mu, x_rs)
+    for t in (qn, kn, v, x):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("loss_attn operands must be contiguous float32 token rows")
+    B, Nq, Dqk = qn.shape
+    Ns, Dv = v.shape[1], v.shape[2]
+    if kn.shape != (B, Ns, Dqk) or x.shape != (B, Nq, Dv):
+        raise ValueError(f"loss_attn: bad shapes q{tuple(qn.shape)} k{tuple(kn.shape)} v{tuple(v.shape)} "
+                         f"x{tuple(x.shape)}")
+    out = torch.empty(B, Nq, Dv, device=qn.device, dtype=torch.float32)
+    _call("mhada_loss_attn", qn, qn.data_ptr(), kn.data_ptr(), v.data_ptr(), x.data_ptr(), x_mu.data_ptr(),
+          x_rs.data_ptr(), out.data_ptr(), B, Nq, Ns, Dqk, Dv, activation)
     return out

@@ -1,0 +1,183 @@
+"""Autograd Functions of the training path on the HIP kernels (fp32, NHWC activations).
+
+Each Function takes the reference module's own parameter tensors (``nn.Conv2d.weight`` /
+``.bias``), so autograd delivers gradients to exactly the parameters whose state_dict keys match
+the reference, and runs its forward and backward through libmhada_hip.so:
+
+* ``conv3x3``  — ReflectionPad2d(1) + Conv2d 3x3 (+ReLU) of the decoder (conv.py:23-45) or the
+  zero-padded Conv2d(padding=1) (+ReLU) of VGG19 (vgg19.py slices, torchvision cfg E).
+  forward: the implicit-GEMM conv (mhada_gemm, CONV3X3 / CONV3X3_ZERO, bias+ReLU epilogue);
+  backward: ReLU mask (mhada_relu_bwd), input gradient = the conv of dY with the flipped,
+  transposed weights (zero pad 1, or the full correlation + mhada_reflect_fold for the reflect
+  pad), weight gradient = mhada_gemm_tn over the im2col of the input, bias = mhada_colsum.
+* ``maxpool2``, ``upsample2x`` (conv.py:71), ``vgg_input`` (vgg19.py:6-12) and their adjoints.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from ._lib import A_CONV3X3, A_CONV3X3_ZERO
+
+F32 = torch.float32
+
+
+def _ceil(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def _pack_fwd(weight: torch.Tensor, cx: int) -> torch.Tensor:
+    """(Co, Ci, 3, 3) -> [Co][9*cx] with k = tap*cx + ci (channels ci >= Ci zero)."""
+    co, ci = weight.shape[:2]
+    w = weight.detach().permute(0, 2, 3, 1)
+    if cx != ci:
+        w = F.pad(w, (0, cx - ci))
+    return w.reshape(co, 9 * cx).contiguous()
+
+
+def _pack_dgrad(weight: torch.Tensor, cx: int, cg: int) -> torch.Tensor:
+    """W'[ci][ky][kx][co] = W[co][ci][2-ky][2-kx] -> [cx][9*cg] (ci >= Ci rows and co >= Co
+    columns zero): the weights of the conv that computes the input gradient."""
+    co, ci = weight.shape[:2]
+    w = weight.detach().flip(2, 3).permute(1, 2, 3, 0)  # (Ci, 3, 3, Co)
+    w = F.pad(w, (0, cg - co, 0, 0, 0, 0, 0, cx - ci))
+    return w.reshape(cx, 9 * cg).contiguous()
+
+
+def _cached(weight: torch.Tensor, kind: str, *dims) -> torch.Tensor:
+    """Packed weights of a frozen layer (VGG19), held on the weight tensor itself and keyed by
+    its version counter; trainable weights change every step and are packed per call."""
+    if weight.requires_grad:
+        return _pack_fwd(weight, *dims) if kind == "f" else _pack_dgrad(weight, *dims)
+    cache = weight.__dict__.setdefault("_mhada_pack", {})
+    key = (kind,) + dims
+    hit = cache.get(key)
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    w = _pack_fwd(weight, *dims) if kind == "f" else _pack_dgrad(weight, *dims)
+    cache[key] = (weight._version, w)
+    return w
+
+
+class Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pad_mode: str, relu: bool):
+        if x.dtype != F32 or not x.is_contiguous():
+            raise ValueError("conv3x3 (training) takes contiguous fp32 NHWC activations")
+        B, H, W, cx = x.shape
+        co, ci = weight.shape[:2]
+        if ci > cx or cx % 32:
+            raise ValueError(f"conv3x3: input channels {cx} must be a multiple of 32 and >= {ci}")
+        ldc = _ceil(co, 4)
+        y = (torch.zeros if ldc != co else torch.empty)(B, H, W, ldc, device=x.device, dtype=F32)
+        ops.conv3x3(x, _cached(weight, "f", cx), bias.detach().float().contiguous(), F32, upsample=False,
+                    relu=relu, pad_mode=pad_mode, pad=1, out=y)
+        ctx.save_for_backward(x, weight, y)
+        ctx.pad_mode, ctx.relu = pad_mode, relu
+        return y if ldc == co else y[..., :co].contiguous()
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor):
+        x, weight, y = ctx.saved_tensors
+        B, H, W, cx = x.shape
+        co = weight.shape[0]
+        ldc = y.shape[-1]
+        gy = gy.contiguous()
+        if ldc != co:
+            gy = F.pad(gy, (0, ldc - co))
+        g = ops.relu_bwd(gy, y) if ctx.relu else gy
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            cg = _ceil(co, 32)
+            gk = g if cg == ldc else F.pad(g, (0, cg - ldc))
+            wt = _cached(weight, "d", cx, cg)
+            if ctx.pad_mode == "zero":
+                gx = ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero", pad=1)
+            else:
+                gx = ops.reflect_fold(ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero",
+                                                  pad=2))
+        if ctx.needs_input_grad[1]:
+            mode = A_CONV3X3 if ctx.pad_mode == "reflect" else A_CONV3X3_ZERO
+            dw = ops.gemm_tn(g, x, M=co, N=9 * cx, K=B * H * W, lda=ldc, b_mode=mode, img=(cx, H, W), pad=1)
+            gw = dw.view(co, 3, 3, cx)[..., :weight.shape[1]].permute(0, 3, 1, 2).contiguous()
+        if ctx.needs_input_grad[2]:
+            gb = ops.colsum(g)[:co].contiguous()
+        return gx, gw, gb, None, None
+
+
+class MaxPool2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return ops.maxpool2(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return ops.maxpool2_bwd(x, gy.contiguous())
+
+
+class Upsample2xFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return ops.upsample2x(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return ops.upsample2x_bwd(gy.contiguous())
+
+
+class VggInputFn(torch.autograd.Function):
+    """imageNet1k_normalize (vgg19.py:6-12) + NCHW -> NHWC with channels padded to 32."""
+
+    @staticmethod
+    def forward(ctx, img):
+        return ops.vgg_input(img.float().contiguous(), 32)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.vgg_input_bwd(g.contiguous())
+
+
+def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True):
+    return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu)
+
+
+def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:
+    """An NCHW view of NHWC storage (channels_last strides; no copy)."""
+    return x.permute(0, 3, 1, 2)
+
+
+def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
+    """Decoder.forward (conv.py:96-100) on the HIP training kernels; ``order`` lists
+    (sequence name, index, upsample-after) as autograd_path.DECODER_ORDER."""
+    x = nchw_to_nhwc(x_nchw.float())
+    for seq, idx, up in order:
+        x = conv3x3(x, getattr(dec, seq)[idx].conv.conv, "reflect", relu=True)
+        if up:
+            x = Upsample2xFn.apply(x)
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, torch.Tensor]:
+    """VGG19.forward (vgg19.py:42-70) on the HIP kernels: relu1_1 .. relu5_1 as NCHW views of
+    NHWC storage."""
+    x = VggInputFn.apply(img)
+    feats = {}
+    for s, (a, b) in enumerate(slices, start=1):
+        seq = getattr(vgg, f"slice{s}")
+        for i in range(a, b):
+            if i in convs:
+                x = conv3x3(x, getattr(seq, str(i)), "zero", relu=True)
+            elif i in pools:
+                x = MaxPool2Fn.apply(x)
+            # ReLU modules are fused into the conv epilogue
+        feats[f"relu{s}_1"] = nhwc_to_nchw(x)
+    return feats

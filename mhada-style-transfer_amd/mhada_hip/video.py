@@ -2,6 +2,8 @@
 
 * ``warp(x, flo, padding_mode)`` — ``utilities.warp`` (utilities.py:100-118);
 * ``flow_warp_mask(flo01, flo10, padding_mode, threshold)`` — utilities.py:121-151;
+* ``cv2_to_tensor(img, resize)`` — utilities.py:43-52 (BGR->RGB, INTER_AREA, toTensor255) as one
+  HIP pass over the u8 frame in device memory (csrc/ingest.hip);
 * ``warping_error(cs1, cs2, flow, mask)`` — the per-frame optical-flow metric of
   exps_sintel.py:101-109 (sum(mask * |cs2 - warp(cs1, flow)|) / (C*H*W));
 * ``VideoStylizer`` — the infer_video.py:58-92 loop: the style is encoded once and, through the
@@ -25,6 +27,21 @@ def warp(x: torch.Tensor, flo: torch.Tensor, padding_mode: str = "zeros") -> tor
     if torch.is_grad_enabled() and (x.requires_grad or flo.requires_grad):
         return losses.warp(x, flo, padding_mode)
     return ops.warp(x, flo, padding_mode)
+
+
+def cv2_to_tensor(img, resize: Optional[tuple] = None, device: Optional[torch.device] = None) -> torch.Tensor:
+    """utilities.cv2_to_tensor: ``img`` is a cv2 BGR u8 frame (H, W, 3) — a numpy array (uploaded
+    through pinned memory to ``device``, default the current ROCm device) or a uint8 device
+    tensor; ``resize`` = (width, height) as cv2.resize takes it.  Returns the fp32 (3, h, w)
+    tensor in [0, 255] on the device (the reference returns it on the CPU and moves it with
+    .to(device) at infer_video.py:81)."""
+    if not isinstance(img, torch.Tensor):
+        t = torch.from_numpy(img)
+        if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:
+            raise ValueError("cv2_to_tensor expects a uint8 (H, W, 3) BGR frame")
+        img = t.pin_memory().to(device or torch.device("cuda", torch.cuda.current_device()), non_blocking=True)
+    out_hw = None if resize is None else (int(resize[1]), int(resize[0]))
+    return ops.frame_ingest(img, out_hw, bgr=True)[0]
 
 
 def flow_warp_mask(flo01: torch.Tensor, flo10: torch.Tensor, padding_mode: str = "zeros",

@@ -463,3 +463,38 @@ def warping_error(cs1: np.ndarray, cs2: np.ndarray, flow: np.ndarray, mask: np.n
     B, C, H, W = cs1.shape
     m = mask.reshape(B, 1, H, W)
     return (np.abs(cs2.astype(np.float64) - w) * m).reshape(B, -1).sum(axis=1) / (C * H * W)
+
+
+# --------------------------------------------------------------------------------------
+# video frame ingest (utilities.py:43-52 cv2_to_tensor, utilities.py:11-16 toTensor255)
+# --------------------------------------------------------------------------------------
+def resize_area(img: np.ndarray, out_w: int, out_h: int, dtype=np.float64) -> np.ndarray:
+    """cv2.resize(img, (out_w, out_h), interpolation=cv2.INTER_AREA) for a downscale, restated
+    from OpenCV's published definition (cv2 is not installed here: PARITY UNPINNED): each output
+    pixel is the overlap-weighted mean of the input over its box [x*sx, (x+1)*sx) x [y*sy,
+    (y+1)*sy) (sx = W/out_w, sy = H/out_h), rounded to u8 half-to-even (cvRound).  Returns the
+    unrounded means in ``dtype`` (callers round; tests use the distance to the rounding tie)."""
+    H, W = img.shape[:2]
+    sx, sy = W / out_w, H / out_h
+
+    def weights(n_out, n_in, s):
+        m = np.zeros((n_out, n_in), dtype=np.float64)
+        for o in range(n_out):
+            a, b = o * s, min((o + 1) * s, n_in)
+            for i in range(int(np.floor(a)), min(int(np.ceil(b)), n_in)):
+                m[o, i] = min(i + 1, b) - max(i, a)
+        return m / m.sum(1, keepdims=True)
+    wy, wx = weights(out_h, H, sy), weights(out_w, W, sx)
+    x = img.astype(np.float64)
+    t = np.tensordot(wy, x, axes=([1], [0]))                    # (out_h, W, C)
+    return np.tensordot(t, wx, axes=([1], [1])).transpose(0, 2, 1).astype(dtype)  # (out_h, out_w, C)
+
+
+def cv2_to_tensor(img_bgr: np.ndarray, resize=None) -> np.ndarray:
+    """utilities.cv2_to_tensor (utilities.py:43-52): BGR->RGB, optional INTER_AREA resize
+    (resize = (width, height)), toTensor255 -> (3, h, w) float32 in [0, 255]."""
+    rgb = img_bgr[..., ::-1]
+    if resize is not None:
+        rgb = np.clip(np.rint(resize_area(rgb, int(resize[0]), int(resize[1]))), 0, 255).astype(np.uint8)
+    t = rgb.transpose(2, 0, 1).astype(np.float32)
+    return (t / np.float32(255)) * np.float32(255)  # ToTensor, then .mul(255)

@@ -88,7 +88,7 @@ def test_library_loads_and_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
-    assert lib.mhada_abi_version() == 3
+    assert lib.mhada_abi_version() == _lib.ABI_VERSION
 
 
 def test_tuning_table_read_once_and_settable():

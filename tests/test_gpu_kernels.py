@@ -29,7 +29,7 @@ TOL = {torch.float32: 2e-5, torch.bfloat16: 1e-2}
 
 def test_library_is_the_native_one():
     lib = _lib.load()
-    assert lib.mhada_abi_version() == 3
+    assert lib.mhada_abi_version() == _lib.ABI_VERSION
     assert _lib.LIB_PATH.endswith("libmhada_hip.so")
 
 

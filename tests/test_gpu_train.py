@@ -54,8 +54,11 @@ def test_rccl_data_parallel_grads_match_single_gpu():
                           for n, p in m.named_parameters() if p.grad is not None})
             tr.close()
         assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 300
+        # same kernels, same inputs; vendor-library (MIOpen/hipBLASLt) reduction order may differ
+        # run to run, so near-zero gradients (K biases: zero in exact arithmetic) are held to an
+        # absolute floor of 1e-5 of the largest gradient
+        gmax = max(float(g.abs().max()) for g in grads[1].values())
         for n in grads[1]:
-            # same kernels, same inputs; only vendor-library (MIOpen/hipBLASLt) reduction order may differ
-            torch.testing.assert_close(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-5 * float(grads[1][n].abs().max()))
+            torch.testing.assert_close(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-5 * gmax)
     finally:
         dist.destroy_process_group()

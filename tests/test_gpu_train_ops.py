@@ -1,0 +1,227 @@
+"""Training-path HIP kernels (csrc/train_ops.hip + the CONV3X3_ZERO gather of gemm.hip) through
+their autograd Functions (mhada_hip/train_fns.py), each against PyTorch fp64 autograd of the same
+reference expression: the decoder's ReflectionPad2d(1) + conv3x3 + ReLU (conv.py:23-45), VGG19's
+zero-padded conv + ReLU and MaxPool2d(2) (vgg19.py, cfg E), the bilinear x2 upsample (conv.py:71)
+and imageNet1k_normalize (vgg19.py:6-12).  fp32 kernels vs fp64: relative L2 < 1e-5."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from mhada_hip import ops, train_fns
+from mhada_hip._lib import A_ROWS
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 576, 5000), (512, 2048, 333), (3, 128, 700), (130, 260, 64)])
+def test_gemm_tn_rows(M, N, K):
+    a = rnd(K, M, seed=1)
+    b = rnd(K, N, seed=2)
+    c = ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS)
+    ref = a.double().T @ b.double()
+    assert rel(c, ref) < 1e-5
+    # deterministic: same bits on a second call
+    assert torch.equal(c, ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS))
+
+
+@pytest.mark.parametrize("rows,C", [(100000, 64), (37, 2048), (4096, 3 * 4)])
+def test_colsum(rows, C):
+    x = rnd(rows, C, seed=3)
+    assert rel(ops.colsum(x), x.double().sum(0)) < 1e-6
+
+
+def _conv_ref(x_nhwc, w, b, pad_mode, relu):
+    x = x_nhwc.permute(0, 3, 1, 2)
+    if pad_mode == "reflect":
+        y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w, b)
+    else:
+        y = F.conv2d(x, w, b, padding=1)
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("pad_mode", ["reflect", "zero"])
+@pytest.mark.parametrize("B,H,W,Ci,Co,cx", [(2, 9, 13, 64, 64, 64), (1, 16, 16, 128, 256, 128), (2, 8, 6, 3, 64, 32),
+                                          (1, 20, 17, 64, 3, 64), (2, 3, 5, 32, 32, 32), (1, 32, 32, 512, 256, 512)])
+def test_conv3x3_fwd_bwd(pad_mode, B, H, W, Ci, Co, cx):
+    x = rnd(B, H, W, cx, seed=H * W)
+    if cx > Ci:
+        x[..., Ci:] = 0  # VGG's padded input channels are zero
+    w = rnd(Co, Ci, 3, 3, seed=2, scale=(9 * Ci) ** -0.5)
+    b = rnd(Co, seed=3, scale=0.1)
+    gy = rnd(B, H, W, Co, seed=4)
+    conv = torch.nn.Conv2d(Ci, Co, 3).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+        conv.bias.copy_(b)
+    xg = x.clone().requires_grad_(True)
+    y = train_fns.conv3x3(xg, conv, pad_mode, relu=True)
+    y.backward(gy)
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True)
+    ref = _conv_ref(x64, w64, b64, pad_mode, True)
+    ref.backward(gy.double())
+    assert rel(y, ref) < 1e-5
+    assert rel(xg.grad[..., :Ci], x64.grad[..., :Ci]) < 1e-5
+    assert rel(conv.weight.grad, w64.grad) < 1e-5
+    assert rel(conv.bias.grad, b64.grad) < 1e-5
+
+
+def test_maxpool2_fwd_bwd_with_ties():
+    # post-ReLU activations: many zeros, so the first-maximum rule decides most windows
+    x = F.relu(rnd(2, 16, 18, 64, seed=5))
+    x[0, 0:2, 0:2, :] = 1.5  # a window of four equal maxima
+    gy = rnd(2, 8, 9, 64, seed=6)
+    xg = x.clone().requires_grad_(True)
+    y = train_fns.MaxPool2Fn.apply(xg)
+    y.backward(gy)
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    yr.backward(gy.permute(0, 3, 1, 2))
+    assert torch.equal(y, yr.permute(0, 2, 3, 1))
+    assert torch.equal(xg.grad, xr.grad.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("H,W", [(8, 8), (5, 7), (1, 3), (64, 32)])
+def test_upsample2x_adjoint(H, W):
+    x = rnd(2, H, W, 64, seed=7)
+    gy = rnd(2, 2 * H, 2 * W, 64, seed=8)
+    xg = x.clone().requires_grad_(True)
+    y = train_fns.Upsample2xFn.apply(xg)
+    y.backward(gy)
+    x64 = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    r = F.interpolate(x64, scale_factor=2, mode="bilinear", align_corners=False)
+    r.backward(gy.double().permute(0, 3, 1, 2))
+    assert rel(y, r.permute(0, 2, 3, 1)) < 1e-6
+    assert rel(xg.grad, x64.grad.permute(0, 2, 3, 1)) < 1e-6
+
+
+def test_vgg_input_and_adjoint():
+    img = (torch.rand(2, 3, 12, 10, generator=torch.Generator().manual_seed(9)) * 255).to(DEV).requires_grad_(True)
+    out = train_fns.VggInputFn.apply(img)
+    assert out.shape == (2, 12, 10, 32) and torch.all(out[..., 3:] == 0)
+    mean = img.new_tensor([0.485, 0.456, 0.406]).view(-1, 1, 1)
+    std = img.new_tensor([0.229, 0.224, 0.225]).view(-1, 1, 1)
+    ref = (img.detach() / 255.0 - mean) / std  # vgg19.py:11, same fp32 ops
+    assert torch.equal(out[..., :3], ref.permute(0, 2, 3, 1))
+    g = rnd(2, 12, 10, 32, seed=10)
+    out.backward(g)
+    img64 = img.detach().double().requires_grad_(True)
+    ((img64 / 255.0 - mean.double()) / std.double()).backward(g[..., :3].permute(0, 3, 1, 2).double())
+    assert rel(img.grad, img64.grad) < 1e-6
+
+
+def test_vgg19_and_decoder_modules_against_aten_autograd():
+    """The HIP training forwards of network.VGG19 and the Decoder (with gradients to the input
+    image / features and the decoder parameters) against the same modules evaluated by aten."""
+    import network
+    from mhada_hip import autograd_path
+    from mhada_hip.recipe import load_recipe, recipe_state_dict
+    vgg = load_recipe(network.VGG19(), "vgg").to(DEV)
+    img = (torch.rand(2, 3, 48, 40, generator=torch.Generator().manual_seed(11)) * 255).to(DEV)
+    x1 = img.clone().requires_grad_(True)
+    f1 = vgg(x1)
+    x2 = img.double().cpu().requires_grad_(True)  # aten fp64 reference on the CPU
+    vgg64 = load_recipe(network.VGG19(), "vgg").double()
+    f2 = {}
+    h = autograd_path.imagenet_normalize(x2).double()
+    for i in range(1, 6):
+        h = getattr(vgg64, f"slice{i}")(h)
+        f2[f"relu{i}_1"] = h
+    loss1 = sum((f1[k] * (j + 1)).square().mean() for j, k in enumerate(sorted(f1)))
+    loss2 = sum((f2[k] * (j + 1)).square().mean() for j, k in enumerate(sorted(f2)))
+    for k in f1:
+        assert rel(f1[k].cpu(), f2[k]) < 1e-5, k
+    loss1.backward()
+    loss2.backward()
+    assert rel(x1.grad.cpu(), x2.grad) < 1e-4
+
+    dec = network.Decoder()
+    sd = recipe_state_dict("dec", {"decoder." + k: tuple(v.shape) for k, v in dec.state_dict().items()})
+    dec.load_state_dict({k[len("decoder."):]: v for k, v in sd.items()}, strict=True)
+    dec64 = network.Decoder().double()  # aten fp64 reference on the CPU
+    dec64.load_state_dict(dec.state_dict())
+    dec = dec.to(DEV)
+    feat = rnd(2, 512, 6, 5, seed=12).requires_grad_(True)
+    y1 = autograd_path.decoder_forward(dec, feat)
+    feat64 = feat.detach().double().cpu().requires_grad_(True)
+    y2 = autograd_path.decoder_forward(dec64, feat64)
+    assert rel(y1.cpu(), y2) < 1e-5
+    g = rnd(*y1.shape, seed=13)
+    y1.backward(g)
+    y2.backward(g.double().cpu())
+    assert rel(feat.grad.cpu(), feat64.grad) < 1e-5
+    for (n, p), (_, p64) in zip(dec.named_parameters(), dec64.named_parameters()):
+        assert rel(p.grad.cpu(), p64.grad) < 1e-5, n
+
+
+# ---- AdaAttnForLoss (adaDecoder.py:52-81) on the wide-head HIP kernel (csrc/loss_attn.hip) -------
+def _loss_attn_ref(c_x, s_x, c_1x, s_1x, act):
+    """adaDecoder.py:52-81 in fp64 (the reference expression, unchunked)."""
+    inorm = lambda t: F.instance_norm(t.double(), eps=1e-5)  # noqa: E731
+    b, _, h, w = c_1x.shape
+    q = inorm(c_1x).reshape(b, -1, h * w).permute(0, 2, 1)
+    k = inorm(s_1x).reshape(b, s_1x.shape[1], -1)
+    v = s_x.double().reshape(b, s_x.shape[1], -1).permute(0, 2, 1)
+    if act == "softmax":
+        a = torch.softmax(torch.bmm(q, k), dim=-1)
+    else:
+        s = torch.bmm(q, k) / torch.bmm(q.norm(dim=-1, keepdim=True), k.norm(dim=1, keepdim=True)) + 1
+        a = s / s.sum(dim=-1, keepdim=True)
+    m = torch.bmm(a, v)
+    sd = torch.sqrt((torch.bmm(a, v * v) - m * m).clamp(min=1e-6))
+    bc, _, hc, wc = c_x.shape
+    m = m.reshape(bc, hc, wc, -1).permute(0, 3, 1, 2)
+    sd = sd.reshape(bc, hc, wc, -1).permute(0, 3, 1, 2)
+    return sd * inorm(c_x) + m
+
+
+@pytest.mark.parametrize("act", ["softmax", "cosine"])
+@pytest.mark.parametrize("B,dqk,dv,hc,wc,hs,ws", [(2, 448, 256, 16, 16, 16, 16), (1, 960, 512, 8, 8, 8, 8),
+                                                   (2, 1472, 512, 4, 4, 4, 4), (1, 448, 256, 9, 7, 5, 11),
+                                                   (1, 96, 64, 20, 3, 6, 6)])
+def test_loss_attn_against_fp64(act, B, dqk, dv, hc, wc, hs, ws):
+    """The three local-feature-loss shapes (relu3/4/5 channel counts) plus ragged token counts;
+    VGG-like non-negative features (post-ReLU), fp32 kernel vs fp64 reference: 1e-4 relative."""
+    from mhada_hip import autograd_path
+    c_x = F.relu(rnd(B, dv, hc, wc, seed=1))
+    s_x = F.relu(rnd(B, dv, hs, ws, seed=2))
+    c_1x = F.relu(rnd(B, dqk, hc, wc, seed=3))
+    s_1x = F.relu(rnd(B, dqk, hs, ws, seed=4))
+    with torch.no_grad():
+        y = autograd_path.ada_attn_for_loss(c_x, s_x, c_1x, s_1x, act)
+    ref = _loss_attn_ref(c_x, s_x, c_1x, s_1x, act)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-4
+
+
+def test_loss_attn_matches_reference_golden():
+    """lf_target4 of the train golden (reference AdaAttnForLoss on reference-VGG features of the
+    golden's content/style): the HIP VGG19 features feed the HIP loss attention."""
+    import network
+    from conftest import load_golden
+    from mhada_hip import losses as L
+    from mhada_hip.recipe import load_recipe, seeded_image
+    g = load_golden("train_64_b2")
+    vgg = load_recipe(network.VGG19(), "vgg").to(DEV)
+    c = seeded_image(2, 64, 64, int(g["content_seed"])).to(DEV)
+    s = seeded_image(2, 64, 64, int(g["style_seed"])).to(DEV)
+    with torch.no_grad():
+        fc, fs = vgg(c), vgg(s)
+        t4 = network.AdaAttnForLoss(512, 960)(fc["relu4_1"], fs["relu4_1"], L.feature_down_sample(fc, 4),
+                                               L.feature_down_sample(fs, 4))
+    assert torch.allclose(t4.cpu(), torch.from_numpy(g["lf_target4"]), rtol=1e-4, atol=1e-4)
