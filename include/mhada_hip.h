@@ -205,7 +205,9 @@ int mhada_warp_l1(const float* cs1, const float* cs2, const float* flow, const f
  *   conv wgrad: A = dY' [pixels][Cout] (lda = Cout), B = im2col of the layer input in b_mode
  *     MHADA_A_CONV3X3 (reflect pad 1) or MHADA_A_CONV3X3_ZERO (zero pad `pad`): k = output pixel,
  *     n = tap*Cin + ci (N = 9*Cin; img_* = the NHWC input), C = dW [Cout][ky][kx][Cin];
- *   linear dW = dY^T X: A = dY [rows][out], B = X [rows][in] (b_mode MHADA_A_ROWS, ldb).
+ *   linear dW = dY^T X: A = dY [rows][out], B = X [rows][in] (b_mode MHADA_A_ROWS, ldb);
+ *   patch-embedding dW (vit.py:109): b_mode MHADA_A_PATCH8, B = the NCHW fp32 image (img_*),
+ *     k = token, n = c*64 + ky*8 + kx (N = 64*img_c).
  * Replaces the weight-gradient half of conv2d / addmm backward (conv.py:27-32, vgg19 convs,
  * vit.py:49-63 Linear layers).  K is split into partial slabs in `work` (>= M*N floats; up to
  * mhada_gemm_tn_splits(M,N,K)*M*N are used) summed in a fixed order: deterministic.  N % 4 == 0. */

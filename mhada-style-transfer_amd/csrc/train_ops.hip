@@ -40,7 +40,9 @@ constexpr int kTnBM = 128, kTnBN = 128, kTnBK = 32;
 
 MHADA_DEV int tn_reflect(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
-// BMODE: MHADA_A_ROWS, MHADA_A_CONV3X3 (reflect pad 1), MHADA_A_CONV3X3_ZERO (zero pad `pad`).
+// BMODE: MHADA_A_ROWS, MHADA_A_CONV3X3 (reflect pad 1), MHADA_A_CONV3X3_ZERO (zero pad `pad`),
+// MHADA_A_PATCH8 (k = token (b, py, px) of the 8x8 / stride-8 patch grid, n = c*64 + ky*8 + kx
+// of an NCHW image [B][img_c][img_h][img_w]: the patch-embedding weight gradient).
 // VEC_A: A rows are 16-B aligned with M % 4 == 0 (else element loads, e.g. the 3-channel layer).
 template <int BMODE, bool VEC_A>
 __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
@@ -59,7 +61,12 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
   // B gather: the column quad of this thread is fixed for the whole K loop (tap, channel)
   int tap_dy = 0, tap_dx = 0, ci = 0;
   const bool bcol_ok = n0 + col < p.N;  // N % 4 == 0 for every B mode (checked on the host)
-  if constexpr (BMODE != MHADA_A_ROWS) {
+  if constexpr (BMODE == MHADA_A_PATCH8) {
+    const int n = min(n0 + col, p.N - 4);
+    ci = n >> 6;                  // image channel
+    tap_dy = (n >> 3) & 7;        // ky
+    tap_dx = n & 7;               // kx (0 or 4: a quad stays inside one patch row)
+  } else if constexpr (BMODE != MHADA_A_ROWS) {
     const int n = min(n0 + col, p.N - 4);
     const int tap = n / p.img_c;
     ci = n - tap * p.img_c;
@@ -83,6 +90,16 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       // B
       if constexpr (BMODE == MHADA_A_ROWS) {
         rb[i] = (kok && bcol_ok) ? *reinterpret_cast<const f32x4*>(p.b + (long long)k * p.ldb + n0 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else if constexpr (BMODE == MHADA_A_PATCH8) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (kok && bcol_ok) {
+          const int gw = p.img_w / 8, gh = p.img_h / 8;
+          const int bb = k / (gh * gw), rem = k - bb * (gh * gw);
+          const int py = rem / gw, px = rem - py * gw;
+          v = *reinterpret_cast<const f32x4*>(p.b + (((long long)bb * p.img_c + ci) * p.img_h + py * 8 + tap_dy) * p.img_w +
+                                             px * 8 + tap_dx);
+        }
+        rb[i] = v;
       } else {
         bool ok = kok && bcol_ok;
         long long src = 0;
@@ -413,6 +430,11 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
     case MHADA_A_ROWS:
       if (a->ldb % 4) return fail("mhada_gemm_tn: ldb must be a multiple of 4");
       break;
+    case MHADA_A_PATCH8:
+      if (a->img_w % 8 || a->img_h % 8 || a->N != 64 * a->img_c) return fail("mhada_gemm_tn: PATCH8 needs H, W % 8 == 0, N == 64*C");
+      if (a->K % ((a->img_h / 8) * (a->img_w / 8))) return fail("mhada_gemm_tn: PATCH8 needs K == batch*(H/8)*(W/8)");
+      p.img_c = a->img_c; p.img_h = a->img_h; p.img_w = a->img_w;
+      break;
     case MHADA_A_CONV3X3:
     case MHADA_A_CONV3X3_ZERO: {
       const int pad = a->b_mode == MHADA_A_CONV3X3 ? 1 : (a->pad ? a->pad : 1);
@@ -445,6 +467,7 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   } while (0)
   if (a->b_mode == MHADA_A_ROWS) TN_LAUNCH(MHADA_A_ROWS);
   else if (a->b_mode == MHADA_A_CONV3X3) TN_LAUNCH(MHADA_A_CONV3X3);
+  else if (a->b_mode == MHADA_A_PATCH8) TN_LAUNCH(MHADA_A_PATCH8);
   else TN_LAUNCH(MHADA_A_CONV3X3_ZERO);
 #undef TN_LAUNCH
   if (int rc = check_launch("mhada_gemm_tn")) return rc;

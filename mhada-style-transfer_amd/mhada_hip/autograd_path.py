@@ -35,9 +35,48 @@ def needs_grad(module: torch.nn.Module, *xs) -> bool:
     return any(p.requires_grad for p in module.parameters())
 
 
+def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
+    """VisionTransformer.forward on the HIP training kernels (train_fns): patch embedding and
+    every Linear (MHA in/out projections, MLP with fused ReLU) on mhada_gemm forward and
+    mhada_gemm / mhada_gemm_tn / mhada_colsum backward; LayerNorm, the pos-embed interpolation and
+    the batch-axis softmax (L = B <= 8 keys per token) stay aten."""
+    from . import train_fns
+    B, _, H, W = x.shape
+    p = vit.patch_size
+    h, w = H // p, W // p
+    N = h * w
+    t = train_fns.PatchEmbedFn.apply(x, vit.patch_embedding.conv_proj.weight, vit.patch_embedding.conv_proj.bias)
+    C = t.shape[2]
+    if vit.pos_embedding is not None:
+        pe = vit.pos_embedding.pos_embed
+        if (h, w) != tuple(pe.shape[2:]):
+            pe = F.interpolate(pe, size=(h, w), mode="bilinear", align_corners=False)
+        t = t + pe.reshape(1, C, N).permute(0, 2, 1)
+    outs = []
+    for blk in vit.encoder:
+        att = blk.attention
+        heads = att.num_heads
+        d = C // heads
+        y = blk.ln1(t).reshape(B * N, C)
+        qkv = train_fns.linear(y, att.in_proj_weight, att.in_proj_bias)
+        q, k, v = (z.reshape(B, N, heads, d).permute(1, 2, 0, 3) for z in qkv.split(C, dim=1))  # (N, H, L=B, d)
+        a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (d ** -0.5), dim=-1)
+        o = torch.matmul(a, v).permute(2, 0, 1, 3).reshape(B * N, C)
+        t = t + train_fns.linear(o, att.out_proj.weight, att.out_proj.bias).view(B, N, C)
+        y2 = blk.ln2(t).reshape(B * N, C)
+        m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True)
+        t = t + train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias).view(B, N, C)
+        outs.append(t.permute(0, 2, 1).reshape(B, C, h, w))
+    return outs
+
+
 def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
     """VisionTransformer.forward (vit.py:148-169); the MHA keeps batch_first=False on a
-    (B, N, C) tensor, i.e. attends over the batch axis exactly as the reference."""
+    (B, N, C) tensor, i.e. attends over the batch axis exactly as the reference.  On a ROCm
+    device the HIP training kernels run it (_vit_forward_hip); the CPU uses aten."""
+    if x.is_cuda and vit.patch_size == 8 and not x.requires_grad and \
+            isinstance(vit.encoder[0].mlp[1], torch.nn.ReLU) and vit.encoder[0].attention.in_proj_weight is not None:
+        return _vit_forward_hip(vit, x)
     B, _, H, W = x.shape
     p = vit.patch_size
     h, w = H // p, W // p
@@ -133,6 +172,11 @@ def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tens
     vmu = v.mean(dim=1, keepdim=True)
     x = _heads_rows(F.instance_norm(fcs), H)
     o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
+    if fc.is_cuda:  # out_conv (1x1) as a token GEMM on the HIP kernels
+        from . import train_fns
+        rows = o.reshape(B, H, h * w, C // H).permute(0, 2, 1, 3).reshape(B * h * w, C)
+        y = train_fns.linear(rows, blk.out_conv.weight.view(C, C), blk.out_conv.bias)
+        return y.view(B, h, w, C).permute(0, 3, 1, 2)
     o = o.reshape(B, H, h * w, C // H).transpose(2, 3).reshape(B, C, h, w)
     return blk.out_conv(o)
 

@@ -10,6 +10,11 @@ the reference, and runs its forward and backward through libmhada_hip.so:
   backward: ReLU mask (mhada_relu_bwd), input gradient = the conv of dY with the flipped,
   transposed weights (zero pad 1, or the full correlation + mhada_reflect_fold for the reflect
   pad), weight gradient = mhada_gemm_tn over the im2col of the input, bias = mhada_colsum.
+* ``linear`` — nn.Linear / the 1x1 out_conv on token rows (vit.py:49-63 MHA projections and MLP,
+  adaDecoder.py:152,205), optional fused ReLU: forward mhada_gemm; backward dX = dY W (mhada_gemm
+  with W^T), dW = dY^T X (mhada_gemm_tn), db = mhada_colsum.
+* ``patch_embed`` — the 8x8 / stride-8 patch conv (vit.py:105-117): forward mhada_gemm PATCH8,
+  weight gradient mhada_gemm_tn PATCH8 (the input image needs no gradient in training).
 * ``maxpool2``, ``upsample2x`` (conv.py:71), ``vgg_input`` (vgg19.py:6-12) and their adjoints.
 """
 from __future__ import annotations
@@ -20,7 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
-from ._lib import A_CONV3X3, A_CONV3X3_ZERO
+from ._lib import A_CONV3X3, A_CONV3X3_ZERO, A_PATCH8, A_ROWS
 
 F32 = torch.float32
 
@@ -101,11 +106,73 @@ class Conv3x3Fn(torch.autograd.Function):
                                                   pad=2))
         if ctx.needs_input_grad[1]:
             mode = A_CONV3X3 if ctx.pad_mode == "reflect" else A_CONV3X3_ZERO
-            dw = ops.gemm_tn(g, x, M=co, N=9 * cx, K=B * H * W, lda=ldc, b_mode=mode, img=(cx, H, W), pad=1)
-            gw = dw.view(co, 3, 3, cx)[..., :weight.shape[1]].permute(0, 3, 1, 2).contiguous()
+            # M = ldc (the zero-padded channel columns of g) keeps the vectorised A loads
+            dw = ops.gemm_tn(g, x, M=ldc, N=9 * cx, K=B * H * W, lda=ldc, b_mode=mode, img=(cx, H, W), pad=1)
+            gw = dw.view(ldc, 3, 3, cx)[:co, :, :, :weight.shape[1]].permute(0, 3, 1, 2).contiguous()
         if ctx.needs_input_grad[2]:
             gb = ops.colsum(g)[:co].contiguous()
         return gx, gw, gb, None, None
+
+
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear layout)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool):
+        x = x.contiguous()
+        y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu)
+        ctx.save_for_backward(x, weight, y if relu else None)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        g = gy.contiguous()
+        if ctx.relu:
+            g = ops.relu_bwd(g, y)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = ops.linear(g, weight.detach().t().contiguous(), None, F32)
+        if ctx.needs_input_grad[1]:
+            M, N = g.shape
+            gw = ops.gemm_tn(g, x, M=N, N=x.shape[1], K=M, lda=N, ldb=x.shape[1], b_mode=A_ROWS)
+        if ctx.needs_input_grad[2]:
+            gb = ops.colsum(g)
+        return gx, gw, gb, None
+
+
+def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bool = False) -> torch.Tensor:
+    return LinearFn.apply(x2d, weight, bias, relu)
+
+
+class PatchEmbedFn(torch.autograd.Function):
+    """PatchEmbedding conv 8x8 / stride 8 (vit.py:105-117): img (B, 3, H, W) fp32 -> tokens
+    [B][N][C]; weight (C, 3, 8, 8).  Gradients for the weight and bias only."""
+
+    @staticmethod
+    def forward(ctx, img, weight, bias):
+        img = img.float().contiguous()
+        C = weight.shape[0]
+        y = ops.patch_embed(img, weight.detach().reshape(C, -1).contiguous(), bias.detach().float().contiguous(), None)
+        ctx.save_for_backward(img, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        img, weight = ctx.saved_tensors
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("PatchEmbedFn: no input-image gradient (training inputs are data)")
+        B, Ci, H, W = img.shape
+        C = weight.shape[0]
+        g = gy.contiguous().view(-1, C)
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            gw = ops.gemm_tn(g, img, M=C, N=64 * Ci, K=g.shape[0], lda=C, b_mode=A_PATCH8,
+                             img=(Ci, H, W)).view_as(weight)
+        if ctx.needs_input_grad[2]:
+            gb = ops.colsum(g)
+        return None, gw, gb
 
 
 class MaxPool2Fn(torch.autograd.Function):
