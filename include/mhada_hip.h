@@ -222,6 +222,11 @@ typedef struct mhada_gemm_tn_args {
 int mhada_gemm_tn_splits(int M, int N, int K);
 int mhada_gemm_tn(const mhada_gemm_tn_args* args, float* work, long long work_floats, mhada_stream_t stream);
 
+/* Backward of the batch-axis MHA core (vit.py:48,59; forward mhada_vit_batch_attn), fp32:
+ * qkv [L][ntok][3C] (the forward input), dout [L][ntok][C] -> dqkv [L][ntok][3C]; L <= 8. */
+int mhada_vit_batch_attn_bwd(const float* qkv, const float* dout, float* dqkv, int L, int ntok, int heads,
+                             int head_dim, mhada_stream_t stream);
+
 /* Bias gradients: out[c] = sum_r x[r][c] (x [rows][C] fp32, C % 4 == 0); work >= C floats
  * (up to 1024*C used), fixed-order reduction. */
 int mhada_colsum(const float* x, float* out, long long rows, int C, float* work, long long work_floats,

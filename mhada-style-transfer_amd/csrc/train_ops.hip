@@ -36,7 +36,7 @@ struct TnP {
   int kchunk, tiles_n;
 };
 
-constexpr int kTnBM = 128, kTnBN = 128, kTnBK = 32;
+constexpr int kTnBN = 128, kTnBK = 32;
 
 MHADA_DEV int tn_reflect(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
@@ -44,16 +44,20 @@ MHADA_DEV int tn_reflect(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2
 // MHADA_A_PATCH8 (k = token (b, py, px) of the 8x8 / stride-8 patch grid, n = c*64 + ky*8 + kx
 // of an NCHW image [B][img_c][img_h][img_w]: the patch-embedding weight gradient).
 // VEC_A: A rows are 16-B aligned with M % 4 == 0 (else element loads, e.g. the 3-channel layer).
-template <int BMODE, bool VEC_A>
+// BM = 128 (M >= 128) or 64 (the 64-channel layers: no half-empty M tiles); waves 2 x 2, each
+// (BM/2) x 64 of the output.
+template <int BMODE, bool VEC_A, int BM>
 __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
-  __shared__ __attribute__((aligned(16))) float sA[2][kTnBK][kTnBM];
+  constexpr int TMW = BM / 64;   // 32-row MFMA blocks per wave
+  constexpr int ACH = BM / 32;   // A chunks (16 B) staged per thread per K-stage
+  __shared__ __attribute__((aligned(16))) float sA[2][kTnBK][BM];
   __shared__ __attribute__((aligned(16))) float sB[2][kTnBK][kTnBN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves of 64 x 64
   const int h = lane >> 5, r32 = lane & 31;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
-  const int m0 = tm * kTnBM, n0 = tn * kTnBN;
+  const int m0 = tm * BM, n0 = tn * kTnBN;
   const int kbeg = blockIdx.y * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
 
   // staging: chunk c = tid + 256 i (i < 4) -> tile row c >> 5 = (tid >> 5) + 8 i, 4 columns at 4 (c & 31)
@@ -73,20 +77,25 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
     tap_dy = tap / 3 - 1;
     tap_dx = tap - (tap / 3) * 3 - 1;
   }
-  f32x4 ra[4], rb[4];
+  f32x4 ra[ACH], rb[4];
   auto issue = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + row0 + 8 * i;
+    for (int i = 0; i < ACH; ++i) {  // A: chunk c = tid + 256 i -> row c / (BM/4), 4 columns at 4 (c % (BM/4))
+      const int c = tid + 256 * i;
+      const int k = k0 + c / (BM / 4);
+      const int m = m0 + 4 * (c % (BM / 4));
       const bool kok = k < kend;
-      // A
-      const int m = m0 + col;
       if constexpr (VEC_A) {
         ra[i] = (kok && m < p.M) ? *reinterpret_cast<const f32x4*>(p.a + (long long)k * p.lda + m) : f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ra[i][e] = (kok && m + e < p.M) ? p.a[(long long)k * p.lda + m + e] : 0.f;
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + row0 + 8 * i;
+      const bool kok = k < kend;
       // B
       if constexpr (BMODE == MHADA_A_ROWS) {
         rb[i] = (kok && bcol_ok) ? *reinterpret_cast<const f32x4*>(p.b + (long long)k * p.ldb + n0 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -124,15 +133,17 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
   };
   auto commit = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<f32x4*>(&sA[buf][row0 + 8 * i][col]) = ra[i];
-      *reinterpret_cast<f32x4*>(&sB[buf][row0 + 8 * i][col]) = rb[i];
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<f32x4*>(&sA[buf][c / (BM / 4)][4 * (c % (BM / 4))]) = ra[i];
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(&sB[buf][row0 + 8 * i][col]) = rb[i];
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[TMW][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TMW; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -150,15 +161,15 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
     if (more) issue(kbeg + (st + 1) * kTnBK);
 #pragma unroll
     for (int kk = 0; kk < kTnBK; kk += 2) {
-      float av[2], bv[2];
+      float av[TMW], bv[2];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) av[mi] = sA[buf][kk + h][wm * 64 + mi * 32 + r32];
+      for (int mi = 0; mi < TMW; ++mi) av[mi] = sA[buf][kk + h][wm * (BM / 2) + mi * 32 + r32];
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) bv[ni] = sB[buf][kk + h][wn * 64 + ni * 32 + r32];
       // D[n][m]: B is the MFMA A operand, so the lane owns output row m = ... + r32 and the
       // registers 4g..4g+3 hold 4 consecutive columns n (16-B slab stores)
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < TMW; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[ni], av[mi], acc[mi][ni], 0, 0, 0);
     }
@@ -168,8 +179,8 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
 
   float* slab = p.slab + (long long)blockIdx.y * p.M * p.N;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    const int m = m0 + wm * 64 + mi * 32 + r32;
+  for (int mi = 0; mi < TMW; ++mi) {
+    const int m = m0 + wm * (BM / 2) + mi * 32 + r32;
     if (m >= p.M) continue;
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
@@ -204,8 +215,72 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
   }
 }
 
+// M <= 4 (the 3-channel last decoder layer's weight gradient): VALU, bandwidth-bound on the B
+// gather.  Block = 256 threads over (row group, column quad); each thread keeps 4 x 4 sums
+// (m, 4 columns), the row groups are summed in LDS in a fixed order, one slab row per block.
+template <int BMODE>
+__global__ void __launch_bounds__(256) tn_skinny_kernel(const TnP p) {
+  __shared__ f32x4 part[256][4];
+  const int tpc = min(p.N / 4 - (int)blockIdx.y * 256, 256);
+  const int groups = 256 / tpc;
+  const int t = threadIdx.x, qd = t % tpc, g = t / tpc;
+  const int n = 4 * ((int)blockIdx.y * 256 + qd);
+  int tap_dy = 0, tap_dx = 0, ci = 0;
+  if constexpr (BMODE != MHADA_A_ROWS) {
+    const int tap = n / p.img_c;
+    ci = n - tap * p.img_c;
+    tap_dy = tap / 3 - 1;
+    tap_dx = tap - (tap / 3) * 3 - 1;
+  }
+  const long long k0 = (long long)blockIdx.x * p.kchunk, k1 = std::min<long long>(p.K, k0 + p.kchunk);
+  f32x4 acc[4] = {};
+  if (g < groups) {
+    for (long long k = k0 + g; k < k1; k += groups) {
+      f32x4 bv;
+      if constexpr (BMODE == MHADA_A_ROWS) {
+        bv = *reinterpret_cast<const f32x4*>(p.b + k * p.ldb + n);
+      } else {
+        const int hw = p.out_h * p.out_w;
+        const int bb = (int)(k / hw), rem = (int)(k - (long long)bb * hw);
+        const int oy = rem / p.out_w, ox = rem - oy * p.out_w;
+        int Y, X;
+        bool ok = true;
+        if constexpr (BMODE == MHADA_A_CONV3X3_ZERO) {
+          Y = oy + tap_dy + 1 - p.pad;
+          X = ox + tap_dx + 1 - p.pad;
+          ok = Y >= 0 && Y < p.img_h && X >= 0 && X < p.img_w;
+        } else {
+          Y = tn_reflect(oy + tap_dy, p.img_h);
+          X = tn_reflect(ox + tap_dx, p.img_w);
+        }
+        bv = ok ? *reinterpret_cast<const f32x4*>(p.b + (((long long)bb * p.img_h + Y) * p.img_w + X) * p.img_c + ci)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float av = m < p.M ? p.a[k * p.lda + m] : 0.f;
+        acc[m] += av * bv;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) part[t][m] = acc[m];
+  __syncthreads();
+  if (t < tpc) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      f32x4 s4 = part[t][m];
+      for (int j = 1; j < groups; ++j) s4 += part[j * tpc + t][m];
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.slab + ((long long)blockIdx.x * p.M + m) * p.N + n) = s4;
+    }
+  }
+}
+
+static int tn_bm(int M) { return M <= 64 ? 64 : 128; }
+
 int tn_splits(int M, int N, int K) {
-  const int tiles = ((M + kTnBM - 1) / kTnBM) * ((N + kTnBN - 1) / kTnBN);
+  if (M <= 4) return std::max(1, std::min(1024, K / 2048));
+  const int tiles = ((M + tn_bm(M) - 1) / tn_bm(M)) * ((N + kTnBN - 1) / kTnBN);
   const int target = 1024;  // blocks: 2 per CU resident, 2 waves of them
   int s = (target + tiles - 1) / tiles;
   const int maxs = (K + kTnBK * 8 - 1) / (kTnBK * 8);  // at least 8 K-stages per split
@@ -215,19 +290,27 @@ int tn_splits(int M, int N, int K) {
 // ======================================================================================
 // column sums (bias gradients): slab[chunk][c] = sum of rows in the chunk
 // ======================================================================================
+// block = 256 threads over (row group g, column quad q): tpc = min(C/4, 256) quads per row pass,
+// 256 / tpc row groups stride the chunk's rows; the groups are then summed in a fixed order in
+// LDS (deterministic).  gridDim.y covers C / 1024 column blocks when C > 1024.
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x, float* __restrict__ slab, long long rows,
                                                      int C, long long rows_per_chunk) {
-  const int c = 4 * (blockIdx.y * 256 + threadIdx.x);
-  if (c >= C) return;
+  __shared__ f32x4 part[256];
+  const int tpc = min(C / 4 - (int)blockIdx.y * 256, 256);  // column quads of this column block
+  const int groups = 256 / tpc;
+  const int t = threadIdx.x, q = t % tpc, g = t / tpc;
+  const int c = 4 * ((int)blockIdx.y * 256 + q);
   const long long r0 = (long long)blockIdx.x * rows_per_chunk, r1 = std::min(rows, r0 + rows_per_chunk);
-  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-  long long r = r0;
-  for (; r + 1 < r1; r += 2) {
-    a += *reinterpret_cast<const f32x4*>(x + r * C + c);
-    b += *reinterpret_cast<const f32x4*>(x + (r + 1) * C + c);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (g < groups)
+    for (long long r = r0 + g; r < r1; r += groups) a += *reinterpret_cast<const f32x4*>(x + r * C + c);
+  part[t] = a;
+  __syncthreads();
+  if (t < tpc) {
+    f32x4 s = part[t];
+    for (int k = 1; k < groups; ++k) s += part[k * tpc + t];
+    *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * C + c) = s;
   }
-  if (r < r1) a += *reinterpret_cast<const f32x4*>(x + r * C + c);
-  *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * C + c) = a + b;
 }
 
 // ======================================================================================
@@ -403,6 +486,86 @@ __global__ void __launch_bounds__(256) vgg_input_bwd_kernel(const float* __restr
   for (int c = 0; c < 3; ++c) dimg[(b * 3 + c) * plane + r] = dout[pix * Cp + c] / c_in_std[c] / 255.0f;
 }
 
+// Backward of nn.MultiheadAttention over the BATCH axis (vit.py:48,59, batch_first=False on
+// (B, N, C): each token n and head h attends over the L = B images).  One wave per (token, head),
+// lane = head dim (64); L <= 8 so the score / probability tiles are 8 x 8 (one lane each):
+//   S = (q/8) k^T, P = softmax_j(S), dP = dO v^T, dS = P (dP - rowsum(P dP)),
+//   dq = dS k / 8, dk = dS^T (q/8), dv = P^T dO.   fp32; writes dqkv [L][ntok][3C] (q|k|v).
+__global__ void __launch_bounds__(256) vit_batch_attn_bwd_kernel(const float* __restrict__ qkv,
+                                                                 const float* __restrict__ dout,
+                                                                 float* __restrict__ dqkv, int L, int ntok,
+                                                                 int heads) {
+  constexpr int D = 64;
+  __shared__ float sq[4][8][D + 1];
+  __shared__ float sk[4][8][D + 1];
+  __shared__ float sv[4][8][D + 1];
+  __shared__ float sg[4][8][D + 1];
+  __shared__ float sp[4][8][8];
+  __shared__ float sds[4][8][8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long pair = (long long)blockIdx.x * 4 + wv;
+  const bool valid = pair < (long long)ntok * heads;
+  const int C = heads * D;
+  const long long pp = valid ? pair : 0;
+  const int n = (int)(pp / heads), hh = (int)(pp - (long long)n * heads);
+  const long long row3 = (long long)ntok * 3 * C, row1 = (long long)ntok * C;
+  const float* base = qkv + (long long)n * 3 * C + hh * D + lane;
+  const float* gbase = dout + (long long)n * C + hh * D + lane;
+  float qr[8], kr[8], vr[8], gr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool in = i < L;
+    qr[i] = in ? base[i * row3] * 0.125f : 0.f;  // 1/sqrt(64)
+    kr[i] = in ? base[i * row3 + C] : 0.f;
+    vr[i] = in ? base[i * row3 + 2 * C] : 0.f;
+    gr[i] = in ? gbase[i * row1] : 0.f;
+    sq[wv][i][lane] = qr[i];
+    sk[wv][i][lane] = kr[i];
+    sv[wv][i][lane] = vr[i];
+    sg[wv][i][lane] = gr[i];
+  }
+  __syncthreads();
+  const int i = lane >> 3, j = lane & 7;
+  const bool ij = i < L && j < L;
+  float s = -INFINITY, dp = 0.f;
+  if (ij) {
+    s = 0.f;
+#pragma unroll 16
+    for (int d = 0; d < D; ++d) {
+      s = fmaf(sq[wv][i][d], sk[wv][j][d], s);
+      dp = fmaf(sg[wv][i][d], sv[wv][j][d], dp);
+    }
+  }
+  float m = s;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const float e = ij ? __expf(s - m) : 0.f;
+  float sum = e;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
+  const float pr = e / sum;
+  float pdp = pr * dp;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) pdp += __shfl_xor(pdp, o, 64);
+  sp[wv][i][j] = pr;
+  sds[wv][i][j] = ij ? pr * (dp - pdp) : 0.f;
+  __syncthreads();
+  if (!valid) return;
+  float* obase = dqkv + (long long)n * 3 * C + hh * D + lane;
+  for (int r = 0; r < L; ++r) {
+    float dq = 0.f, dk = 0.f, dv = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      dq = fmaf(sds[wv][r][c], kr[c], dq);   // sum_j dS[r][j] k_j
+      dk = fmaf(sds[wv][c][r], qr[c], dk);   // sum_i dS[i][r] (q_i / 8)
+      dv = fmaf(sp[wv][c][r], gr[c], dv);    // sum_i P[i][r] dO_i
+    }
+    obase[r * row3] = dq * 0.125f;
+    obase[r * row3 + C] = dk;
+    obase[r * row3 + 2 * C] = dv;
+  }
+}
+
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static dim3 grid1(long long n) { return dim3((unsigned)((n + 255) / 256)); }
 
@@ -456,18 +619,26 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   p.kchunk = ((p.K + S - 1) / S + kTnBK - 1) / kTnBK * kTnBK;
   S = (p.K + p.kchunk - 1) / p.kchunk;
   p.tiles_n = (p.N + kTnBN - 1) / kTnBN;
-  const int tiles = ((p.M + kTnBM - 1) / kTnBM) * p.tiles_n;
+  const int bm = tn_bm(p.M);
+  const int tiles = ((p.M + bm - 1) / bm) * p.tiles_n;
   p.slab = work;
   if (S > 65535) return fail("mhada_gemm_tn: too many splits");
   const dim3 grid((unsigned)tiles, (unsigned)S);
-#define TN_LAUNCH(MODE)                                                                   \
-  do {                                                                                    \
-    if (vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true>), grid, dim3(256), 0, s, p); \
-    else hipLaunchKernelGGL((gemm_tn_kernel<MODE, false>), grid, dim3(256), 0, s, p);      \
+  const dim3 gsk((unsigned)S, (unsigned)((p.N / 4 + 255) / 256));
+#define TN_LAUNCH(MODE)                                                                             \
+  do {                                                                                              \
+    if (p.M <= 4) hipLaunchKernelGGL((tn_skinny_kernel<MODE>), gsk, dim3(256), 0, s, p);           \
+    else if (bm == 64 && vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true, 64>), grid, dim3(256), 0, s, p); \
+    else if (bm == 64) hipLaunchKernelGGL((gemm_tn_kernel<MODE, false, 64>), grid, dim3(256), 0, s, p); \
+    else if (vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true, 128>), grid, dim3(256), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_tn_kernel<MODE, false, 128>), grid, dim3(256), 0, s, p);         \
   } while (0)
   if (a->b_mode == MHADA_A_ROWS) TN_LAUNCH(MHADA_A_ROWS);
   else if (a->b_mode == MHADA_A_CONV3X3) TN_LAUNCH(MHADA_A_CONV3X3);
-  else if (a->b_mode == MHADA_A_PATCH8) TN_LAUNCH(MHADA_A_PATCH8);
+  else if (a->b_mode == MHADA_A_PATCH8) {
+    if (p.M <= 4) return fail("mhada_gemm_tn: PATCH8 needs M > 4");
+    TN_LAUNCH(MHADA_A_PATCH8);
+  }
   else TN_LAUNCH(MHADA_A_CONV3X3_ZERO);
 #undef TN_LAUNCH
   if (int rc = check_launch("mhada_gemm_tn")) return rc;
@@ -479,7 +650,8 @@ extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, f
                             mhada_stream_t s_) {
   if (!x || !out || !work || rows <= 0 || C <= 0) return fail("mhada_colsum: bad args");
   if (C % 4 || !al16(x) || !al16(work)) return fail("mhada_colsum: C % 4 == 0 and 16-byte aligned x, work");
-  long long chunks = std::min<long long>(std::max<long long>(1, rows / 256), 1024);
+  // ~1024 blocks of at least 16 rows each (the reduction pass then reads 1024 * C floats)
+  long long chunks = std::min<long long>(std::max<long long>(1, rows / 16), 1024);
   chunks = std::min<long long>(chunks, work_floats / C);
   if (chunks < 1) return fail("mhada_colsum: workspace smaller than C floats");
   const long long rpc = (rows + chunks - 1) / chunks;
@@ -543,4 +715,15 @@ extern "C" int mhada_vgg_input_bwd(const float* dout, float* dimg, int B, int H,
   hipLaunchKernelGGL(vgg_input_bwd_kernel, grid1((long long)B * H * W), dim3(256), 0, (hipStream_t)s_, dout, dimg, B, H,
                      W, Cp);
   return check_launch("mhada_vgg_input_bwd");
+}
+
+extern "C" int mhada_vit_batch_attn_bwd(const float* qkv, const float* dout, float* dqkv, int L, int ntok, int heads,
+                                        int head_dim, mhada_stream_t s_) {
+  if (!qkv || !dout || !dqkv || L <= 0 || L > 8 || ntok <= 0 || heads <= 0)
+    return fail("mhada_vit_batch_attn_bwd: bad args (1 <= L <= 8)");
+  if (head_dim != 64) return fail("mhada_vit_batch_attn_bwd: head_dim must be 64");
+  const long long pairs = (long long)ntok * heads;
+  hipLaunchKernelGGL(vit_batch_attn_bwd_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, (hipStream_t)s_, qkv,
+                     dout, dqkv, L, ntok, heads);
+  return check_launch("mhada_vit_batch_attn_bwd");
 }

@@ -76,6 +76,7 @@ SIGNATURES = {
     "mhada_rows_normalize": (_I, [_vp] * 4 + [_I, _I, _I, _I, _vp]),
     "mhada_gemm_tn": (_I, [ctypes.POINTER(GemmTnArgs), _vp, _c_ll, _vp]),
     "mhada_colsum": (_I, [_vp, _vp, _c_ll, _I, _vp, _c_ll, _vp]),
+    "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),

@@ -396,7 +396,7 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     C = x.shape[-1]
     rows = x.numel() // C
     out = torch.empty(C, device=x.device, dtype=torch.float32)
-    work = torch.empty(min(1024, max(1, rows // 256)) * C, device=x.device, dtype=torch.float32)
+    work = torch.empty(min(1024, max(1, rows // 16)) * C, device=x.device, dtype=torch.float32)
     _call("mhada_colsum", x, x.data_ptr(), out.data_ptr(), rows, C, work.data_ptr(), work.numel())
     return out
 
@@ -481,3 +481,12 @@ def loss_attn(qn: torch.Tensor, kn: torch.Tensor, v: torch.Tensor, x: torch.Tens
     _call("mhada_loss_attn", qn, qn.data_ptr(), kn.data_ptr(), v.data_ptr(), x.data_ptr(), x_mu.data_ptr(),
           x_rs.data_ptr(), out.data_ptr(), B, Nq, Ns, Dqk, Dv, activation)
     return out
+
+
+def vit_batch_attn_bwd(qkv: torch.Tensor, dout: torch.Tensor, L: int, ntok: int, heads: int) -> torch.Tensor:
+    """``mhada_vit_batch_attn_bwd``: fp32 qkv [L][ntok][3C], dout [L][ntok][C] -> dqkv."""
+    _need_gpu(qkv, dout)
+    C = qkv.shape[-1] // 3
+    dqkv = torch.empty_like(qkv)
+    _call("mhada_vit_batch_attn_bwd", qkv, qkv.data_ptr(), dout.data_ptr(), dqkv.data_ptr(), L, ntok, heads, C // heads)
+    return dqkv

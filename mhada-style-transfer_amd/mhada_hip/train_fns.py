@@ -146,6 +146,27 @@ def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bo
     return LinearFn.apply(x2d, weight, bias, relu)
 
 
+class BatchAxisAttnFn(torch.autograd.Function):
+    """The core of nn.MultiheadAttention(batch_first=False) on a (B, N, C) tensor (vit.py:48,59):
+    per token and head, softmax over the L = B images of (q/8) k^T, times v.  qkv [L][N][3C]
+    fp32 (the packed in-projection output) -> [L][N][C]; mhada_vit_batch_attn forward,
+    mhada_vit_batch_attn_bwd backward."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads: int):
+        qkv = qkv.contiguous()
+        L, N, _ = qkv.shape
+        ctx.save_for_backward(qkv)
+        ctx.heads = heads
+        return ops.vit_batch_attn(qkv, L, N, heads)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (qkv,) = ctx.saved_tensors
+        L, N, _ = qkv.shape
+        return ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads), None
+
+
 class PatchEmbedFn(torch.autograd.Function):
     """PatchEmbedding conv 8x8 / stride 8 (vit.py:105-117): img (B, 3, H, W) fp32 -> tokens
     [B][N][C]; weight (C, 3, 8, 8).  Gradients for the weight and bias only."""

@@ -153,6 +153,13 @@ def test_vgg19_and_decoder_modules_against_aten_autograd():
     dec = network.Decoder()
     sd = recipe_state_dict("dec", {"decoder." + k: tuple(v.shape) for k, v in dec.state_dict().items()})
     dec.load_state_dict({k[len("decoder."):]: v for k, v in sd.items()}, strict=True)
+    # biases shifted by +5: pre-activations then sit far from zero, so fp32 and fp64 never take
+    # different ReLU branches (a flip near the input changes a whole neighbourhood of gradients
+    # and every weight gradient of the early layers); the masking itself is pinned per layer above
+    with torch.no_grad():
+        for m in dec.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.bias.add_(5.0)
     dec64 = network.Decoder().double()  # aten fp64 reference on the CPU
     dec64.load_state_dict(dec.state_dict())
     dec = dec.to(DEV)
@@ -164,14 +171,8 @@ def test_vgg19_and_decoder_modules_against_aten_autograd():
     g = rnd(*y1.shape, seed=13)
     y1.backward(g)
     y2.backward(g.double().cpu())
-    # Through 9 ReLU layers with a random upstream gradient, a pre-activation within ~1e-7 of zero
-    # takes the opposite ReLU branch in fp32 and fp64 (about one of the ~6e5 activations here),
-    # and its whole gradient then differs: the chain is held to 1e-2 in norm and 99.9 % of the
-    # elements to 1e-4 of the largest (each layer alone is pinned at 1e-5 by the tests above).
     def close(a, b):
-        a, b = a.cpu().double(), b.double()
-        tol = 1e-4 * b.abs().max()
-        return rel(a, b) < 1e-2 and ((a - b).abs() > tol).double().mean().item() < 1e-3
+        return rel(a.cpu(), b) < 1e-5
     assert close(feat.grad, feat64.grad)
     for (n, p), (_, p64) in zip(dec.named_parameters(), dec64.named_parameters()):
         assert close(p.grad, p64.grad), n
@@ -291,3 +292,40 @@ def test_vit_training_forward_matches_aten_autograd():
     for (n, p), (_, p64) in zip(vit.named_parameters(), vit64.named_parameters()):
         err = (p.grad.cpu().double() - p64.grad).norm().item()
         assert err <= 1e-4 * p64.grad.norm().item() + 1e-7 * gmax, n
+
+
+@pytest.mark.parametrize("M,N,K,mode", [(64, 576, 30000, "reflect"), (4, 576, 20000, "reflect"), (3, 576, 5000, "zero"),
+                                        (256, 2304, 8000, "zero")])
+def test_gemm_tn_conv_tiles(M, N, K, mode):
+    """Weight-gradient tiles: the 64-row variant, the skinny (M <= 4) VALU kernel and 128 rows."""
+    from mhada_hip._lib import A_CONV3X3, A_CONV3X3_ZERO
+    ci = N // 9
+    H = W = 50
+    B = max(1, K // (H * W))
+    K = B * H * W
+    x = rnd(B, H, W, ci, seed=31)
+    g = rnd(K, M, seed=32)
+    c = ops.gemm_tn(g, x, M=M, N=N, K=K, lda=M, b_mode=A_CONV3X3 if mode == "reflect" else A_CONV3X3_ZERO,
+                    img=(ci, H, W), pad=1)
+    xp = F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect" if mode == "reflect" else "constant")
+    cols = F.unfold(xp, 3)  # (B, ci*9, H*W) with k = ci*9 + tap
+    cols = cols.view(B, ci, 9, H * W).permute(0, 3, 2, 1).reshape(K, 9 * ci)  # -> [pixel][tap*ci + c]
+    ref = g.double().T @ cols
+    assert rel(c, ref) < 1e-5
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 8])
+def test_batch_axis_attention_fwd_bwd(L):
+    """nn.MultiheadAttention's core over the batch axis (vit.py:48,59) on the HIP kernels vs fp64."""
+    N, C, heads = 77, 512, 8
+    qkv = rnd(L, N, 3 * C, seed=40 + L).requires_grad_(True)
+    out = train_fns.BatchAxisAttnFn.apply(qkv, heads)
+    g = rnd(L, N, C, seed=50 + L)
+    out.backward(g)
+    q64 = qkv.detach().double().requires_grad_(True)
+    q, k, v = (z.reshape(L, N, heads, 64).permute(1, 2, 0, 3) for z in q64.split(C, dim=-1))
+    a = torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1)
+    ref = (a @ v).permute(2, 0, 1, 3).reshape(L, N, C)
+    ref.backward(g.double())
+    assert rel(out, ref) < 1e-6
+    assert rel(qkv.grad, q64.grad) < 1e-6

@@ -113,6 +113,10 @@ def conv_suite():
             w = (torch.randn(Co, 9 * Ci, device=dev) / (9 * Ci) ** 0.5).to(dt)
             bias = torch.randn(Co, device=dev)
             fns = {"fused": lambda: ops.conv3x3(x, w, bias, dt, upsample=up)}
+            if not up:  # MIOpen calibration point (zero padding, channels-last, same shape)
+                xc = x.permute(0, 3, 1, 2)
+                w4 = w.view(Co, 3, 3, Ci).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+                fns["miopen"] = lambda: torch.nn.functional.conv2d(xc, w4, bias.to(dt), padding=1)
             if dt == torch.float32 and Co > 128:
                 fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.conv3x3, ops.upsample2x(x) if up else x, w,
                                                   bias, dt, upsample=False)
