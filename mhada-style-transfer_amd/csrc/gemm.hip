@@ -859,52 +859,53 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 
   // ring slots of K-tiles g, g+1, g+2 (global K-tile counter g, continuous across tiles)
   int sl0 = 0, sl1 = 1, sl2 = NSLOT == 2 ? 0 : 2;
-  while (true) {
-    for (int kt = 0; kt < KT; ++kt) {
-      const int cb = sl0;
-      // sources of K-tiles g+1 (W) and g+2 (A): this tile or the next one
-      const bool w1 = kt + 1 < KT || has_nxt;
-      const St& s1 = kt + 1 < KT ? cur : nxt;
-      const int k1 = kt + 1 < KT ? kt + 1 : 0;
-      const bool a2 = kt + 2 < KT || has_nxt;
-      const St& s2 = kt + 2 < KT ? cur : nxt;
-      const int k2 = kt + 2 < KT ? kt + 2 : kt + 2 - KT;
-      if constexpr (TN == 2) {
-        // phase 0
-        read_a(0, cb); read_w(0, 0, cb);
-        if (w1) stage_w(s1, 0, k1, sl1);
-        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
-        // phase 1
-        read_w(1, 0, cb);
-        if (w1) stage_w(s1, 1, k1, sl1);
-        PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
-        // phase 2
-        read_a(1, cb); read_w(0, 1, cb);
-        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
-        // phase 3
-        read_w(1, 1, cb);
-      } else {
-        // phase 0: k-steps of pair 0
-        read_a(0, cb); read_w(0, 0, cb);
-        if (w1) stage_w(s1, 0, k1, sl1);
-        PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
-        // phase 1: pair 1
-        read_a(1, cb); read_w(0, 1, cb);
-      }
-      if (a2) {
-        stage_a(s2, 0, k2, sl2); stage_a(s2, 1, k2, sl2);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      PP_LGKM0(); PP_BARRIER(); compute(TN - 1); PP_BARRIER();
-      if constexpr (NSLOT == 2) {
-        sl0 ^= 1; sl1 ^= 1; sl2 ^= 1;
-      } else {
-        const int o = sl0;
-        sl0 = sl1; sl1 = sl2; sl2 = o;
-      }
+  // one K-tile: W of K-tile g+1 comes from (s1, k1), A of K-tile g+2 from (s2, k2).  The three
+  // call sites below bind s1 / s2 to `cur` or `nxt` at compile time: selecting the struct by a
+  // runtime condition made hipcc copy the whole staging state every iteration (~280 v_mov + 50-100
+  // v_readlane per K-tile in the last two K-tiles of each tile).
+  auto ktile = [&](const St& s1, const int k1, const bool w1, const St& s2, const int k2, const bool a2)
+      __attribute__((always_inline)) {
+    const int cb = sl0;
+    if constexpr (TN == 2) {
+      // phase 0
+      read_a(0, cb); read_w(0, 0, cb);
+      if (w1) stage_w(s1, 0, k1, sl1);
+      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+      // phase 1
+      read_w(1, 0, cb);
+      if (w1) stage_w(s1, 1, k1, sl1);
+      PP_LGKM0(); PP_BARRIER(); compute(1); PP_BARRIER();
+      // phase 2
+      read_a(1, cb); read_w(0, 1, cb);
+      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+      // phase 3
+      read_w(1, 1, cb);
+    } else {
+      // phase 0: k-steps of pair 0
+      read_a(0, cb); read_w(0, 0, cb);
+      if (w1) stage_w(s1, 0, k1, sl1);
+      PP_LGKM0(); PP_BARRIER(); compute(0); PP_BARRIER();
+      // phase 1: pair 1
+      read_a(1, cb); read_w(0, 1, cb);
     }
+    if (a2) {
+      stage_a(s2, 0, k2, sl2); stage_a(s2, 1, k2, sl2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    PP_LGKM0(); PP_BARRIER(); compute(TN - 1); PP_BARRIER();
+    if constexpr (NSLOT == 2) {
+      sl0 ^= 1; sl1 ^= 1; sl2 ^= 1;
+    } else {
+      const int o = sl0;
+      sl0 = sl1; sl1 = sl2; sl2 = o;
+    }
+  };
+  while (true) {
+    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, true, cur, kt + 2, true);
+    ktile(cur, KT - 1, true, nxt, 0, has_nxt);  // KT >= 2 (checked on the host)
+    ktile(nxt, 0, has_nxt, nxt, 1, has_nxt);
     // tile boundary: re-align the groups so both store in the same interval (a store between
     // staggered barriers would hold the other group's compute phase), then re-stagger
     if (grp == 0) PP_BARRIER();

@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(256) vit_batch_attn_bwd_kernel(const float* __
   float sum = e;
 #pragma unroll
   for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
-  const float pr = e / sum;
+  const float pr = ij ? e / sum : 0.f;  // rows i >= L have sum 0 (and must stay out of dv)
   float pdp = pr * dp;
 #pragma unroll
   for (int o = 1; o < 8; o <<= 1) pdp += __shfl_xor(pdp, o, 64);
@@ -650,8 +650,8 @@ extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, f
                             mhada_stream_t s_) {
   if (!x || !out || !work || rows <= 0 || C <= 0) return fail("mhada_colsum: bad args");
   if (C % 4 || !al16(x) || !al16(work)) return fail("mhada_colsum: C % 4 == 0 and 16-byte aligned x, work");
-  // ~1024 blocks of at least 16 rows each (the reduction pass then reads 1024 * C floats)
-  long long chunks = std::min<long long>(std::max<long long>(1, rows / 16), 1024);
+  // up to 128 blocks of at least 64 rows (the fixed-order reduction pass loops over the chunks)
+  long long chunks = std::min<long long>(std::max<long long>(1, rows / 64), 128);
   chunks = std::min<long long>(chunks, work_floats / C);
   if (chunks < 1) return fail("mhada_colsum: workspace smaller than C floats");
   const long long rpc = (rows + chunks - 1) / chunks;

@@ -396,7 +396,7 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     C = x.shape[-1]
     rows = x.numel() // C
     out = torch.empty(C, device=x.device, dtype=torch.float32)
-    work = torch.empty(min(1024, max(1, rows // 16)) * C, device=x.device, dtype=torch.float32)
+    work = torch.empty(min(128, max(1, rows // 64)) * C, device=x.device, dtype=torch.float32)
     _call("mhada_colsum", x, x.data_ptr(), out.data_ptr(), rows, C, work.data_ptr(), work.numel())
     return out
 
