@@ -284,3 +284,23 @@ def test_mhada_attn_late_max_jump(kernel, Nc, Ns):
     ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
     assert torch.isfinite(y.float()).all()
     assert rel(y.float(), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("kernel", ["fs", "w8"])
+@pytest.mark.parametrize("B,Nc,Ns", [(1, 256, 64), (2, 300, 100), (1, 513, 128), (1, 97, 1000), (2, 1000, 777),
+                                     (1, 64, 4096)])
+def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
+    """The bf16 softmax kernels (fixed shift "fs", online max "w8") at 1..32 key tiles of 128,
+    ragged and whole, and partial query blocks: against fp64 torch on the same bf16 operands
+    (bf16 P: 1e-2)."""
+    H = 8
+    q = (rnd(B, H, Nc, 64, seed=15) * 0.35).bfloat16()
+    kv = (rnd(B, H, Ns, 128, seed=16) * 0.35).bfloat16()
+    vt = ops.transpose_v(kv)
+    fcs = rnd(B, Nc, 512, seed=17)
+    mu, rs = ops.instnorm_stats(fcs)
+    vmu = rnd(B, 512, seed=18)
+    with _lib.tuning(attn_fixed_shift=int(kernel == "fs")):
+        y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+    ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
+    assert rel(y.float(), ref) < 1e-2
