@@ -48,7 +48,7 @@ const char* mhada_last_error(void);
  * calls change it (not thread-safe against concurrent launches: set knobs between launches).
  * Knobs (value range): attn_fixed_shift (0|1), attn_waves (4|8), attn_tk (64|128),
  * attn_prio (0|1), vit_attn_vec (0|1), out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1),
- * gemm_persist (0|1), gemm_pp128 (0|1), gemm_ldsepi (0|1), gemm_n64 (128|256).
+ * gemm_persist (0|1), gemm_pp128 (0|1), gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1).
  * Returns MHADA_ERR_ARG for an unknown knob or an out-of-range value.  No reference
  * counterpart (the reference has no kernels). */
 int mhada_set_tuning(const char* name, int value);

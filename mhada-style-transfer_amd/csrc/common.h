@@ -40,8 +40,14 @@ struct Tuning {
   int gemm_pp128 = 1;        // 256x128 persistent ping-pong form for 65..128 columns
   int gemm_ldsepi = 1;       // ping-pong epilogue staged through LDS
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
+  int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
 };
 const Tuning& tuning();
+
+// conv_tile.hip: bf16 3x3 conv, Cin = Cout = 64, reflect pad, optional fused bilinear x2
+// upsample of the input; H, W = output size.  Dispatched from mhada_gemm.
+int conv3x3_c64(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, bool up, int relu,
+                hipStream_t s);
 
 // ---- scalar conversions -----------------------------------------------------------------
 template <typename T> MHADA_DEV float to_f32(T x);

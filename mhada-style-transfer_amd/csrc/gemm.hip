@@ -1132,6 +1132,12 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   }
   const int nz = a->nb1 * a->nb2;
   if (nz > 65535) return fail("mhada_gemm: too many batch entries");
+  // the decoder's 64 -> 64 layer (with its fused upsample): direct tile kernel (conv_tile.hip)
+  if (tuning().conv_c64 && a->compute == MHADA_BF16 && a->a_dtype == MHADA_BF16 && a->c_dtype == MHADA_BF16 &&
+      (a->a_mode == MHADA_A_CONV3X3 || a->a_mode == MHADA_A_CONV3X3_UP2) && a->img_c == 64 && a->N == 64 &&
+      a->ldc == 64 && a->ldw == 576 && a->bias && !a->r)
+    return conv3x3_c64(a->a, a->w, a->bias, a->c, a->M / (p.out_h * p.out_w), p.out_h, p.out_w,
+                       a->a_mode == MHADA_A_CONV3X3_UP2, a->relu, stream);
   if (a->compute == MHADA_F32) return dispatch_mode<float, float, float>(a->a_mode, p, nz, stream);
   if (a->a_dtype == MHADA_F32) {
     if (a->c_dtype == MHADA_F32) return dispatch_mode<bf16, float, float>(a->a_mode, p, nz, stream);

@@ -108,6 +108,28 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
     assert rel(y.permute(0, 3, 1, 2), ref) < TOL[cdt]
 
 
+@pytest.mark.parametrize("up", [False, True])
+@pytest.mark.parametrize("B,H,W", [(2, 4, 8), (1, 9, 13), (2, 33, 20), (1, 64, 128), (1, 3, 2), (3, 17, 70)])
+def test_conv3x3_c64_tile(up, B, H, W):
+    """The decoder's 64 -> 64 layer on the direct tile kernel (conv_tile.hip, bf16 in / out):
+    against fp64 on the same bf16 input (upsampled by upsample2x_kernel for up=True), the fused
+    upsample bit-identical to upsample2x + conv, and close to the implicit-GEMM path."""
+    x = torch.rand(B, H, W, 64, generator=torch.Generator().manual_seed(H * W)).to(DEV).bfloat16()
+    w = rnd(64, 64, 3, 3, scale=(9 * 64) ** -0.5, seed=2)
+    b = rnd(64, seed=3)
+    wp = w.permute(0, 2, 3, 1).reshape(64, -1).bfloat16().contiguous()
+    y = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=up)
+    xin = ops.upsample2x(x) if up else x
+    ref = torch.relu(F.conv2d(F.pad(xin.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
+                              wp.double().view(64, 3, 3, 64).permute(0, 3, 1, 2), b.double()))
+    assert rel(y.permute(0, 3, 1, 2), ref) < 5e-3
+    if up:
+        assert torch.equal(y, ops.conv3x3(xin, wp, b, torch.bfloat16, upsample=False))
+    with _lib.tuning(conv_c64=0):
+        y0 = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=up)
+    assert rel(y, y0) < 5e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128)])
 def test_upsample2x(dt, H, W, C):
