@@ -201,11 +201,19 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
   const long long n4 = rows * ncol / 4;
   if (q >= n4) return;
   const long long total = rows * ncol;
-  f32x4 acc = *reinterpret_cast<const f32x4*>(slab + 4 * q);
-  for (int s = 1; s < S; ++s) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(slab + (long long)s * total + 4 * q);
-    acc += v;
+  // 8 slab loads in flight per batch, summed in slab order (a one-load-per-iteration loop was
+  // latency bound: 64 slabs of 1 MiB reduced at ~0.5 TB/s)
+  const float* sp = slab + 4 * q;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(sp);
+  int s = 1;
+  for (; s + 8 <= S; s += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const f32x4*>(sp + (long long)(s + j) * total);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
   }
+  for (; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(sp + (long long)s * total);
   const long long i = 4 * q, r = i / ncol, c = i - r * ncol;
   if (ld == ncol) {
     *reinterpret_cast<f32x4*>(out + i) = acc;

@@ -115,6 +115,26 @@ def test_api_shapes_and_calling_conventions():
     assert torch.equal(cs, cs3)
 
 
+def test_feature_outputs_are_channels_last_nchw():
+    """fc / fs / fcs are NCHW tensors in torch.channels_last memory format (views of the
+    token-major storage; the reference's are contiguous NCHW, vit.py:165-166 / adaDecoder.py:205).
+    Every torch op, .reshape and .contiguous() behave as on the reference's tensors; a raw
+    .view(B, -1) needs .contiguous() first.  cs is contiguous NCHW."""
+    ms = models()
+    c = seeded_image(2, 64, 48, 1).to(DEV)
+    fc, fs, fcs, cs = stylize(ms, c, c)
+    assert cs.is_contiguous()
+    for t in (*fc, *fs, fcs):
+        assert t.is_contiguous(memory_format=torch.channels_last)
+        ref = t.contiguous()
+        assert torch.equal(t.reshape(2, -1), ref.view(2, -1))
+        assert torch.equal(t.flatten(2).transpose(1, 2), ref.flatten(2).transpose(1, 2))
+        assert torch.allclose(torch.nn.functional.avg_pool2d(t, 2), torch.nn.functional.avg_pool2d(ref, 2),
+                              rtol=1e-6, atol=1e-5)
+        with pytest.raises(RuntimeError):
+            t.view(2, -1)
+
+
 def test_bf16_autocast_selects_bf16_path():
     ms = models()
     for m in ms:
