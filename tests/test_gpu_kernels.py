@@ -257,6 +257,22 @@ def test_mhada_online_softmax_rescale_branch(dt):
     assert rel(y, ref) < (max(1e-5, 2 * err32) if dt == torch.float32 else 5e-2)
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs a second visible GPU")
+def test_block_on_a_non_current_device():
+    """Every launch runs under a device guard on its operands' device and that device's current
+    stream (ops._call): a module moved to cuda:1 works while cuda:0 is current."""
+    blk0 = _block("softmax", torch.float32)
+    blk1 = _block("softmax", torch.float32).to("cuda:1")
+    fc = rnd(2, 512, 9, 7, seed=21)
+    fs = rnd(2, 512, 5, 6, seed=22)
+    torch.cuda.set_device(0)
+    with torch.no_grad():
+        y0 = blk0(fc, fs, fc)
+        y1 = blk1(fc.to("cuda:1"), fs.to("cuda:1"), fc.to("cuda:1"))
+    assert y1.device == torch.device("cuda:1")
+    assert torch.equal(y0.cpu(), y1.cpu())
+
+
 def test_mhada_is_per_sample_independent():
     """Unlike the ViT (batch-axis attention), MHAda blocks are per-sample."""
     blk = _block("softmax", torch.float32)
