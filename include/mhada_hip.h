@@ -29,6 +29,7 @@ typedef void* mhada_stream_t; /* hipStream_t */
 enum { MHADA_OK = 0, MHADA_ERR_ARG = 1, MHADA_ERR_LAUNCH = 2 };
 enum { MHADA_F32 = 0, MHADA_BF16 = 1 };
 enum { MHADA_ACT_SOFTMAX = 0, MHADA_ACT_COSINE = 1 };
+enum { MHADA_PAD_REFLECT = 0, MHADA_PAD_ZERO = 1 };
 enum {
   MHADA_A_ROWS = 0,        /* A[m*lda + k], row-major                                     */
   MHADA_A_PATCH8 = 1,      /* A = im2col of an NCHW fp32 image, 8x8 patches, stride 8     */
@@ -39,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 4 (training: CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 5 (Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -269,6 +270,19 @@ int mhada_rows_normalize(const float* x, const float* mu, const float* rs, float
  * out: [B][3][Ho][Wo] fp32. */
 int mhada_frame_ingest(const void* frames, int B, int H, int W, long long row_bytes, int bgr, float* out,
                        int Ho, int Wo, mhada_stream_t stream);
+
+/* fp32 3x3 convolution as Winograd F(2x2,3x3) on the fp32 MFMA (2.25x fewer products than the
+ * direct correlation).  Replaces the fp32 Conv2d(k=3) of the decoder (ReflectionPad2d(1) + conv,
+ * conv.py:23-33,36-45,61-72: pad_mode MHADA_PAD_REFLECT) and of VGG19 (vgg19.py:15-70, zero
+ * padding 1), and the training input-gradient convs (zero pad 1, or pad 2 = the full correlation,
+ * output (H+2) x (W+2); train_image.py:139).  x NHWC [B][H][W][Cin] fp32, u = the transformed
+ * filters from mhada_wino_weights (w packed [Cout][3][3][Cin] fp32 -> u [Cin/8][16][Cout][8]),
+ * bias [Cout] or NULL, y NHWC [B][Ho][Wo][ldc] (ldc >= Cout), optional ReLU.
+ * Cin % 8 == 0, Cout % 64 == 0. */
+int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, mhada_stream_t stream);
+int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
+                       int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
+                       mhada_stream_t stream);
 
 #ifdef __cplusplus
 }

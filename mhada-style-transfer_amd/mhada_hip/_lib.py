@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmhada_hi
 F32, BF16 = 0, 1
 ACT_SOFTMAX, ACT_COSINE = 0, 1
 A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO = 0, 1, 2, 3, 4
+PAD_REFLECT, PAD_ZERO = 0, 1
 
 _c_ll = ctypes.c_longlong
 _vp = ctypes.c_void_p
@@ -84,6 +85,8 @@ SIGNATURES = {
     "mhada_upsample2x_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_wino_weights": (_I, [_vp, _vp, _I, _I, _vp]),
+    "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp]),
 }
 
 _lib = None
@@ -113,7 +116,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 def get_tuning(name: str) -> int:

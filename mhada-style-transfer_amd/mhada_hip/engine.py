@@ -311,7 +311,10 @@ def decoder_prep(dec, dtype):
         for name, up in DECODER_LAYERS:
             conv = mods[name].conv.conv
             w = conv.weight.permute(0, 2, 3, 1).reshape(conv.weight.shape[0], -1).to(dt).contiguous()
-            layers.append((w, conv.bias.float().contiguous(), up))
+            # fp32: the Winograd-transformed filters (ops.conv3x3 runs F(2x2,3x3) when eligible)
+            u = ops.wino_weights(w) if dt == torch.float32 and w.shape[0] % 64 == 0 and (w.shape[1] // 9) % 8 == 0 \
+                else None
+            layers.append((w, conv.bias.float().contiguous(), up, u))
         last = mods[LAST_LAYER].conv.conv
         # [out][cin][ky][kx] -> [ky*3+kx][cin][out]
         return dict(layers=layers, w_last=last.weight.permute(2, 3, 1, 0).float().contiguous(),
@@ -323,11 +326,11 @@ def decoder_forward_tokens(dec, x_nhwc: torch.Tensor, dt: torch.dtype, clamp255:
     """Decoder.forward (conv.py:96-100) on NHWC input; returns NCHW fp32 (B,3,8h,8w)."""
     prep = decoder_prep(dec, dt)
     x = x_nhwc
-    for w, b, up in prep["layers"]:
+    for w, b, up, u in prep["layers"]:
         if up and not _fuse_upsample(dt, w):
             x = ops.upsample2x(x)
             up = False
-        x = ops.conv3x3(x, w, b, dt, upsample=up, relu=True)
+        x = ops.conv3x3(x, w, b, dt, upsample=up, relu=True, wino_u=u)
     return ops.conv3x3_out3(x, prep["w_last"], prep["b_last"], clamp255=clamp255)
 
 

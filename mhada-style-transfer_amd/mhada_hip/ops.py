@@ -120,15 +120,64 @@ def patch_embed(img: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, pos: Opt
                 r=pos, ldr=C, sr=(0, 0), ldc=C, sc=(N * C, 0))
 
 
+# fp32 3x3 convs run as Winograd F(2x2,3x3) (csrc/wino.hip) where the shape allows it; False
+# forces the implicit-GEMM direct product (A/B measurements, tests).
+WINO = True
+
+
+def wino_eligible(x: torch.Tensor, w: torch.Tensor, upsample: bool) -> bool:
+    return (WINO and w.dtype == torch.float32 and x.dtype == torch.float32 and not upsample
+            and x.shape[-1] % 8 == 0 and w.shape[0] % 64 == 0 and x.shape[1] >= 2 and x.shape[2] >= 2)
+
+
+def wino_weights(w: torch.Tensor) -> torch.Tensor:
+    """``mhada_wino_weights``: w packed [Cout][9*Cin] fp32 -> U [Cin/8][16][Cout][8]."""
+    _need_gpu(w)
+    Co, K = w.shape
+    Ci = K // 9
+    if w.dtype != torch.float32 or K != 9 * Ci or not w.is_contiguous():
+        raise ValueError("wino_weights needs a contiguous fp32 [Cout][9*Cin] weight")
+    u = torch.empty(Ci // 8, 16, Co, 8, device=w.device, dtype=torch.float32)
+    _call("mhada_wino_weights", w, w.data_ptr(), u.data_ptr(), Co, Ci)
+    return u
+
+
+def conv3x3_wino(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = True,
+                 pad_mode: str = "reflect", pad: int = 1, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``mhada_conv3x3_wino``: fp32 NHWC conv3x3 from the transformed filters ``u``."""
+    _need_gpu(x, u, bias, out)
+    B, H, W, Ci = x.shape
+    Co = u.shape[2]
+    if x.dtype != torch.float32 or not x.is_contiguous() or u.shape[0] * 8 != Ci:
+        raise ValueError("conv3x3_wino: contiguous fp32 NHWC input matching the filters")
+    if pad_mode == "reflect":
+        mode, Ho, Wo, pad = _lib.PAD_REFLECT, H, W, 1
+    elif pad_mode == "zero":
+        mode, Ho, Wo = _lib.PAD_ZERO, H + 2 * (pad - 1), W + 2 * (pad - 1)
+    else:
+        raise ValueError(f"pad_mode {pad_mode!r}")
+    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32) if out is None else out
+    if y.shape[:3] != (B, Ho, Wo) or y.dtype != torch.float32 or y.shape[-1] < Co or not y.is_contiguous():
+        raise ValueError("conv3x3_wino: bad output buffer")
+    _call("mhada_conv3x3_wino", x, x.data_ptr(), u.data_ptr(), _ptr(bias), y.data_ptr(), B, H, W, Ci, Co,
+          y.shape[-1], mode, pad, int(relu))
+    return y
+
+
 def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
             upsample: bool, relu: bool = True, pad_mode: str = "reflect", pad: int = 1,
-            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, wino_u: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NHWC x [B][H][W][Cin] -> NHWC [B][H'][W'][Cout]; ReflectionPad2d(1)+conv3x3(+ReLU),
     optionally on bilinear-x2(x), or (pad_mode "zero") a zero-padded conv with padding `pad`
     (1: same size, 2: the full correlation, H' = H + 2).  w packed [Cout][9*Cin] in the compute
-    dtype.  ``out`` may be a preallocated [B][H'][W'][ldc >= Cout] buffer (channel padding)."""
+    dtype.  ``out`` may be a preallocated [B][H'][W'][ldc >= Cout] buffer (channel padding).
+    fp32 runs as Winograd F(2x2,3x3) when the shape allows (``wino_u``: cached transformed
+    filters of ``w``)."""
     B, H, W, Ci = x.shape
     Co = w.shape[0]
+    if out_dtype == torch.float32 and wino_eligible(x, w, upsample) and x.is_contiguous():
+        u = wino_u if wino_u is not None else wino_weights(w)
+        return conv3x3_wino(x, u, bias, relu, pad_mode, pad, out)
     if pad_mode == "zero":
         if upsample:
             raise ValueError("zero-padded conv3x3 has no fused upsample")

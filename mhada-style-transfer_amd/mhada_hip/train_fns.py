@@ -19,7 +19,7 @@ the reference, and runs its forward and backward through libmhada_hip.so:
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
@@ -67,6 +67,21 @@ def _cached(weight: torch.Tensor, kind: str, *dims) -> torch.Tensor:
     return w
 
 
+def _wino(weight: torch.Tensor, kind: str, packed: torch.Tensor, *dims) -> Optional[torch.Tensor]:
+    """Winograd-transformed filters of a frozen layer's packed weights (cached like _cached);
+    None for trainable weights (ops.conv3x3 transforms them per call) or ineligible shapes."""
+    if weight.requires_grad or packed.dtype != F32 or packed.shape[0] % 64 or (packed.shape[1] // 9) % 8:
+        return None
+    cache = weight.__dict__.setdefault("_mhada_pack", {})
+    key = ("u", kind) + dims
+    hit = cache.get(key)
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    u = ops.wino_weights(packed)
+    cache[key] = (weight._version, u)
+    return u
+
+
 class Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pad_mode: str, relu: bool):
@@ -78,8 +93,9 @@ class Conv3x3Fn(torch.autograd.Function):
             raise ValueError(f"conv3x3: input channels {cx} must be a multiple of 32 and >= {ci}")
         ldc = _ceil(co, 4)
         y = (torch.zeros if ldc != co else torch.empty)(B, H, W, ldc, device=x.device, dtype=F32)
-        ops.conv3x3(x, _cached(weight, "f", cx), bias.detach().float().contiguous(), F32, upsample=False,
-                    relu=relu, pad_mode=pad_mode, pad=1, out=y)
+        wf = _cached(weight, "f", cx)
+        ops.conv3x3(x, wf, bias.detach().float().contiguous(), F32, upsample=False,
+                    relu=relu, pad_mode=pad_mode, pad=1, out=y, wino_u=_wino(weight, "f", wf, cx))
         ctx.save_for_backward(x, weight, y)
         ctx.pad_mode, ctx.relu = pad_mode, relu
         return y if ldc == co else y[..., :co].contiguous()
@@ -99,11 +115,12 @@ class Conv3x3Fn(torch.autograd.Function):
             cg = _ceil(co, 32)
             gk = g if cg == ldc else F.pad(g, (0, cg - ldc))
             wt = _cached(weight, "d", cx, cg)
+            ut = _wino(weight, "d", wt, cx, cg)
             if ctx.pad_mode == "zero":
-                gx = ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero", pad=1)
+                gx = ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero", pad=1, wino_u=ut)
             else:
                 gx = ops.reflect_fold(ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero",
-                                                  pad=2))
+                                                  pad=2, wino_u=ut))
         if ctx.needs_input_grad[1]:
             mode = A_CONV3X3 if ctx.pad_mode == "reflect" else A_CONV3X3_ZERO
             # M = ldc (the zero-padded channel columns of g) keeps the vectorised A loads

@@ -108,6 +108,50 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
     assert rel(y.permute(0, 3, 1, 2), ref) < TOL[cdt]
 
 
+@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
+                                              (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64),
+                                              (1, 16, 16, 512, 256, 256), (2, 2, 5, 24, 192, 196)])
+def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
+    """fp32 Winograd F(2x2,3x3) (wino.hip) against fp64 conv2d: reflect / zero padding 1 / the
+    pad-2 full correlation, odd and tiny output grids (partial tiles), channel-padded outputs
+    (ldc > Cout, pad columns untouched), bias + ReLU and none; and against the direct
+    implicit-GEMM product (ops.WINO = False)."""
+    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(H * W + Ci)).to(DEV) - 0.3
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, seed=2)
+    b = rnd(Co, seed=3)
+    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous()
+    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
+    xn = x.permute(0, 3, 1, 2).double()
+    xp = F.pad(xn, (1, 1, 1, 1), mode="reflect") if pad_mode == "reflect" else F.pad(xn, (pad,) * 4)
+    for bias, relu in ((b, True), (None, False)):
+        out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
+        y = ops.conv3x3_wino(x, ops.wino_weights(wp), bias, relu, pad_mode, pad, out=out)
+        ref = F.conv2d(xp, w.double(), None if bias is None else bias.double())
+        ref = torch.relu(ref) if relu else ref
+        assert rel(y[..., :Co].permute(0, 3, 1, 2), ref) < 2e-6
+        assert bool((y[..., Co:] == 7.0).all())
+        if Ci % 32:  # the fp32 implicit GEMM gathers 32-channel chunks
+            continue
+        ops.WINO = False
+        try:
+            yd = ops.conv3x3(x, wp, bias, torch.float32, upsample=False, relu=relu, pad_mode=pad_mode, pad=pad)
+        finally:
+            ops.WINO = True
+        assert rel(y[..., :Co], yd) < 2e-6
+
+
+def test_conv3x3_wino_routing():
+    """ops.conv3x3 takes the Winograd kernel for eligible fp32 shapes (same result as the explicit
+    call) and the implicit GEMM otherwise (Cout % 64 != 0)."""
+    x = torch.rand(1, 12, 10, 64, generator=torch.Generator().manual_seed(4)).to(DEV)
+    w = rnd(128, 9 * 64, scale=1 / 24, seed=5)
+    b = rnd(128, seed=6)
+    assert ops.wino_eligible(x, w, False) and not ops.wino_eligible(x, w[:96], False)
+    assert torch.equal(ops.conv3x3(x, w, b, torch.float32, upsample=False),
+                       ops.conv3x3_wino(x, ops.wino_weights(w), b))
+
+
 @pytest.mark.parametrize("up", [False, True])
 @pytest.mark.parametrize("B,H,W", [(2, 4, 8), (1, 9, 13), (2, 33, 20), (1, 64, 128), (1, 3, 2), (3, 17, 70)])
 def test_conv3x3_c64_tile(up, B, H, W):
