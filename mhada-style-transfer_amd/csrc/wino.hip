@@ -10,40 +10,45 @@
 // instead of 36: 2.25x fewer MFMA FLOPs.  Transforms (Lavin & Gray 2016):
 //   V = B^T d B  (input 4x4)   U = G g G^T  (3x3 filter -> 4x4)   Y = A^T (U . V) A  (2x2)
 // and for each of the 16 positions xi the channel reduction M_xi[tile][co] = sum_ci V_xi[tile][ci]
-// U_xi[ci][co] is a GEMM; all 16 run here inside one workgroup, so V and M never touch HBM.
-// The transforms only add/subtract (G's 1/2 is exact), so the result is the direct
-// correlation up to fp32 rounding of 4-term sums.
+// U_xi[ci][co] is a GEMM; all 16 run inside one workgroup, so V and M never touch HBM.  The
+// transforms only add / subtract (G's 1/2 is exact): the direct correlation up to fp32 rounding
+// of 4-term sums.
 //
-// Workgroup = 4 waves (one per SIMD) = 32 Winograd tiles (4 x 8 tiles = 8 x 16 output pixels)
-// x 64 output channels.  Wave w owns the four positions xi = (i = w, j = 0..3): 8 accumulator
-// blocks (32 tiles x 32 channels) = 128 registers.  Per 8-channel chunk of the input:
-//   * each thread loads its (tile, channel) 4x4 input patch (padding resolved on load) and the
-//     U slice [16][64 co][8 ci] (contiguous 32 KiB, prepacked by mhada_wino_weights), issued one
-//     chunk ahead into registers;
-//   * after the current chunk's MFMAs it transforms the patch and writes V[16][32][8] and U into
-//     the other LDS buffer (rows padded to 48 B: conflict-free ds_read_b128 down 16 rows);
-//   * per chunk a wave runs 32 MFMAs (4 k-steps x 4 xi x 2 channel blocks; k-step s of lane half
-//     h takes channel 4h + s, read as one ds_read_b128 for A and for B).
-// Epilogue: each wave reduces its row i of the 4x4 grid along j (P_i = M_i. A), the four row
-// partials meet in LDS, and Y = A^T P + bias (+ReLU) is stored as 64-channel pixel rows.
+// Workgroup = 4 waves (one per SIMD, 512 registers each) = 64 Winograd tiles (8 x 8 tiles =
+// 16 x 16 output pixels) x 64 output channels; wave w owns tiles 32(w&1).. x channels 32(w>>1)..
+// for ALL 16 positions (16 accumulator blocks = 256 AGPRs), so the output transform runs in
+// registers.  The input channels stream in chunks of 4; per chunk:
+//   * the raw 18 x 18-pixel input patch (16 B per pixel, padding resolved at the load) and the
+//     transformed-filter slice U [16][64 co][4 ci] (16 KiB, contiguous, prepacked by
+//     mhada_wino_weights) arrive in registers one chunk ahead and are written to LDS;
+//   * beside the wave's 32 MFMAs of chunk k (2 k-steps x 16 positions) it transforms the raw
+//     patch of chunk k+1 (16 LDS reads, the B^T d B adds, 16 LDS writes per thread) into the
+//     other V buffer; one barrier per chunk.
+// The first version (32 tiles x 64 channels per workgroup, 8-channel chunks, 16 scalar gathers
+// per thread, all-position exchange through LDS in the epilogue) was L2-bandwidth bound: its
+// loads alone took as long as its MFMAs (ablation builds).  Here the filter slice is
+// reused by twice the tiles and the input arrives as whole 16-B pixels.
+// LDS operand rows are 16 B (4 channels) with the two 8-B halves swapped for rows 16..31 of every
+// 32, so the ds_read_b64 of 32 consecutive rows is conflict-free.
 #include "common.h"
 
 #ifndef WINO_DBG
-#define WINO_DBG 0  // ablation builds (tools/wino_dbg.py): 1 no MFMA, 2 no loads, 4 no transform/LDS stores
+#define WINO_DBG 0  // ablation builds (tools/wino_dbg.py): 1 no MFMA, 2 no loads, 4 no transform
 #endif
 
 namespace mhada {
 
 namespace {
-constexpr int kTY = 4, kTX = 8, kTT = kTY * kTX;  // tiles per workgroup
-constexpr int kCO = 64;                            // output channels per workgroup
-constexpr int kCK = 8;                             // input channels per chunk
-constexpr int kLR = 12;                            // LDS row: 8 floats + 4 pad (48 B)
-constexpr int kVS = 16 * kTT * kLR;                // V buffer (floats)
-constexpr int kUS = 16 * kCO * kLR;                // U buffer (floats)
-constexpr int kStage = kVS + kUS;                  // 18432 floats = 72 KiB
-constexpr int kLE = kCO + 4;                       // epilogue row stride (floats)
-static_assert(8 * kTT * kLE <= 2 * kStage, "epilogue exchange must fit the staging buffers");
+constexpr int kT = 8;                  // tiles per side: 8 x 8 tiles, 16 x 16 output pixels
+constexpr int kTT = kT * kT;           // 64 tiles
+constexpr int kCO = 64;                // output channels per workgroup
+constexpr int kCK = 8;                 // input channels per chunk
+constexpr int kRP = 2 * kT + 2;        // raw patch side: 18 pixels
+constexpr int kRaw = kRP * kRP;        // 324 pixels x 32 B
+constexpr int kRDma = (2 * kRaw + 63) / 64;  // LDS-DMA instructions for the raw patch (11)
+constexpr int kVS = 16 * kTT * kCK;    // V buffer (floats): [16][64 tiles][8]
+constexpr int kUS = 16 * kCO * kCK;    // U buffer (floats): [16][64 co][8]
+constexpr int kRS = kRDma * 64 * 4;    // raw buffer (floats): 704 16-B slots, 648 used
 
 struct WinoP {
   const float* x;     // NHWC [B][H][W][Cin]
@@ -59,10 +64,25 @@ MHADA_DEV int reflect_clamp(int v, int n) {
   v = v < 0 ? -v : (v >= n ? 2 * n - 2 - v : v);
   return min(max(v, 0), n - 1);
 }
+// float offset of the 16-B half `half` (channels 4*half .. 4*half+3) of 32-B row `row`: halves
+// swapped on rows with bit 3 set, so ds_read_b128 of 32 consecutive rows is conflict-free
+MHADA_DEV int swz(int row, int half) { return row * 8 + ((half ^ ((row >> 3) & 1)) << 2); }
+MHADA_DEV void glds16(const float* src, float* lds) {  // LDS-DMA: lane l -> lds + 16 l bytes
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
 
-__global__ void __launch_bounds__(256, 1) wino_kernel(const WinoP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kStage];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+__global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS)];  // 150 KiB
+  auto sV = [&](int i) { return lds + i * kVS; };
+  auto sU = [&](int i) { return lds + 2 * kVS + i * kUS; };
+  auto sR = [&](int i) { return lds + 2 * (kVS + kUS) + i * kRS; };
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // wave w: positions xi = 8e .. 8e+7 (rows 2e, 2e+1 of the 4x4 grid, e = w >> 2) x tiles
+  // 32(w & 1).. x channels 32((w >> 1) & 1)..; every thread also transforms one (tile, channel)
+  // and every wave issues a share of the LDS-DMA
+  const int e = wave >> 2, th = wave & 1, ch = (wave >> 1) & 1;
 
   // logical block: output-channel block fastest (neighbours share the input patch in L2)
   int id = xcd_remap(blockIdx.x, p.nblk);
@@ -73,66 +93,74 @@ __global__ void __launch_bounds__(256, 1) wino_kernel(const WinoP p) {
   const int by = id % p.nby;
   const int b = id / p.nby;
   const int co0 = nb * kCO;
-
-  // this thread's transform item: tile t, channel c of the chunk
-  const int tc = tid & 7, tt = tid >> 3;
-  const int ty = by * kTY + (tt >> 3), tx = bx * kTX + (tt & 7);
   const int P = p.zero ? p.pad : 1;
-  int off[16];
-  bool inb[16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int iy = 2 * ty - P + i, ix = 2 * tx - P + j;
-      bool ok = true;
-      if (p.zero) {
-        ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        iy = min(max(iy, 0), p.H - 1);
-        ix = min(max(ix, 0), p.W - 1);
-      } else {
-        iy = reflect_clamp(iy, p.H);
-        ix = reflect_clamp(ix, p.W);
-      }
-      off[4 * i + j] = ((b * p.H + iy) * p.W + ix) * p.Cin + tc;
-      inb[4 * i + j] = ok;
-    }
-
-  struct Stage {
-    float d[16];
-    f32x4 us[8];
-  };
-  const float* ub = p.u + (long long)co0 * 8;
-  const long long ustride = (long long)16 * p.Cout * 8;  // floats per 8-channel chunk
   const int nck = p.Cin / kCK;
-  // loads of chunk min(k, nck-1): clamped so every issue is unconditional (straight-line code
-  // keeps the compiler's vmcnt tracking exact); surplus chunks land in a buffer nobody reads
-  auto issue = [&](Stage& r, int k) {
+
+  // raw patch DMA: instruction j (wave j % 8, j < 11) fills 16-B slots 64 j + lane = pixel
+  // (slot >> 1), channel half (slot & 1); padding pixels load a clamped pixel (zeroed later)
+  int roff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int slot = 64 * (wave + 8 * t) + lane;
+    const int px = min(slot >> 1, kRaw - 1);
+    int iy = 2 * by * kT - P + px / kRP, ix = 2 * bx * kT - P + px % kRP;
+    if (p.zero) {
+      iy = min(max(iy, 0), p.H - 1);
+      ix = min(max(ix, 0), p.W - 1);
+    } else {
+      iy = reflect_clamp(iy, p.H);
+      ix = reflect_clamp(ix, p.W);
+    }
+    roff[t] = ((b * p.H + iy) * p.W + ix) * p.Cin + 4 * (slot & 1);
+  }
+  // U DMA: instructions 4w .. 4w+3 of 32; slot 64 j + lane = (xi, co row, stored half); the
+  // source half is the logical one (swz)
+  int uoff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int slot = 64 * (4 * wave + t) + lane;
+    const int xi = slot >> 7, row = (slot >> 1) & 63, sh = slot & 1;
+    uoff[t] = (xi * p.Cout + co0 + row) * kCK + 4 * (sh ^ ((row >> 3) & 1));
+  }
+  const long long ustride = (long long)16 * p.Cout * kCK;  // floats per chunk
+  auto dma = [&](int cu, float* su, int cr, float* sr) {
 #if WINO_DBG & 2
     return;
 #endif
-    k = min(k, nck - 1);
-    const float* xc = p.x + k * kCK;
+    cu = min(cu, nck - 1);
+    cr = min(cr, nck - 1);
+    const float* uc = p.u + cu * ustride;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) r.d[e] = xc[off[e]];  // clamped address, unconditional load
-    const float* uc = ub + k * ustride;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i;  // (xi, co, half): 16 x 64 x 2 chunks of 16 B
-      const int xi = idx >> 7, rem = idx & 127;
-      r.us[i] = *reinterpret_cast<const f32x4*>(uc + (long long)xi * p.Cout * 8 + rem * 4);
-    }
+    for (int t = 0; t < 4; ++t) glds16(uc + uoff[t], su + (4 * wave + t) * 256);
+    glds16(p.x + roff[0] + cr * kCK, sr + wave * 256);
+    if (wave + 8 < kRDma) glds16(p.x + roff[1] + cr * kCK, sr + (wave + 8) * 256);
   };
-  auto commit = [&](Stage& r, float* st) {
+
+  // transform item: channel tc of tile tt; zero-padding positions of its 4x4 patch
+  const int tc = tid & 7, tt = tid >> 3;
+  const int tbase = ((2 * (tt >> 3)) * kRP + 2 * (tt & 7)) * kCK + tc;
+  const int vdst = swz(tt, tc >> 2) + (tc & 3);
+  unsigned zmask = 0;
+  if (p.zero) {
+    const int y0 = 2 * (by * kT + (tt >> 3)) - P, x0 = 2 * (bx * kT + (tt & 7)) - P;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (y0 + i < 0 || y0 + i >= p.H || x0 + j < 0 || x0 + j >= p.W) zmask |= 1u << (4 * i + j);
+  }
+  auto transform = [&](const float* sr, float* sv) {
 #if WINO_DBG & 4
     return;
 #endif
-    // zero padding applied here, not at the load: nothing consumes the loads before the MFMAs,
-    // so they stay in flight across them (a select next to the load made the compiler wait)
     float d[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) d[e] = inb[e] ? r.d[e] : 0.f;
-    // V = B^T d B
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = sr[tbase + (i * kRP + j) * kCK];
+        d[4 * i + j] = (zmask >> (4 * i + j)) & 1 ? 0.f : v;
+      }
     float t[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -141,116 +169,106 @@ __global__ void __launch_bounds__(256, 1) wino_kernel(const WinoP p) {
       t[2 * 4 + j] = d[2 * 4 + j] - d[1 * 4 + j];
       t[3 * 4 + j] = d[1 * 4 + j] - d[3 * 4 + j];
     }
-    float* sv = st + tt * kLR + tc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float v0 = t[4 * i + 0] - t[4 * i + 2];
-      const float v1 = t[4 * i + 1] + t[4 * i + 2];
-      const float v2 = t[4 * i + 2] - t[4 * i + 1];
-      const float v3 = t[4 * i + 1] - t[4 * i + 3];
-      sv[(4 * i + 0) * kTT * kLR] = v0;
-      sv[(4 * i + 1) * kTT * kLR] = v1;
-      sv[(4 * i + 2) * kTT * kLR] = v2;
-      sv[(4 * i + 3) * kTT * kLR] = v3;
-    }
-    float* su = st + kVS;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i;
-      const int xi = idx >> 7, co = (idx >> 1) & 63, half = idx & 1;
-      *reinterpret_cast<f32x4*>(su + (xi * kCO + co) * kLR + 4 * half) = r.us[i];
+      sv[(4 * i + 0) * kTT * kCK + vdst] = t[4 * i + 0] - t[4 * i + 2];
+      sv[(4 * i + 1) * kTT * kCK + vdst] = t[4 * i + 1] + t[4 * i + 2];
+      sv[(4 * i + 2) * kTT * kCK + vdst] = t[4 * i + 2] - t[4 * i + 1];
+      sv[(4 * i + 3) * kTT * kCK + vdst] = t[4 * i + 1] - t[4 * i + 3];
     }
   };
 
-  f32x16 acc[4][2];
+  f32x16 acc[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int x = 0; x < 8; ++x)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][n][e] = 0.f;
-
-  auto mfmas = [&](const float* st) {
+    for (int q = 0; q < 16; ++q) acc[x][q] = 0.f;
+  // operands: A rows = tiles 32 th + r32, B rows = channels 32 ch + r32, positions 8e + x;
+  // k-step s of lane half h takes channel 4h + s
+  const int arow = swz(32 * th + r32, h) + 8 * e * (kTT * kCK), brow = swz(32 * ch + r32, h) + 8 * e * (kCO * kCK);
+  auto mfmas = [&](const float* sv, const float* su) {
 #if WINO_DBG & 1
     return;
 #endif
-    f32x4 av[4], bv[4][2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int xi = 4 * wave + j;
-      av[j] = *reinterpret_cast<const f32x4*>(st + (xi * kTT + r32) * kLR + 4 * h);
+    for (int x = 0; x < 8; ++x) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(sv + x * (kTT * kCK) + arow);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(su + x * (kCO * kCK) + brow);
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-        bv[j][n] = *reinterpret_cast<const f32x4*>(st + kVS + (xi * kCO + 32 * n + r32) * kLR + 4 * h);
+      for (int s = 0; s < 4; ++s) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x], 0, 0, 0);
     }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[j][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j][s], bv[j][n][s], acc[j][n], 0, 0, 0);
   };
-  // Two chunks of loads in flight (one MFMA phase does not cover an L2-miss latency): chunk c is
-  // staged in register set c & 1; step k runs chunk k's MFMAs, then commits chunk k+1 (loaded
-  // two steps earlier) and reuses its registers for chunk k+3.  The loop is unrolled by two so
-  // the register sets stay static.
-  Stage r0, r1;
-  float* buf0 = lds;
-  float* buf1 = lds + kStage;
-  issue(r0, 0);
-  commit(r0, buf0);
-  issue(r1, 1);
-  issue(r0, 2);
-  __syncthreads();
-  auto step = [&](const float* cur, Stage& r, float* nxt, int knext) {
+  auto publish = [&]() {  // this wave's DMA landed, then the workgroup barrier
     __builtin_amdgcn_sched_barrier(0);
-    mfmas(cur);
-    __builtin_amdgcn_sched_barrier(0);
-    commit(r, nxt);
-    issue(r, knext);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  for (int k = 0; k + 1 < nck; k += 2) {
-    step(buf0, r1, buf1, k + 3);
-    step(buf1, r0, buf0, k + 4);
-  }
-  if (nck & 1) mfmas(buf0);
-  __syncthreads();
 
-  // row partials P_w[q] = sum_j M[w][j] A[j][q]  (A^T = [[1,1,1,0],[0,1,-1,-1]])
-  float* ex = lds;  // [w*2+q][tile][kLE]
-#pragma unroll
-  for (int n = 0; n < 2; ++n)
+  // prologue: U(0) and raw(0) -> transform into V[0]; raw(1) in R[1]
+  dma(0, sU(0), 0, sR(0));
+  dma(0, sU(0), 1, sR(1));
+  publish();
+  transform(sR(0), sV(0));
+  __syncthreads();
+  // chunk k: DMA of U(k+1) into U[(k+1)&1] and raw(k+2) into R[k&1]; MFMAs on V/U[k&1]; the
+  // transform of raw(k+1) into V[(k+1)&1]; one barrier
+  for (int k = 0; k < nck; ++k) {
+    const int c = k & 1, n = c ^ 1;
+    dma(k + 1, sU(n), k + 2, sR(c));
+    mfmas(sV(c), sU(c));
+    transform(sR(n), sV(n));
+    publish();
+  }
+
+  // output transform Y = A^T M A (A^T = [[1,1,1,0],[0,1,-1,-1]]): row partials
+  // P_i[q] = sum_j M[i][j] A[j][q]; Y[0][q] = P0 + P1 + P2, Y[1][q] = P1 - P2 - P3.  Waves
+  // 4-7 (rows 2, 3) hand their share (P2, -P2 - P3) to waves 0-3 through LDS.
+  float* ex = lds + (wave & 3) * (16 * 4 * 64) + lane;  // [w&3][r][4][64 lanes] (64 KiB)
+  static_assert(4 * 16 * 4 * 64 <= 2 * kVS, "epilogue exchange must fit sV");
+  if (e) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int tile = (r & 3) + 8 * (r >> 2) + 4 * h, co = 32 * n + r32;
-      const float m0 = acc[0][n][r], m1 = acc[1][n][r], m2 = acc[2][n][r], m3 = acc[3][n][r];
-      ex[((2 * wave + 0) * kTT + tile) * kLE + co] = m0 + m1 + m2;
-      ex[((2 * wave + 1) * kTT + tile) * kLE + co] = m1 - m2 - m3;
-    }
-  __syncthreads();
-  const int co = tid & 63;
-  const float bias = p.bias ? p.bias[co0 + co] : 0.f;
+      float m[2][2];
 #pragma unroll
-  for (int it = 0; it < kTT / 4; ++it) {
-    const int tile = (tid >> 6) + 4 * it;
-    const int oy0 = 2 * (by * kTY + (tile >> 3)), ox0 = 2 * (bx * kTX + (tile & 7));
+      for (int i = 0; i < 2; ++i) {
+        const float m0 = acc[4 * i][r], m1 = acc[4 * i + 1][r], m2 = acc[4 * i + 2][r], m3 = acc[4 * i + 3][r];
+        m[i][0] = m0 + m1 + m2;
+        m[i][1] = m1 - m2 - m3;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ex[(r * 4 + 2 * q) * 64] = m[0][q];
+        ex[(r * 4 + 2 * q + 1) * 64] = -m[0][q] - m[1][q];
+      }
+    }
+  }
+  __syncthreads();
+  if (e) return;
+  const int co = co0 + 32 * ch + r32;
+  const float bias = p.bias ? p.bias[co] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int tile = 32 * th + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float m[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float m0 = acc[4 * i][r], m1 = acc[4 * i + 1][r], m2 = acc[4 * i + 2][r], m3 = acc[4 * i + 3][r];
+      m[i][0] = m0 + m1 + m2;
+      m[i][1] = m1 - m2 - m3;
+    }
+    const int oy0 = 2 * (by * kT + (tile >> 3)), ox0 = 2 * (bx * kT + (tile & 7));
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const float p0 = ex[((0 + q) * kTT + tile) * kLE + co];
-      const float p1 = ex[((2 + q) * kTT + tile) * kLE + co];
-      const float p2 = ex[((4 + q) * kTT + tile) * kLE + co];
-      const float p3 = ex[((6 + q) * kTT + tile) * kLE + co];
-      float y0 = p0 + p1 + p2 + bias, y1 = p1 - p2 - p3 + bias;
+      float y0 = m[0][q] + m[1][q] + ex[(r * 4 + 2 * q) * 64] + bias;
+      float y1 = m[1][q] + ex[(r * 4 + 2 * q + 1) * 64] + bias;
       if (p.relu) {
         y0 = fmaxf(y0, 0.f);
         y1 = fmaxf(y1, 0.f);
       }
       const int ox = ox0 + q;
       if (ox < p.Wo) {
-        if (oy0 < p.Ho) p.y[((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co0 + co] = y0;
-        if (oy0 + 1 < p.Ho) p.y[((long long)(b * p.Ho + oy0 + 1) * p.Wo + ox) * p.ldc + co0 + co] = y1;
+        if (oy0 < p.Ho) p.y[((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co] = y0;
+        if (oy0 + 1 < p.Ho) p.y[((long long)(b * p.Ho + oy0 + 1) * p.Wo + ox) * p.ldc + co] = y1;
       }
     }
   }
@@ -273,13 +291,13 @@ __global__ void wino_weights_kernel(const float* __restrict__ w, float* __restri
     gg[2 * 3 + kx] = 0.5f * (a - bb + c);
     gg[3 * 3 + kx] = c;
   }
-  float* ub = u + ((long long)(ci >> 3) * 16 * Cout + co) * 8 + (ci & 7);
+  float* ub = u + ((long long)(ci / kCK) * 16 * Cout + co) * kCK + (ci % kCK);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float a = gg[3 * r], bb = gg[3 * r + 1], c = gg[3 * r + 2];
     const float v[4] = {a, 0.5f * (a + bb + c), 0.5f * (a - bb + c), c};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ub[(long long)(4 * r + j) * Cout * 8] = v[j];
+    for (int j = 0; j < 4; ++j) ub[(long long)(4 * r + j) * Cout * kCK] = v[j];
   }
 }
 }  // namespace
@@ -289,7 +307,7 @@ __global__ void wino_weights_kernel(const float* __restrict__ w, float* __restri
 using namespace mhada;
 
 extern "C" int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, mhada_stream_t s_) {
-  if (!w || !u || Cout <= 0 || Cin <= 0 || Cin % 8) return fail("mhada_wino_weights: bad args (Cin % 8 == 0)");
+  if (!w || !u || Cout <= 0 || Cin <= 0 || Cin % kCK) return fail("mhada_wino_weights: bad args (Cin % 8 == 0)");
   const long long n = (long long)Cout * Cin;
   hipLaunchKernelGGL(wino_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s_, w, u,
                      Cout, Cin);
@@ -305,6 +323,7 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   if (pad_mode != MHADA_PAD_REFLECT && pad_mode != MHADA_PAD_ZERO) return fail("mhada_conv3x3_wino: bad pad_mode");
   if (pad_mode == MHADA_PAD_ZERO && pad != 1 && pad != 2) return fail("mhada_conv3x3_wino: zero pad must be 1 or 2");
   if (ldc < Cout) return fail("mhada_conv3x3_wino: ldc < Cout");
+  if (((uintptr_t)x | (uintptr_t)u) & 15) return fail("mhada_conv3x3_wino: x and u must be 16-byte aligned");
   WinoP p;
   p.x = x; p.u = u; p.bias = bias; p.y = y;
   p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
@@ -315,13 +334,13 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   p.relu = relu;
   p.ldc = ldc;
   const int TY = (p.Ho + 1) / 2, TX = (p.Wo + 1) / 2;
-  p.nby = (TY + kTY - 1) / kTY;
-  p.nbx = (TX + kTX - 1) / kTX;
+  p.nby = (TY + kT - 1) / kT;
+  p.nbx = (TX + kT - 1) / kT;
   p.nbn = Cout / kCO;
   const long long nblk = (long long)B * p.nby * p.nbx * p.nbn;
   if (nblk > (1LL << 31) - 1 || (long long)B * H * W * Cin > (1LL << 31) - 1)
     return fail("mhada_conv3x3_wino: problem too large for 32-bit indexing");
   p.nblk = (int)nblk;
-  hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(256), 0, (hipStream_t)s_, p);
+  hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
   return check_launch("mhada_conv3x3_wino");
 }

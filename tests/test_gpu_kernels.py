@@ -111,7 +111,8 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
 @pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
 @pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
                                               (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64),
-                                              (1, 16, 16, 512, 256, 256), (2, 2, 5, 24, 192, 196)])
+                                              (1, 16, 16, 512, 256, 256), (2, 2, 5, 24, 192, 196),
+                                              (1, 40, 36, 96, 64, 64)])
 def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
     """fp32 Winograd F(2x2,3x3) (wino.hip) against fp64 conv2d: reflect / zero padding 1 / the
     pad-2 full correlation, odd and tiny output grids (partial tiles), channel-padded outputs
