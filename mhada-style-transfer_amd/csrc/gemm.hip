@@ -1004,11 +1004,12 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
     return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
   }
   if constexpr (sizeof(TC) == 4) {
-    // persistent ping-pong (256x256 tiles) when there are at least as many tiles as CUs (below
-    // that the 128x128 kernel keeps more of the chip busy); tuning gemm_pp / gemm_persist = 0 disable
+    // persistent ping-pong (256x256 tiles) when the tiles fill at least 7/8 of the CUs (below
+    // that the 128x128 kernel keeps more of the chip busy; the 1080p frame's N = 512 GEMMs have
+    // 254 tiles); tuning gemm_pp / gemm_persist = 0 disable
     if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3 || AMODE == MHADA_A_CONV3X3_ZERO)) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
-      if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && t256 >= num_cus() && pp_enabled() && persist_enabled() &&
+      if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE))
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)

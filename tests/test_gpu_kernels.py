@@ -35,6 +35,7 @@ def test_library_is_the_native_one():
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(100, 96, 64), (1024, 1536, 512), (333, 512, 2048), (4096, 64, 64), (17, 2048, 512),
+                                   (32400, 512, 2048), (32400, 512, 512),
                                    (1000, 384, 576), (8192, 512, 64), (2000, 128, 512), (700, 100, 256)])
 def test_linear(cdt, M, N, K):
     x = rnd(M, K, seed=1, dtype=cdt)
