@@ -166,6 +166,14 @@ int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const f
 int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
                          const float* dmo, const float* dd, float* dq, float* dk, float* dv,
                          int BH, int Nc, int Ns, mhada_stream_t stream);
+/* The dK / dV' half of mhada_attn_train_bwd, optionally spilling dS (the gradient of the
+ * natural-unit logits) to ds [BH][Nc][Ns] fp32 (NULL: no spill).  With the spill, dQ = dS K is a
+ * plain batched GEMM (mhada_gemm with W = K^T) instead of the query-stationary kernel that
+ * recomputes S and dA: 896 instead of 1280 FLOP per (query, key, head), for 8 B of HBM traffic
+ * per (query, key, head) — the trade the 288 GB / 8 TB/s part makes cheaply. */
+int mhada_attn_train_dkv(const float* q, const float* k, const float* v, const float* lse, const float* dmo,
+                         const float* dd, float* dk, float* dv, float* ds, int BH, int Nc, int Ns,
+                         mhada_stream_t stream);
 
 /* Last decoder layer (conv.py:96, ConvReLU(64, 3)): ReflectionPad2d(1) + conv3x3 Cin->3 +
  * bias + ReLU on NHWC x [B][H][W][Cin] (dtype), written NCHW fp32 y [B][3][H][W] — the

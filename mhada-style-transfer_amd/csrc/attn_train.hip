@@ -54,8 +54,19 @@ struct TrainP {
   float* dq;         // [BH][Nc][64]
   float* dk;         // [BH][Ns][64]
   float* dv;         // [BH][Ns][64]
+  float* ds;         // [BH][Nc][Ns] dS spill (dQ = dS K as a GEMM), or null
   int Nc, Ns, nb, nblk;  // nb = row blocks per (b, h)
 };
+
+// Workgroup barrier for the LDS hand-off only: __syncthreads() also acts as a release fence
+// that drains every outstanding global store (vmcnt counts stores on CDNA4), which would
+// serialise the dS spill stores with the next tile.
+MHADA_DEV void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // Register-staged copy of rows [r0, r0+TT) of a [n][W] matrix (zero rows past n) into a padded
 // LDS tile: load() issues the global reads one tile ahead, store() writes them after the
@@ -373,6 +384,12 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
       P[r] = __builtin_amdgcn_exp2f(S[r] - sL[cb][qi]);
       dS[r] = P[r] * (dA[r] - sD[cb][qi]);
     }
+    if (p.ds) {  // spill dS [q][key]: for each register the 32 lanes of a half write 128 B
+      float* dsr = p.ds + (bh * p.Nc + t * TT) * (long long)p.Ns + key;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kv && t * TT + acc_row(r, h) < p.Nc) dsr[(long long)acc_row(r, h) * p.Ns] = dS[r];
+    }
     // G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -386,7 +403,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
       dK[1] = mfma(qq[32], dS[r], dK[1]);
     }
     if (nxt) store(cb ^ 1);
-    __syncthreads();
+    lds_barrier();
   }
   if (!kv) return;
   const long long row = bh * p.Ns + key;
@@ -452,4 +469,17 @@ extern "C" int mhada_attn_train_bwd(const float* q, const float* k, const float*
   // and measured the same, tools/train_attn_bench.py)
   hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   return check_launch("mhada_attn_train_bwd");
+}
+
+extern "C" int mhada_attn_train_dkv(const float* q, const float* k, const float* v, const float* lse,
+                                    const float* dmo, const float* dd, float* dk, float* dv, float* ds, int BH,
+                                    int Nc, int Ns, mhada_stream_t s_) {
+  if (!q || !k || !v || !lse || !dmo || !dd || !dk || !dv || BH <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_train_dkv: bad args");
+  TrainP p = {};
+  p.q = q; p.k = k; p.v = v; p.lse = const_cast<float*>(lse); p.dmo = dmo; p.dd = dd; p.dk = dk; p.dv = dv;
+  p.ds = ds; p.Nc = Nc; p.Ns = Ns;
+  if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_dkv: grid too large");
+  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
+  return check_launch("mhada_attn_train_dkv");
 }

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_bwd": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
+    "mhada_attn_train_dkv": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_upsample2x": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_warp": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),

@@ -325,19 +325,39 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     return out, mo, lse
 
 
-def attn_train_bwd(q, k, v, lse, dmo, dd):
-    """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64)."""
+# Largest dS spill (BH * Nc * Ns fp32) the training backward takes (512^2 batch 8: 4.3 GB, reused
+# across the step's attention calls by the caching allocator); larger problems, or spill=False,
+# recompute S and dA in the query-stationary dQ kernel instead.
+DS_SPILL_BYTES = 16 << 30
+
+
+def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
+    """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64).  With the dS spill
+    (default when it fits DS_SPILL_BYTES and Ns % 4 == 0): ``mhada_attn_train_dkv`` writes dS and
+    dQ = dS K runs as one batched GEMM (896 instead of 1280 FLOP per query-key-head pair)."""
     _rows64(q, k, v, lse, dmo, dd)
     BH, Nc, _ = q.shape
     Ns = k.shape[1]
     if lse.shape != (BH, Nc) or dmo.shape != (BH, Nc, 128) or dd.shape != (BH, Nc) or k.shape != (BH, Ns, 64) \
             or v.shape != k.shape:
         raise ValueError("attn_train_bwd: bad shapes")
+    if spill is None:
+        spill = Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)
-    _call("mhada_attn_train_bwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
-          dd.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), BH, Nc, Ns)
+    if not spill:
+        _call("mhada_attn_train_bwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
+              dd.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), BH, Nc, Ns)
+        return dq, dk, dv
+    if Ns % 4:
+        raise ValueError("attn_train_bwd: the dS spill needs Ns % 4 == 0")
+    ds = torch.empty(BH, Nc, Ns, device=q.device, dtype=torch.float32)
+    _call("mhada_attn_train_dkv", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
+          dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, Nc, Ns)
+    kt = k.transpose(1, 2).contiguous()  # W[n = d][k = key] of the NT GEMM
+    gemm(a=ds, w=kt, c=dq, M=Nc, N=64, K=Ns, compute=torch.float32, lda=Ns, sa=(Nc * Ns, 0), nb=(BH, 1),
+         ldw=Ns, sw=(64 * Ns, 0), ldc=64, sc=(Nc * 64, 0))
     return dq, dk, dv
 
 

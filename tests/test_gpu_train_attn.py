@@ -57,6 +57,24 @@ def test_attn_train_fwd_bwd_vs_fp64(BH, Nc, Ns, scale):
         assert err < max(2e-4, 3 * err32), (name, err, err32)
 
 
+@pytest.mark.parametrize("BH,Nc,Ns", [(2, 128, 64), (1, 37, 300), (3, 500, 256), (2, 33, 4)])
+def test_attn_train_bwd_ds_spill_matches_recompute(BH, Nc, Ns):
+    """dS spilled by the dK/dV' kernel + dQ = dS K as a batched GEMM (ops.attn_train_bwd's default)
+    against the recompute path (query-stationary dQ kernel): dK, dV' bit-identical (same kernel,
+    same order), dQ to fp32 summation order."""
+    g = torch.Generator().manual_seed(BH * 1000 + Nc + Ns)
+    q, k, v = (torch.randn(BH, n, 64, generator=g).cuda() * 0.5 for n in (Nc, Ns, Ns))
+    v = (v - v.mean(dim=1, keepdim=True)).contiguous()
+    x = torch.randn(BH, Nc, 64, generator=g).cuda()
+    out, mo, lse = ops.attn_train_fwd(q, k, v, x)
+    dmo = torch.randn(BH, Nc, 128, generator=g).cuda()
+    dd = (dmo * mo).sum(-1).contiguous()
+    a = ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=True)
+    b = ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=False)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert _rel(a[0].double(), b[0].double()) < 1e-5
+
+
 def test_attn_train_lse_and_stats():
     g = torch.Generator().manual_seed(5)
     q, x = torch.randn(2, 96, 64, generator=g), torch.randn(2, 96, 64, generator=g)

@@ -33,6 +33,8 @@ def timeit(fn):
 
 
 tf = timeit(lambda: ops.attn_train_fwd(q, k, v, x))
-tb = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd))
+tb = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=False))
+ts = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=True))
 print(f"fwd {tf:.3f} ms ({384 * pairs / tf / 1e9:.1f} TF)  "
-      f"bwd {tb:.3f} ms ({1280 * pairs / tb / 1e9:.1f} TF)")
+      f"bwd recompute {tb:.3f} ms ({1280 * pairs / tb / 1e9:.1f} TF)  "
+      f"bwd dS spill {ts:.3f} ms ({896 * pairs / ts / 1e9:.1f} TF of the 896-FLOP form)")
