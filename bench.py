@@ -255,7 +255,9 @@ def run_train(steps, warmup, rank, world):
             "config": {"workload": "train step (4 ViT + 3 AdaFormer + 5 VGG19 fwd, 4 losses, bwd, Adam)",
                        "global_batch": batch * world, "resolution": 512,
                        "parallelism": f"dp{world} (RCCL grad all-reduce)" if world > 1 else "single GPU",
-                       "engine": "MHAda attention fwd+bwd on HIP (attn_train.hip); rest PyTorch-ROCm autograd (DESIGN.md §6)"},
+                       "engine": "every conv / linear / attention fwd+bwd on HIP kernels (Winograd fp32 convs, "
+                                 "dS-spill attention backward, TN weight-gradient GEMMs); losses, Adam and glue on "
+                                 "PyTorch-ROCm (DESIGN.md §3b)"},
             "last_losses": last}
 
 
