@@ -203,6 +203,204 @@ __global__ void __launch_bounds__(64 * W) loss_attn_kernel(const LossAttnP p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// LDS-staged form for d_qk <= 448 with d_v = 256 (the relu3_1 level of the loss: d_qk 448,
+// N = (H/4)^2 — 16384 tokens at 512^2, 90 % of the loss-attention time).  The kernel above reads
+// K and V straight from L2 per lane (each wave instruction touches 32 key rows); here a workgroup
+// of 8 waves = 2 query groups x the 4 d-slices shares one K / V tile staged through LDS by
+// coalesced 16-B loads (whole 32-row tiles are contiguous in memory), issued a tile ahead into
+// registers: half the L2 stream per query and none of the scattered row reads.  Per 32-key tile:
+//   commit V(t) -> sV; issue loads of K(t+1), V(t+1); partial S^T from sK -> sS; barrier;
+//   fixed-order sum of the 4 partials, softmax, P V / P V^2 from sV; commit K(t+1) -> sK; barrier
+// (single-buffered sK / sV / sS: each buffer's last reader finishes before the barrier that
+// precedes its next writer).  K rows padded to 4*dsl + 4 floats (= 4 mod 64 words: conflict-free
+// ds_read_b128 down 32 rows), V rows to 260.
+// ---------------------------------------------------------------------------------------
+template <int ACT>
+__global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
+  constexpr int W = 4, DH = 56, NB = 2, VLD = 260;  // d slice <= 112 = 2 x DH
+  constexpr int KLDMAX = 452;
+  __shared__ __attribute__((aligned(16))) float sK[32 * KLDMAX];
+  __shared__ __attribute__((aligned(16))) float sV[32 * VLD];
+  __shared__ __attribute__((aligned(16))) float sS[2][W][16][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qg = wave >> 2, ws = wave & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int nqb = (p.Nq + 63) / 64;
+  const int b = t0 / nqb, qb = t0 - b * nqb;
+  const int q = qb * 64 + qg * 32 + r32;
+  const int qc = min(q, p.Nq - 1);
+  const int KLD = 4 * p.dsl + 4;
+  const int dh = p.dsl / 2, dbase = ws * p.dsl + h * dh;
+  float qreg[DH];
+  {
+    const float* qrow = p.q + ((long long)b * p.Nq + qc) * p.Dqk;
+#pragma unroll
+    for (int s = 0; s < DH; s += 4) {
+      const f32x4 v4 = (s < dh && dbase + s < p.Dqk) ? *reinterpret_cast<const f32x4*>(qrow + dbase + s)
+                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qreg[s + e] = v4[e];
+    }
+  }
+  // K columns [Dqk, 4 dsl) stay zero (never written by the tile commits)
+  for (int i = tid; i < 32 * (KLD - p.Dqk); i += 512) {
+    const int row = i / (KLD - p.Dqk), col = p.Dqk + i % (KLD - p.Dqk);
+    sK[row * KLD + col] = 0.f;
+  }
+  const float* kb = p.k + (long long)b * p.Ns * p.Dqk;
+  const float* vb = p.v + (long long)b * p.Ns * p.Dv;
+  // tile staging: K tile = 32 rows x Dqk/4 16-B chunks, V tile = 32 x 64 chunks (clamped rows)
+  const int kcr = p.Dqk / 4, kch = 32 * kcr;
+  constexpr int KR = (32 * 112 + 511) / 512;  // <= 7 chunks per thread (d_qk <= 448)
+  f32x4 rk[KR], rv[4];
+  auto issue = [&](int key0) {
+#pragma unroll
+    for (int i = 0; i < KR; ++i) {
+      const int c = min(tid + 512 * i, kch - 1), row = c / kcr, col = c - row * kcr;
+      rk[i] = *reinterpret_cast<const f32x4*>(kb + (long long)min(key0 + row, p.Ns - 1) * p.Dqk + 4 * col);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 512 * i, row = c >> 6, col = c & 63;
+      rv[i] = *reinterpret_cast<const f32x4*>(vb + (long long)min(key0 + row, p.Ns - 1) * p.Dv + 4 * col);
+    }
+  };
+  auto commit_k = [&]() {
+#pragma unroll
+    for (int i = 0; i < KR; ++i) {
+      const int c = min(tid + 512 * i, kch - 1), row = c / kcr, col = c - row * kcr;
+      *reinterpret_cast<f32x4*>(sK + row * KLD + 4 * col) = rk[i];
+    }
+  };
+  auto commit_v = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 512 * i, row = c >> 6, col = c & 63;
+      *reinterpret_cast<f32x4*>(sV + row * VLD + 4 * col) = rv[i];
+    }
+  };
+
+  f32x16 O[2 * NB];
+#pragma unroll
+  for (int i = 0; i < 2 * NB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[i][e] = 0.f;
+  float m2 = -INFINITY, l = 0.f;
+
+  const int ntile = (p.Ns + 31) / 32;
+  issue(0);
+  commit_k();
+  __syncthreads();
+  for (int tt = 0; tt < ntile; ++tt) {
+    const int key0 = tt * 32;
+    commit_v();  // V(tt): sV's readers (P V of tile tt-1) passed the last barrier
+    issue(min(tt + 1, ntile - 1) * 32);
+    // ---- partial S^T[key][q] over this wave's d slice, K from LDS
+    f32x16 S;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) S[e] = 0.f;
+    {
+      const float* kr = sK + r32 * KLD + dbase;
+#pragma unroll
+      for (int s = 0; s < DH; s += 4) {
+        if (s < dh) {  // wave-uniform
+          const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + s);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) S = __builtin_amdgcn_mfma_f32_32x32x2f32(k4[e], qreg[s + e], S, 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sS[qg][ws][r][lane] = S[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float a = sS[qg][0][r][lane];
+#pragma unroll
+      for (int w = 1; w < W; ++w) a += sS[qg][w][r][lane];
+      S[r] = a;
+    }
+    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        S[r] = key < p.Ns ? S[r] * kLog2e : -INFINITY;
+        mx = fmaxf(mx, S[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (mx > m2 + kLossRescaleThr || tt == 0) {
+        const float mn = fmaxf(m2, mx);
+        const float alpha = m2 == -INFINITY ? 0.f : exp2f(m2 - mn);
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 2 * NB; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) O[i][e] *= alpha;
+        m2 = mn;
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        S[r] = exp2f(S[r] - m2);
+        sum += S[r];
+      }
+      l += sum;
+    } else {
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        S[r] = key < p.Ns ? S[r] + 1.0f : 0.f;
+        sum += S[r];
+      }
+      l += sum;
+    }
+    // ---- O^T[dv][q] += V^T P^T and (V^2)^T P^T, V from LDS
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* vr = sV + ((r & 3) + 8 * (r >> 2) + 4 * h) * VLD + ws * 64 + r32;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const float vx = vr[32 * j];
+        O[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vx, S[r], O[j], 0, 0, 0);
+        O[NB + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vx * vx, S[r], O[NB + j], 0, 0, 0);
+      }
+    }
+    commit_k();  // K(tt+1): every wave's S^T reads of sK ended before the barrier above
+    __syncthreads();
+  }
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q >= p.Nq) return;
+  const float inv = 1.f / lt;
+  const int dvb = ws * 64;
+  const float* xr = p.x + ((long long)b * p.Nq + q) * p.Dv + dvb;
+  const float* mu = p.x_mu + (long long)b * p.Dv + dvb;
+  const float* rs = p.x_rs + (long long)b * p.Dv + dvb;
+  float* orow = p.out + ((long long)b * p.Nq + q) * p.Dv + dvb;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dv = 32 * j + 8 * g + 4 * h;
+      const f32x4 xx = *reinterpret_cast<const f32x4*>(xr + dv);
+      const f32x4 mm = *reinterpret_cast<const f32x4*>(mu + dv);
+      const f32x4 rr = *reinterpret_cast<const f32x4*>(rs + dv);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[j][4 * g + e] * inv;
+        const float e2 = O[NB + j][4 * g + e] * inv;
+        o[e] = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f)) * ((xx[e] - mm[e]) * rr[e]) + m1;
+      }
+      *reinterpret_cast<f32x4*>(orow + dv) = o;
+    }
+}
+
 // InstanceNorm applied to token rows: out[b][n][c] = (x - mu[b][c]) * rs[b][c]; with unit != 0
 // each normalised row is further divided by its L2 norm (the cosine activation's q/|q|, k/|k|:
 // adaDecoder.py:30-32).  One wave per row.
@@ -273,6 +471,14 @@ extern "C" int mhada_loss_attn(const float* q, const float* k, const float* v, c
   const int W = Dv / 64;
   if (W & (W - 1)) return fail("mhada_loss_attn: d_v / 64 must be 1, 2, 4 or 8");
   p.dsl = (Dqk + W * 8 - 1) / (W * 8) * 8;
+  if (W == 4 && p.dsl <= 112) {  // d_v 256, d_qk <= 448: the LDS-staged form, 64 queries per workgroup
+    const long long nb64 = (long long)B * ((Nq + 63) / 64);
+    if (activation == MHADA_ACT_SOFTMAX)
+      hipLaunchKernelGGL(loss_attn_lds_kernel<MHADA_ACT_SOFTMAX>, dim3((unsigned)nb64), dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL(loss_attn_lds_kernel<MHADA_ACT_COSINE>, dim3((unsigned)nb64), dim3(512), 0, s, p);
+    return check_launch("mhada_loss_attn");
+  }
   const dim3 grid((unsigned)nblk);
 #define LA(ACT, WW) hipLaunchKernelGGL((loss_attn_kernel<ACT, WW, 64, 64>), grid, dim3(64 * WW), 0, s, p)
   if (activation == MHADA_ACT_SOFTMAX) {

@@ -202,7 +202,8 @@ def _loss_attn_ref(c_x, s_x, c_1x, s_1x, act):
 @pytest.mark.parametrize("act", ["softmax", "cosine"])
 @pytest.mark.parametrize("B,dqk,dv,hc,wc,hs,ws", [(2, 448, 256, 16, 16, 16, 16), (1, 960, 512, 8, 8, 8, 8),
                                                    (2, 1472, 512, 4, 4, 4, 4), (1, 448, 256, 9, 7, 5, 11),
-                                                   (1, 96, 64, 20, 3, 6, 6)])
+                                                   (1, 96, 64, 20, 3, 6, 6), (2, 448, 256, 40, 33, 21, 37),
+                                                   (1, 96, 256, 11, 13, 9, 10)])
 def test_loss_attn_against_fp64(act, B, dqk, dv, hc, wc, hs, ws):
     """The three local-feature-loss shapes (relu3/4/5 channel counts) plus ragged token counts;
     VGG-like non-negative features (post-ReLU), fp32 kernel vs fp64 reference: 1e-4 relative."""
