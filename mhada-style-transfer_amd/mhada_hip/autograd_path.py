@@ -148,47 +148,48 @@ def _fused_train_attn(blk, fc) -> bool:
 
 def _head_proj(mods, t: torch.Tensor, H: int) -> torch.Tensor:
     """Per-head 1x1 convs (adaDecoder.py:188-190, f/g/h_list[i] on channel slice i) on the
-    modules' own parameters: (B, 64H, h, w) -> (B*H, h*w, 64).  On a ROCm device: one token GEMM
-    with the block-diagonal (64H x 64H) weight on the HIP training kernels (train_fns.linear) —
-    8x the FLOPs of the per-head products, but ~2 us of MFMA time per call against ~0.4 ms for
-    the vendor library's batched 64x64 kernels; the gradient reaches each head's weight through
-    block_diag.  On the CPU: a head-batched matmul."""
+    modules' own parameters.  On a ROCm device: ONE grouped GEMM over the heads on the HIP
+    kernels (train_fns.head_proj; the gradients reach each head's weight through torch.stack),
+    (B, 64H, h, w) -> (H*B, h*w, 64) in HEAD-major order.  On the CPU: a head-batched matmul,
+    (B*H, h*w, 64) batch-major.  The attention core treats (head, batch) pairs independently;
+    _heads_rows and the out_conv gather follow the same order."""
     B, C, h, w = t.shape
     d = C // H
     if t.is_cuda:
         from . import train_fns
-        wbd = torch.block_diag(*[m.weight.reshape(d, d) for m in mods])
-        bias = torch.cat([m.bias for m in mods])
+        wst = torch.stack([m.weight.reshape(d, d) for m in mods])
+        bst = torch.stack([m.bias for m in mods])
         rows = t.permute(0, 2, 3, 1).reshape(B * h * w, C)
-        y = train_fns.linear(rows, wbd, bias)
-        return y.view(B, h * w, H, d).permute(0, 2, 1, 3).reshape(B * H, h * w, d)
+        return train_fns.head_proj(rows, wst, bst).view(H * B, h * w, d)
     wgt = torch.stack([m.weight.reshape(d, d) for m in mods], 0)  # (H, out, in)
     bias = torch.stack([m.bias for m in mods], 0).unsqueeze(1)     # (H, 1, out)
     y = torch.matmul(t.reshape(B, H, d, h * w).transpose(2, 3), wgt.transpose(1, 2)) + bias
     return y.reshape(B * H, h * w, d)
 
 
-def _heads_rows(t: torch.Tensor, H: int) -> torch.Tensor:
-    """(B, 64H, h, w) -> (B*H, h*w, 64) contiguous."""
+def _heads_rows(t: torch.Tensor, H: int, head_major: bool = False) -> torch.Tensor:
+    """(B, 64H, h, w) -> (B*H, h*w, 64) contiguous, batch-major or (head_major) (H*B, ...)."""
     B, C, h, w = t.shape
+    if head_major:
+        return t.reshape(B, H, C // H, h * w).permute(1, 0, 3, 2).reshape(H * B, h * w, C // H).contiguous()
     return t.reshape(B, H, C // H, h * w).transpose(2, 3).reshape(B * H, h * w, C // H).contiguous()
 
 
 def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
-    """AdaAttnMultiHead.forward (adaDecoder.py:162-206) with the per-head 1x1 convs batched
-    over heads (hipBLASLt; a groups=8 conv2d took MIOpen's 4.5 ms CK weight-gradient kernel)
-    and the attention on MHAdaAttnFn."""
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206) with the per-head 1x1 convs grouped over
+    heads (on a ROCm device one grouped GEMM each, head-major operands) and the attention on
+    MHAdaAttnFn."""
     B, C, h, w = fc.shape
     H = blk.num_heads
     q = _head_proj(blk.f_list, F.instance_norm(fc), H).contiguous()
     k = _head_proj(blk.g_list, F.instance_norm(fs), H).contiguous()
     v = _head_proj(blk.h_list, fs, H)
     vmu = v.mean(dim=1, keepdim=True)
-    x = _heads_rows(F.instance_norm(fcs), H)
+    x = _heads_rows(F.instance_norm(fcs), H, head_major=fc.is_cuda)
     o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
     if fc.is_cuda:  # out_conv (1x1) as a token GEMM on the HIP kernels
         from . import train_fns
-        rows = o.reshape(B, H, h * w, C // H).permute(0, 2, 1, 3).reshape(B * h * w, C)
+        rows = o.view(H, B * h * w, C // H).permute(1, 0, 2).reshape(B * h * w, C)
         y = train_fns.linear(rows, blk.out_conv.weight.view(C, C), blk.out_conv.bias)
         return y.view(B, h, w, C).permute(0, 3, 1, 2)
     o = o.reshape(B, H, h * w, C // H).transpose(2, 3).reshape(B, C, h, w)

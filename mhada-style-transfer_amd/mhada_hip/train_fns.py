@@ -163,6 +163,51 @@ def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bo
     return LinearFn.apply(x2d, weight, bias, relu)
 
 
+class HeadProjFn(torch.autograd.Function):
+    """The per-head 1x1 convs of AdaAttnMultiHead (adaDecoder.py:143-145,188-190: f/g/h_list[i] on
+    channel slice i) as ONE grouped GEMM over the heads: token rows x [T][H*64], stacked weights
+    [H][64][64] and biases [H][64] -> y [H][T][64] (head-major: the (head, batch) order the
+    training attention takes).  Backward: dX as the grouped GEMM with the transposed head weights
+    (written straight into each head's column block), dW per head on the TN kernel, db a column
+    sum.  1/8 of the block-diagonal 512x512 product's FLOPs in each direction."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        T, C = x.shape
+        H = weight.shape[0]
+        if C != 64 * H or weight.shape[1:] != (64, 64):
+            raise ValueError("HeadProjFn: x [T][64H], weight [H][64][64]")
+        y = torch.empty(H, T, 64, device=x.device, dtype=F32)
+        ops.gemm(a=x, w=weight.detach().contiguous(), c=y, M=T, N=64, K=64, compute=F32, lda=C, sa=(64, 0),
+                 nb=(H, 1), ldw=64, sw=(4096, 0), bias=bias.detach().contiguous(), sb=(64, 0), ldc=64,
+                 sc=(T * 64, 0))
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        T, C = x.shape
+        H = weight.shape[0]
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty(T, C, device=x.device, dtype=F32)
+            ops.gemm(a=gy, w=weight.detach().transpose(1, 2).contiguous(), c=gx, M=T, N=64, K=64, compute=F32,
+                     lda=64, sa=(T * 64, 0), nb=(H, 1), ldw=64, sw=(4096, 0), ldc=C, sc=(64, 0))
+        if ctx.needs_input_grad[1]:
+            gw = torch.stack([ops.gemm_tn(gy[i], x[:, 64 * i:], M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS)
+                              for i in range(H)])
+        if ctx.needs_input_grad[2]:
+            gb = torch.stack([ops.colsum(gy[i]) for i in range(H)])
+        return gx, gw, gb
+
+
+def head_proj(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    return HeadProjFn.apply(x2d, weight, bias)
+
+
 class BatchAxisAttnFn(torch.autograd.Function):
     """The core of nn.MultiheadAttention(batch_first=False) on a (B, N, C) tensor (vit.py:48,59):
     per token and head, softmax over the L = B images of (q/8) k^T, times v.  qkv [L][N][3C]

@@ -330,3 +330,24 @@ def test_batch_axis_attention_fwd_bwd(L):
     ref.backward(g.double())
     assert rel(out, ref) < 1e-6
     assert rel(qkv.grad, q64.grad) < 1e-6
+
+
+@pytest.mark.parametrize("T,H", [(300, 8), (4096, 8), (77, 2)])
+def test_head_proj_grouped_gemm_vs_fp64(T, H):
+    """train_fns.HeadProjFn (the per-head 1x1 convs of adaDecoder.py:188-190 as one grouped GEMM,
+    head-major output) against fp64 autograd of the per-head products: output and the gradients of
+    x, the stacked weights and biases."""
+    from mhada_hip import train_fns
+    x = rnd(T, 64 * H, seed=11)
+    w = rnd(H, 64, 64, scale=0.125, seed=12)
+    b = rnd(H, 64, seed=13)
+    gy = rnd(H, T, 64, seed=14)
+    xs, ws, bs = (t.clone().requires_grad_() for t in (x, w, b))
+    y = train_fns.head_proj(xs, ws, bs)
+    y.backward(gy)
+    xd, wd, bd = (t.double().clone().requires_grad_() for t in (x, w, b))
+    yd = torch.stack([xd[:, 64 * h:64 * h + 64] @ wd[h].T + bd[h] for h in range(H)])
+    yd.backward(gy.double())
+    assert rel(y, yd) < 2e-6
+    for a, r in ((xs.grad, xd.grad), (ws.grad, wd.grad), (bs.grad, bd.grad)):
+        assert rel(a, r) < 2e-6
