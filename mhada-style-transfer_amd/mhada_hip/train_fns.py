@@ -200,7 +200,7 @@ class HeadProjFn(torch.autograd.Function):
             gw = torch.stack([ops.gemm_tn(gy[i], x[:, 64 * i:], M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS)
                               for i in range(H)])
         if ctx.needs_input_grad[2]:
-            gb = torch.stack([ops.colsum(gy[i]) for i in range(H)])
+            gb = gy.sum(dim=1)  # one reduction over the tokens for all heads (8 colsum launches cost more)
         return gx, gw, gb
 
 
