@@ -172,6 +172,7 @@ class HeadProjFn(torch.autograd.Function):
     sum.  1/8 of the block-diagonal 512x512 product's FLOPs in each direction."""
 
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, x, weight, bias):
         x = x.contiguous()
         T, C = x.shape
@@ -186,6 +187,7 @@ class HeadProjFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         T, C = x.shape

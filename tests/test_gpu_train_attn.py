@@ -113,3 +113,23 @@ def test_fused_block_grads_match_autograd_block():
     for i, (a, b) in enumerate(zip(*results)):
         err = (a.double() - b.double()).abs().max().item()
         assert err <= max(1e-3 * b.abs().max().item(), 1e-5 * gmax), (i, err)
+
+
+def test_fused_block_under_autocast_runs_fp32_kernels():
+    """Training under torch.autocast(bf16): the HIP training ops cast their operands to fp32
+    (custom_fwd), so the fused block runs and matches its fp32 result (the bf16
+    projection outputs used to crash the fp32-only kernels)."""
+    blk = load_recipe(network.AdaAttnTransformerMultiHead(), "ada").cuda().adaAttnHead[0]
+    g = torch.Generator().manual_seed(5)
+    fc, fs, fcs = (torch.randn(2, 512, 8, 8, generator=g).cuda().requires_grad_() for _ in range(3))
+    ys = []
+    for amp in (False, True):
+        for t in (fc, fs, fcs, *blk.parameters()):
+            t.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = autograd_path.block_forward(blk, fc, fs, fcs)
+        y.float().sum().backward()
+        ys.append((y.detach().float(), fc.grad.clone()))
+    assert torch.isfinite(ys[1][0]).all() and torch.isfinite(ys[1][1]).all()
+    assert _rel(ys[1][0].double(), ys[0][0].double()) < 5e-2
+    assert _rel(ys[1][1].double(), ys[0][1].double()) < 5e-2
