@@ -23,11 +23,17 @@ imgs = [(seeded_image(8, 512, 512, 100 + i).to(dev), seeded_image(8, 512, 512, 5
 for c, s in imgs[:2]:
     tr.step(c, s)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=False) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
     tr.step(*imgs[2])
     torch.cuda.synchronize()
 out = open(sys.argv[1], "w") if len(sys.argv) > 1 else sys.stdout
 print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60), file=out)
+for op in ("aten::copy_", "aten::add_", "aten::add"):
+    rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key == op]
+    rows.sort(key=lambda e: -e.self_device_time_total)
+    print(f"\n==== {op}: top input shapes by device time", file=out)
+    for e in rows[:15]:
+        print(f"{e.self_device_time_total / 1e3:9.2f} ms  {e.count:5d} calls  {e.input_shapes}", file=out)
 for op in ("aten::copy_", "aten::add", "aten::add_", "aten::cat", "aten::mse_loss_backward", "aten::fill_"):
     rows = [e for e in prof.key_averages(group_by_stack_n=6) if e.key == op]
     rows.sort(key=lambda e: -e.self_device_time_total)
