@@ -181,11 +181,28 @@ def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tens
     MHAdaAttnFn."""
     B, C, h, w = fc.shape
     H = blk.num_heads
-    q = _head_proj(blk.f_list, F.instance_norm(fc), H).contiguous()
-    k = _head_proj(blk.g_list, F.instance_norm(fs), H).contiguous()
-    v = _head_proj(blk.h_list, fs, H)
+    if fc.is_cuda:  # token-major throughout: the features are channels-last NCHW views
+        from . import train_fns
+        d = C // H
+        tok = lambda t: t.permute(0, 2, 3, 1).reshape(t.shape[0], -1, C)  # noqa: E731
+        fct, fst, fcst = tok(fc), tok(fs), tok(fcs)
+        ns = fst.shape[1]
+
+        def proj(mods, rows):
+            wst = torch.stack([m.weight.reshape(d, d) for m in mods])
+            bst = torch.stack([m.bias for m in mods])
+            return train_fns.head_proj(rows, wst, bst)  # [H][rows][d]
+
+        q = proj(blk.f_list, train_fns.instance_norm_tokens(fct).view(B * h * w, C)).view(H * B, h * w, d)
+        k = proj(blk.g_list, train_fns.instance_norm_tokens(fst).view(B * ns, C)).view(H * B, ns, d)
+        v = proj(blk.h_list, fst.reshape(B * ns, C)).view(H * B, ns, d)
+        x = train_fns.instance_norm_tokens(fcst).view(B, h * w, H, d).permute(2, 0, 1, 3).reshape(H * B, h * w, d)
+    else:
+        q = _head_proj(blk.f_list, F.instance_norm(fc), H).contiguous()
+        k = _head_proj(blk.g_list, F.instance_norm(fs), H).contiguous()
+        v = _head_proj(blk.h_list, fs, H)
+        x = _heads_rows(F.instance_norm(fcs), H)
     vmu = v.mean(dim=1, keepdim=True)
-    x = _heads_rows(F.instance_norm(fcs), H, head_major=fc.is_cuda)
     o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
     if fc.is_cuda:  # out_conv (1x1) as a token GEMM on the HIP kernels
         from . import train_fns

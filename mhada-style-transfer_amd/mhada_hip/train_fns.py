@@ -163,6 +163,36 @@ def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bo
     return LinearFn.apply(x2d, weight, bias, relu)
 
 
+class InstanceNormTokensFn(torch.autograd.Function):
+    """F.instance_norm (no affine, eps 1e-5, biased variance; adaDecoder.py:147-149,188-190) on
+    token-major rows x [B][N][C]: mhada_instnorm_stats (fixed-order fp64 partials) +
+    mhada_rows_normalize.  Backward: dx = rstd (dy - mean_N(dy) - y mean_N(dy y)).  Working on the
+    token-major storage of the block's channels-last features avoids the NCHW <-> NHWC copies of
+    aten's instance_norm."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x):
+        x = x.contiguous()
+        mu, rs = ops.instnorm_stats(x)
+        y = ops.rows_normalize(x, mu, rs)
+        ctx.save_for_backward(y, rs)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        y, rs = ctx.saved_tensors
+        dy = dy.contiguous()
+        m1 = dy.mean(dim=1, keepdim=True)
+        m2 = (dy * y).mean(dim=1, keepdim=True)
+        return (dy - m1 - y * m2) * rs.unsqueeze(1)
+
+
+def instance_norm_tokens(x: torch.Tensor) -> torch.Tensor:
+    return InstanceNormTokensFn.apply(x)
+
+
 class HeadProjFn(torch.autograd.Function):
     """The per-head 1x1 convs of AdaAttnMultiHead (adaDecoder.py:143-145,188-190: f/g/h_list[i] on
     channel slice i) as ONE grouped GEMM over the heads: token rows x [T][H*64], stacked weights

@@ -351,3 +351,20 @@ def test_head_proj_grouped_gemm_vs_fp64(T, H):
     assert rel(y, yd) < 2e-6
     for a, r in ((xs.grad, xd.grad), (ws.grad, wd.grad), (bs.grad, bd.grad)):
         assert rel(a, r) < 2e-6
+
+
+@pytest.mark.parametrize("B,N,C", [(2, 300, 512), (8, 4096, 64), (1, 37, 68)])
+def test_instance_norm_tokens_vs_fp64(B, N, C):
+    """train_fns.InstanceNormTokensFn (token-major InstanceNorm, adaDecoder.py:147-149) against
+    fp64 F.instance_norm autograd on the same values in NCHW: output and input gradient."""
+    from mhada_hip import train_fns
+    x = rnd(B, N, C, seed=21) * 3 + 1
+    dy = rnd(B, N, C, seed=22)
+    xs = x.clone().requires_grad_()
+    y = train_fns.instance_norm_tokens(xs)
+    y.backward(dy)
+    xd = x.double().clone().requires_grad_()
+    yd = F.instance_norm(xd.transpose(1, 2), eps=1e-5).transpose(1, 2)
+    yd.backward(dy.double())
+    assert rel(y, yd) < 2e-6
+    assert rel(xs.grad, xd.grad) < 2e-5
