@@ -67,6 +67,10 @@ MHADA_DEV int reflect_clamp(int v, int n) {
 // float offset of the 16-B half `half` (channels 4*half .. 4*half+3) of 32-B row `row`: halves
 // swapped on rows with bit 3 set, so ds_read_b128 of 32 consecutive rows is conflict-free
 MHADA_DEV int swz(int row, int half) { return row * 8 + ((half ^ ((row >> 3) & 1)) << 2); }
+// Raw-patch 16-B slot swizzle (an involution): bit 1 of the slot flips with bit 3, so the
+// transform's ds_read_b32 of 4 tiles x 8 channels (slots s0 + 4 tx + {0, 1}) hit 8 distinct
+// 4-bank groups (ds_read_b32 serves 32 lanes over 32 banks; unswizzled, tiles tx and tx + 2 met).
+MHADA_DEV int rswz(int slot) { return slot ^ (((slot >> 3) & 1) << 1); }
 MHADA_DEV void glds16(const float* src, float* lds) {  // LDS-DMA: lane l -> lds + 16 l bytes
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -101,7 +105,7 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   int roff[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int slot = 64 * (wave + 8 * t) + lane;
+    const int slot = rswz(64 * (wave + 8 * t) + lane);  // logical slot stored at this position
     const int px = min(slot >> 1, kRaw - 1);
     int iy = 2 * by * kT - P + px / kRP, ix = 2 * bx * kT - P + px % kRP;
     if (p.zero) {
@@ -138,7 +142,15 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
 
   // transform item: channel tc of tile tt; zero-padding positions of its 4x4 patch
   const int tc = tid & 7, tt = tid >> 3;
-  const int tbase = ((2 * (tt >> 3)) * kRP + 2 * (tt & 7)) * kCK + tc;
+  // LDS float offsets of the item's 16 raw values (swizzled 16-B slots, see rswz)
+  int roffs[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pix = (2 * (tt >> 3) + i) * kRP + 2 * (tt & 7) + j;
+      roffs[4 * i + j] = rswz(2 * pix + (tc >> 2)) * 4 + (tc & 3);
+    }
   const int vdst = swz(tt, tc >> 2) + (tc & 3);
   unsigned zmask = 0;
   if (p.zero) {
@@ -158,7 +170,7 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float v = sr[tbase + (i * kRP + j) * kCK];
+        const float v = sr[roffs[4 * i + j]];
         d[4 * i + j] = (zmask >> (4 * i + j)) & 1 ? 0.f : v;
       }
     float t[16];
