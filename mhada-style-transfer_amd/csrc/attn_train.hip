@@ -68,10 +68,10 @@ MHADA_DEV void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Register-staged copy of rows [r0, r0+TT) of a [n][W] matrix (zero rows past n) into a padded
-// LDS tile: load() issues the global reads one tile ahead, store() writes them after the
-// current tile's math (one barrier per tile, two LDS buffers).
-template <int NT, int W>
+// Register-staged copy of rows [r0, r0+TT) of a [n][W] matrix (zero rows past n; with CLAMP, r0
+// may lie past n) into a padded LDS tile: load() issues the global reads one tile ahead, store()
+// writes them after the current tile's math (one barrier per tile, two LDS buffers).
+template <int NT, int W, bool CLAMP = false>
 struct Stager {
   static constexpr int CPR = W / 4;             // 16-B chunks per row
   static constexpr int N = TT * CPR / NT;       // chunks per thread
@@ -81,8 +81,15 @@ struct Stager {
   MHADA_DEV void load(const float* g, int r0, int n, int tid) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int c = tid + NT * i, row = c / CPR, col = (c % CPR) * 4;
-      r[i] = r0 + row < n ? ld4(g + (long long)(r0 + row) * W + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int c = tid + NT * i, row = c / CPR, col = (c % CPR) * 4, gr = r0 + row;
+      if constexpr (CLAMP) {
+        // unconditional load of a clamped row, zeroed afterwards: a branch around the load makes
+        // the wait-count pass drain every outstanding store before the tile's LDS write
+        const f32x4 x = ld4(g + (long long)min(gr, n - 1) * W + col);
+        r[i] = gr < n ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        r[i] = gr < n ? ld4(g + (long long)gr * W + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
   MHADA_DEV void store(float* s, int tid) const {
@@ -313,7 +320,7 @@ __global__ void __launch_bounds__(64 * NW) attn_train_dq_kernel(const TrainP p) 
 // ---------------------------------------------------------------------------------------
 // dK, dV': wave = 32 keys (one per lane column); streams 32-query tiles of Q, dO, lse2, D
 // ---------------------------------------------------------------------------------------
-template <int NW, int OCC>
+template <int NW, int OCC, bool SPILL>
 __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const TrainP p) {
   constexpr int NT = 64 * NW;
   __shared__ __attribute__((aligned(16))) float sQ[2][TT * LP];
@@ -332,17 +339,27 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   const float* lb = p.lse + bh * p.Nc;
   const float* db = p.dd + bh * p.Nc;
   f32x16 G1[2] = {f32x16{}, f32x16{}}, G2[2] = {f32x16{}, f32x16{}}, dK[2] = {f32x16{}, f32x16{}};
-  Stager<NT, 64> gq;
-  Stager<NT, 128> go;
+  Stager<NT, 64, SPILL> gq;
+  Stager<NT, 128, SPILL> go;
   float gl = INFINITY, gd = 0.f;
+  // With SPILL the loop body is branch-free around global memory (clamped loads, the tile after
+  // the last one loaded and discarded, range-checked buffer stores for dS): the wait before the
+  // LDS write then counts only the tile loads, and the dS stores stay in flight across tiles
+  // (a branch around any of them made the wait-count pass drain every store: 8.69 -> 8.32 ms per
+  // 512^2 B8 block backward).  Without stores the plain branches are cheaper.
   auto load = [&](int q0) {
     gq.load(qb, q0, p.Nc, tid);
     go.load(ob, q0, p.Nc, tid);
-    if (tid < TT && q0 + tid < p.Nc) {
-      gl = lb[q0 + tid];
-      gd = db[q0 + tid];
+    const int qi = q0 + (tid & (TT - 1));
+    if constexpr (SPILL) {
+      const float l0 = lb[min(qi, p.Nc - 1)], d0 = db[min(qi, p.Nc - 1)];
+      gl = qi < p.Nc ? l0 : INFINITY;  // padded query: P = 0
+      gd = qi < p.Nc ? d0 : 0.f;
+    } else if (tid < TT && qi < p.Nc) {
+      gl = lb[qi];
+      gd = db[qi];
     } else {
-      gl = INFINITY;  // padded query: P = 0
+      gl = INFINITY;
       gd = 0.f;
     }
   };
@@ -354,6 +371,12 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
       sD[buf][tid] = gd;
     }
   };
+  // dS rows of this (b, h): offsets past num_records (rows >= Nc, or a key >= Ns, whose lanes
+  // add (Nc + 32) rows) are dropped; unsigned offsets < 2 (Nc + 32) Ns * 4 < 2^32 (entry check)
+  const unsigned dkey = kv ? key * 4u : (unsigned)(p.Nc + TT) * p.Ns * 4;
+  const __amdgpu_buffer_rsrc_t dsr =
+      __builtin_amdgcn_make_buffer_rsrc(SPILL ? p.ds + bh * p.Nc * p.Ns : nullptr, 0,
+                                        SPILL ? p.Nc * p.Ns * 4 : 0, 0x00020000);
   load(0);
   store(0);
   __syncthreads();
@@ -361,7 +384,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   for (int t = 0; t < nt; ++t) {
     const int cb = t & 1;
     const bool nxt = t + 1 < nt;
-    if (nxt) load((t + 1) * TT);
+    if (SPILL || nxt) load((t + 1) * TT);
     // S (queries x keys) = Q . K^T, dA (queries x keys) = [dM' | dE2'] . [V' | V'^2]^T
     f32x16 S = {}, dA = {};
     const float* qrow = sQ[cb] + r32 * LP + 32 * h;
@@ -384,11 +407,12 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
       P[r] = __builtin_amdgcn_exp2f(S[r] - sL[cb][qi]);
       dS[r] = P[r] * (dA[r] - sD[cb][qi]);
     }
-    if (p.ds) {  // spill dS [q][key]: for each register the 32 lanes of a half write 128 B
-      float* dsr = p.ds + (bh * p.Nc + t * TT) * (long long)p.Ns + key;
+    if constexpr (SPILL) {  // dS [q][key]: for each register the 32 lanes of a half write 128 B
+      const unsigned base = (unsigned)(t * TT + 4 * h) * p.Ns * 4 + dkey;
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (kv && t * TT + acc_row(r, h) < p.Nc) dsr[(long long)acc_row(r, h) * p.Ns] = dS[r];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dS[r]), dsr,
+                                              (int)(base + ((r & 3) + 8 * (r >> 2)) * p.Ns * 4u), 0, 0);
     }
     // G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
 #pragma unroll
@@ -428,6 +452,8 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
 }
 
 constexpr int kNW = 4;
+// per-(b, h) dS slice addressed by 32-bit buffer offsets, with 0x7ffffff0 free as the drop offset
+constexpr long long kMaxSpillRows = (0x7fff0000LL / 4);
 
 bool set_grid(TrainP& p, long long BH, int n) {
   p.nb = (n + 32 * kNW - 1) / (32 * kNW);
@@ -467,19 +493,21 @@ extern "C" int mhada_attn_train_bwd(const float* q, const float* k, const float*
   if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_bwd: grid too large");
   // 288 registers, one wave per SIMD, no spills (two waves per SIMD at 256 registers spilled 18
   // and measured the same, tools/train_attn_bench.py)
-  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
+  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1, false>), dim3(p.nblk), dim3(64 * kNW), 0, s, p);
   return check_launch("mhada_attn_train_bwd");
 }
 
 extern "C" int mhada_attn_train_dkv(const float* q, const float* k, const float* v, const float* lse,
                                     const float* dmo, const float* dd, float* dk, float* dv, float* ds, int BH,
                                     int Nc, int Ns, mhada_stream_t s_) {
-  if (!q || !k || !v || !lse || !dmo || !dd || !dk || !dv || BH <= 0 || Nc <= 0 || Ns <= 0)
+  if (!q || !k || !v || !lse || !dmo || !dd || !dk || !dv || !ds || BH <= 0 || Nc <= 0 || Ns <= 0)
     return fail("mhada_attn_train_dkv: bad args");
+  if ((long long)(Nc + TT) * Ns > kMaxSpillRows)
+    return fail("mhada_attn_train_dkv: (Nc + 32) * Ns above 2^29 - 2^14 (32-bit dS offsets)");
   TrainP p = {};
   p.q = q; p.k = k; p.v = v; p.lse = const_cast<float*>(lse); p.dmo = dmo; p.dd = dd; p.dk = dk; p.dv = dv;
   p.ds = ds; p.Nc = Nc; p.Ns = Ns;
   if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_dkv: grid too large");
-  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
+  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1, true>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
   return check_launch("mhada_attn_train_dkv");
 }

@@ -329,6 +329,8 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
 # across the step's attention calls by the caching allocator); larger problems, or spill=False,
 # recompute S and dA in the query-stationary dQ kernel instead.
 DS_SPILL_BYTES = 16 << 30
+# Per-(b, h) slice bound of the kernel's 32-bit dS buffer offsets ((Nc + 32) * Ns, attn_train.hip)
+DS_SPILL_MAX_ROWS = 0x7fff0000 // 4
 
 
 def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
@@ -342,7 +344,7 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
             or v.shape != k.shape:
         raise ValueError("attn_train_bwd: bad shapes")
     if spill is None:
-        spill = Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES
+        spill = Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)

@@ -10,6 +10,7 @@ import torch  # noqa: E402
 from mhada_hip import ops  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+libs = sys.argv[2:]  # optional: A/B of several builds in this process (interleaved, median of 5)
 BH, N = 64, 4096
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, x = (torch.randn(BH, N, 64, device="cuda", generator=g) * 0.3 for _ in range(3))
@@ -32,6 +33,20 @@ def timeit(fn):
     return a.elapsed_time(b) / reps
 
 
+if libs:
+    from mhada_hip import _lib
+    handles = {p: _lib.load(p) for p in libs}
+    res = {p: [] for p in libs}
+    for _ in range(5):
+        for p in libs:
+            _lib._lib = handles[p]
+            res[p].append((timeit(lambda: ops.attn_train_fwd(q, k, v, x)),
+                           timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=False)),
+                           timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=True))))
+    for p in libs:
+        med = [sorted(r[i] for r in res[p])[2] for i in range(3)]
+        print(f"{p}: fwd {med[0]:.3f} ms  bwd recompute {med[1]:.3f} ms  bwd dS spill {med[2]:.3f} ms")
+    sys.exit(0)
 tf = timeit(lambda: ops.attn_train_fwd(q, k, v, x))
 tb = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=False))
 ts = timeit(lambda: ops.attn_train_bwd(q, k, v, lse, dmo, dd, spill=True))
