@@ -16,8 +16,9 @@ no collective on the data path (barrier + max-over-ranks timing only) -> scaling
 
 Roofline: the dominant kernel is the fused MHAda attention (mhada_attn, 6 launches/step);
 its algorithmic FLOPs per launch = 6*Nc*Ns*C*B (QK^T, PV, PV^2; 2 FLOP/MAC), timed live with
-HIP events on its launch stream over the timed region.  CPU baseline: the numpy oracle
-(oracle/mhada_oracle.py, a restatement of the reference) on one 512^2 frame on rank 0.
+HIP events on its launch stream over the timed region.  CPU baseline (rank 0, N=1): the
+reference's aten fp32 expression (tests/torch_ref.py, golden-pinned) at B=1 on the job's host
+cores, with the numpy oracle beside it.
 """
 import argparse
 import json
@@ -248,17 +249,40 @@ def run_train(steps, warmup, rank, world):
         dist.barrier()
     el = time.perf_counter() - t0
     el = max_over_ranks(el, world)
+    agree = None
+    if world > 1:
+        agree = rank_agreement([tr.vit_c, tr.vit_s, tr.ada])
+        assert agree["identical"], f"DP ranks diverged: {agree}"
+    backend = dist.get_backend() if world > 1 else None
     return {"metric": "train_image.py step throughput at 512x512, 8 images/GPU [configs[3]]",
             "value": round(batch * steps * world / el, 3), "unit": "images/s", "n_gpus": world, "steps": steps,
             "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic rand*255 images, recipe random-init weights",
             "config": {"workload": "train step (4 ViT + 3 AdaFormer + 5 VGG19 fwd, 4 losses, bwd, Adam)",
                        "global_batch": batch * world, "resolution": 512,
-                       "parallelism": f"dp{world} (RCCL grad all-reduce)" if world > 1 else "single GPU",
+                       "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} grad all-reduce)"
+                                       if world > 1 else "single GPU"),
+                       "backend": backend,
                        "engine": "every conv / linear / attention fwd+bwd on HIP kernels (Winograd fp32 convs, "
                                  "dS-spill attention backward, TN weight-gradient GEMMs); losses, Adam and glue on "
                                  "PyTorch-ROCm (DESIGN.md §3b)"},
-            "last_losses": last}
+            "last_losses": last, "rank_agreement": agree}
+
+
+def rank_agreement(modules) -> dict:
+    """After DP steps every rank must hold bit-identical parameters (same averaged gradients, same
+    Adam): per-parameter fp64 checksums, all-reduced MAX and MIN over the ranks, must coincide."""
+    ps = [p for m in modules for p in m.parameters()]
+    dev = ps[0].device if dist.get_backend() == "nccl" else torch.device("cpu")
+    sums = torch.stack([p.detach().double().sum() for p in ps]).to(dev)
+    sq = torch.stack([p.detach().double().square().sum() for p in ps]).to(dev)
+    v = torch.cat([sums, sq])
+    hi, lo = v.clone(), v.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    spread = float((hi - lo).abs().max())
+    return {"params": len(ps), "max_checksum_spread": spread, "identical": spread == 0.0,
+            "backend": dist.get_backend(), "world": dist.get_world_size()}
 
 
 def cpu_model() -> str:
@@ -273,38 +297,67 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_threads() -> tuple:
+    """(threads used, CPUs in this process's affinity mask).  SURVEY §8(d): the CPU path runs with
+    torch.set_num_threads(len(os.sched_getaffinity(0))); the GPU box caps a job's CPU share with
+    OMP_NUM_THREADS (16 per GPU there), which bounds the count when it is smaller."""
+    aff = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, cap) if cap > 0 else aff), aff
+
+
 def cpu_baseline():
-    """numpy oracle (oracle/mhada_oracle.py, restatement of the reference CPU path) timed on the
-    box's host cores at B=1: 3 frames at 256^2, 2 at 512^2 (the headline value) and one 1024^2
-    frame."""
-    import numpy as np
+    """The reference's PyTorch CPU arithmetic timed on the box's host cores (SURVEY §8d "CPU path
+    beside it"; infer_time.py:64-87 times the same three module calls): tests/torch_ref.py — the
+    aten fp32 restatement of vit_c / vit_s / adaFormer, pinned to the reference's own outputs by
+    tests/test_torch_ref_cpu.py — at B=1: 3 frames at 256^2, 2 at 512^2 (the headline value) and
+    one 1024^2 frame, on torch.set_num_threads(cores).  The numpy oracle (oracle/mhada_oracle.py)
+    is timed beside it at 256^2 as a second, labelled number."""
     from mhada_hip.recipe import recipe_state_dict, seeded_image
     from oracle import mhada_oracle as O
     import network
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch_ref
+    threads, aff = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     shapes = lambda m: {k: tuple(v.shape) for k, v in m.state_dict().items()}  # noqa: E731
-    p_vc = O.to_numpy_params(recipe_state_dict("vit_c", shapes(network.VisionTransformer(pos_embedding=True))))
-    p_vs = O.to_numpy_params(recipe_state_dict("vit_s", shapes(network.VisionTransformer(pos_embedding=False))))
-    p_ada = O.to_numpy_params(recipe_state_dict("ada", shapes(network.AdaAttnTransformerMultiHead())))
-    per_res = {}
-    for res, n in ((256, 3), (512, 2), (1024, 1)):
-        c = seeded_image(1, res, res, 11).numpy()
-        s = seeded_image(1, res, res, 12).numpy()
-        t0 = time.perf_counter()
-        for _ in range(n):
-            O.stylize(c, s, p_vc, p_vs, p_ada)
-        el = time.perf_counter() - t0
-        per_res[f"{res}x{res}_b1"] = {"frames_per_s": round(n / el, 5), "frames": n, "seconds": round(el, 2)}
+    sd_vc = recipe_state_dict("vit_c", shapes(network.VisionTransformer(pos_embedding=True)))
+    sd_vs = recipe_state_dict("vit_s", shapes(network.VisionTransformer(pos_embedding=False)))
+    sd_ada = recipe_state_dict("ada", shapes(network.AdaAttnTransformerMultiHead()))
+    per_res, oracle_res = {}, {}
+    try:
+        with torch.no_grad():  # one untimed small call (thread pool, allocator)
+            torch_ref.stylize(seeded_image(1, 256, 256, 11), seeded_image(1, 256, 256, 12), sd_vc, sd_vs, sd_ada)
+        for res, n in ((256, 3), (512, 2), (1024, 1)):
+            c = seeded_image(1, res, res, 11)
+            s = seeded_image(1, res, res, 12)
+            with torch.no_grad():
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    torch_ref.stylize(c, s, sd_vc, sd_vs, sd_ada)
+                el = time.perf_counter() - t0
+            per_res[f"{res}x{res}_b1"] = {"frames_per_s": round(n / el, 5), "frames": n, "seconds": round(el, 2)}
+        p = [O.to_numpy_params(sd) for sd in (sd_vc, sd_vs, sd_ada)]
+        for res, n in ((256, 2),):
+            c = seeded_image(1, res, res, 11).numpy()
+            s = seeded_image(1, res, res, 12).numpy()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                O.stylize(c, s, *p)
+            el = time.perf_counter() - t0
+            oracle_res[f"{res}x{res}_b1"] = {"frames_per_s": round(n / el, 5), "frames": n, "seconds": round(el, 2)}
+    finally:
+        torch.set_num_threads(prev)
     v = per_res["512x512_b1"]
-    return {"value": v["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": v["frames_per_s"], "unit": "frames/s", "cores": threads, "affinity_cpus": aff, "kind": "port",
             "cpu_model": cpu_model(), "per_resolution": per_res,
-            "sample": f"oracle/mhada_oracle.py (numpy fp32, {threads} BLAS threads, same recipe weights) at B=1: "
+            "sample": f"tests/torch_ref.py (the reference's aten fp32 expression, golden-pinned) on "
+                      f"torch.set_num_threads({threads}), recipe weights, B=1: "
                       + ", ".join(f"{k} {d['frames']} frame(s) in {d['seconds']} s" for k, d in per_res.items())
-                      + "; value = the 512x512 rate"}
+                      + "; value = the 512x512 rate",
+            "numpy_oracle": {"per_resolution": oracle_res,
+                             "note": "oracle/mhada_oracle.py (numpy fp32, same weights), BLAS threads as configured"}}
 
 
 def main():

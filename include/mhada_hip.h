@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 5 (Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 6 (LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -240,6 +240,24 @@ int mhada_vit_batch_attn_bwd(const float* qkv, const float* dout, float* dqkv, i
  * (up to 1024*C used), fixed-order reduction. */
 int mhada_colsum(const float* x, float* out, long long rows, int C, float* work, long long work_floats,
                  mhada_stream_t stream);
+
+/* nn.LayerNorm for the training path (vit.py:54-55,58,62; replaces aten native_layer_norm and
+ * its backward): y fp32 [rows][cols], stats [rows][2] = (mean, rstd) for the backward.
+ * cols 256 / 512 / 1024; 16-byte aligned x, y, gamma, beta. */
+int mhada_layernorm_fwd(const float* x, float* y, float* stats, const float* gamma, const float* beta,
+                        int rows, int cols, float eps, mhada_stream_t stream);
+
+/* LayerNorm backward: dx [rows][cols], dgamma / dbeta [cols] (fixed-order sums: per-128-row block
+ * partials, then the slab reduction).  work: >= (ceil(rows/128) * 2 + 2) * cols floats. */
+int mhada_layernorm_bwd(const float* x, const float* dy, const float* stats, const float* gamma, float* dx,
+                        float* dgamma, float* dbeta, float* work, long long work_floats, int rows, int cols,
+                        mhada_stream_t stream);
+
+/* Adjoint of mhada_pos_embed (vit.py:91-92 under autograd; replaces aten's atomic
+ * upsample_bilinear2d_backward): g token-major [oh*ow][C] -> gpos [C][bh][bw], a gather per source
+ * pixel in a fixed order (deterministic). */
+int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int oh, int ow,
+                        mhada_stream_t stream);
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */
 int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t stream);
 /* Adjoint of ReflectionPad2d(1) (conv.py:27,31): dxp [B][H+2][W+2][C] (the full-correlation

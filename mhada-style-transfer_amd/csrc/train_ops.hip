@@ -14,6 +14,11 @@
 //                     backward (gradient to the FIRST maximum of each window in row-major scan
 //                     order, as ATen's max_pool2d keeps it).
 //   mhada_upsample2x_bwd  adjoint of the bilinear x2 upsample (conv.py:71, align_corners=False).
+//   mhada_layernorm_fwd / mhada_layernorm_bwd  nn.LayerNorm (vit.py:54-55,58,62; eps 1e-6) with
+//                     the row statistics kept for the backward; dX per row, dGamma / dBeta as
+//                     per-block column partials summed in a fixed order.
+//   mhada_pos_embed_bwd  adjoint of the PosEmbedding bilinear resize (vit.py:91-92): a gather
+//                     per source pixel (fixed order) in place of ATen's atomic scatter.
 //   mhada_vgg_input / mhada_vgg_input_bwd  imageNet1k_normalize (vgg19.py:6-12) fused with the
 //                     NCHW -> NHWC layout change (channels zero padded to a multiple of 32 so the
 //                     first conv runs on the implicit-GEMM kernel), and its adjoint.
@@ -319,6 +324,174 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x
     for (int k = 1; k < groups; ++k) s += part[k * tpc + t];
     *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * C + c) = s;
   }
+}
+
+// ======================================================================================
+// LayerNorm for training: forward keeps (mean, rstd) per row; backward
+//   xh = (x - mean) rstd,  g' = dy * gamma,
+//   dx = rstd (g' - mean_c(g') - xh mean_c(g' xh)),  dgamma = sum_rows dy xh,  dbeta = sum_rows dy
+// One wave per row (VPL = cols / 64 values per lane, 16-B column quads as layernorm_kernel).
+// ======================================================================================
+template <int VPL>
+__global__ void __launch_bounds__(256) ln_fwd_train_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           float* __restrict__ stats, const float* __restrict__ g,
+                                                           const float* __restrict__ b, int rows, float eps) {
+  constexpr int COLS = VPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * COLS;
+  float v[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(xr + (i * 64 + lane) * 4);
+    v[4 * i] = t[0]; v[4 * i + 1] = t[1]; v[4 * i + 2] = t[2]; v[4 * i + 3] = t[3];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.0f / COLS);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const float d = v[i] - mean;
+    ss += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / COLS) + eps);
+  float* yr = y + (long long)row * COLS;
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + c);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[4 * i + e] - mean) * rstd * gg[e] + bb[e];
+    *reinterpret_cast<f32x4*>(yr + c) = o;
+  }
+  if (lane == 0) *reinterpret_cast<float2*>(stats + 2LL * row) = make_float2(mean, rstd);
+}
+
+constexpr int kLnBwdRows = 128;  // rows per block (32 per wave)
+
+template <int VPL>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     const float* __restrict__ stats, const float* __restrict__ g,
+                                                     float* __restrict__ dx, float* __restrict__ slab, int rows) {
+  constexpr int COLS = VPL * 64;
+  __shared__ f32x4 part[4][2][VPL / 4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float gg[VPL], dgp[VPL], dbp[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(g + (i * 64 + lane) * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gg[4 * i + e] = t[e];
+      dgp[4 * i + e] = 0.f;
+      dbp[4 * i + e] = 0.f;
+    }
+  }
+  const int r0 = blockIdx.x * kLnBwdRows, r1 = min(rows, r0 + kLnBwdRows);
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const float2 st = *reinterpret_cast<const float2*>(stats + 2LL * row);
+    const float* xr = x + (long long)row * COLS;
+    const float* dr = dy + (long long)row * COLS;
+    float xh[VPL], gd[VPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL / 4; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + c);
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(dr + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * i + e;
+        xh[k] = (xv[e] - st.x) * st.y;
+        gd[k] = dv[e] * gg[k];
+        s1 += gd[k];
+        s2 += gd[k] * xh[k];
+        dgp[k] += dv[e] * xh[k];
+        dbp[k] += dv[e];
+      }
+    }
+    const float m1 = wave_sum(s1) * (1.0f / COLS), m2 = wave_sum(s2) * (1.0f / COLS);
+    float* o = dx + (long long)row * COLS;
+#pragma unroll
+    for (int i = 0; i < VPL / 4; ++i) {
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = st.y * (gd[4 * i + e] - m1 - xh[4 * i + e] * m2);
+      *reinterpret_cast<f32x4*>(o + (i * 64 + lane) * 4) = r;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPL / 4; ++i) {
+    part[wv][0][i][lane] = f32x4{dgp[4 * i], dgp[4 * i + 1], dgp[4 * i + 2], dgp[4 * i + 3]};
+    part[wv][1][i][lane] = f32x4{dbp[4 * i], dbp[4 * i + 1], dbp[4 * i + 2], dbp[4 * i + 3]};
+  }
+  __syncthreads();
+  // waves summed in a fixed order; slab[blk] = [dgamma partial (COLS) | dbeta partial (COLS)]
+  for (int q = threadIdx.x; q < 2 * (VPL / 4) * 64; q += 256) {
+    const int which = q / ((VPL / 4) * 64), rem = q - which * (VPL / 4) * 64, i = rem >> 6, ln = rem & 63;
+    f32x4 a = part[0][which][i][ln];
+    a += part[1][which][i][ln];
+    a += part[2][which][i][ln];
+    a += part[3][which][i][ln];
+    *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * 2 * COLS + which * COLS + (i * 64 + ln) * 4) = a;
+  }
+}
+
+// ======================================================================================
+// PosEmbedding resize adjoint: gpos[c][sy][sx] = sum over target pixels (oy, ox) of the bilinear
+// weight pos_embed_kernel gives source (sy, sx) times g[oy*ow + ox][c].  Gather per source pixel
+// over a window of target rows / columns that contains every one referencing it, re-deriving the
+// forward's indices and weights with its exact float operations (deterministic, no atomics).
+// ======================================================================================
+MHADA_DEV void pe_src(int o, float sh, int n, int& i0, int& i1, float& l0, float& l1) {
+  const float sf = fmaxf(sh * ((float)o + 0.5f) - 0.5f, 0.f);
+  i0 = min((int)sf, n - 1);
+  i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  l1 = sf - (float)i0;
+  l0 = 1.f - l1;
+}
+
+MHADA_DEV float pe_weight(int o, float sh, int n, int src) {
+  int i0, i1;
+  float l0, l1;
+  pe_src(o, sh, n, i0, i1, l0, l1);
+  return (i0 == src ? l0 : 0.f) + (i1 == src ? l1 : 0.f);
+}
+
+__global__ void __launch_bounds__(256) pos_embed_bwd_kernel(const float* __restrict__ g, float* __restrict__ gpos,
+                                                            int C, int bh, int bw, int oh, int ow) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)C * bh * bw) return;
+  const int c = (int)(idx % C);
+  const int pix = (int)(idx / C);
+  const int sy = pix / bw, sx = pix - (pix / bw) * bw;
+  float acc = 0.f;
+  if (oh == bh && ow == bw) {
+    acc = g[(long long)pix * C + c];
+  } else {
+    const float shy = (float)bh / (float)oh, shx = (float)bw / (float)ow;
+    // target o maps to source coordinate ~ (o + 0.5) sh - 0.5; sources sy-1 .. sy+1 bound the window
+    const int ylo = max(0, (int)floorf(((float)sy - 1.5f) / shy) - 1);
+    const int yhi = min(oh - 1, (int)ceilf(((float)sy + 1.5f) / shy) + 1);
+    const int xlo = max(0, (int)floorf(((float)sx - 1.5f) / shx) - 1);
+    const int xhi = min(ow - 1, (int)ceilf(((float)sx + 1.5f) / shx) + 1);
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      const float wy = pe_weight(oy, shy, bh, sy);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        const float wx = pe_weight(ox, shx, bw, sx);
+        if (wx != 0.f) row += wx * g[((long long)oy * ow + ox) * C + c];
+      }
+      acc += wy * row;
+    }
+  }
+  gpos[(long long)c * bh * bw + pix] = acc;
 }
 
 // ======================================================================================
@@ -670,6 +843,57 @@ extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, f
   hipLaunchKernelGGL(slab_reduce_kernel, grid1(C / 4), dim3(256), 0, (hipStream_t)s_, work, out, 1LL, C, (long long)C,
                      (int)chunks);
   return check_launch("mhada_colsum(reduce)");
+}
+
+extern "C" int mhada_layernorm_fwd(const float* x, float* y, float* stats, const float* gamma, const float* beta,
+                                   int rows, int cols, float eps, mhada_stream_t s_) {
+  if (!x || !y || !stats || !gamma || !beta || rows <= 0) return fail("mhada_layernorm_fwd: bad args");
+  if (!al16(x) || !al16(y) || !al16(gamma) || !al16(beta) || ((uintptr_t)stats & 7))
+    return fail("mhada_layernorm_fwd: x, y, gamma, beta 16-byte aligned, stats 8-byte aligned");
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)s_;
+  switch (cols) {
+    case 256: hipLaunchKernelGGL(ln_fwd_train_kernel<4>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
+    case 512: hipLaunchKernelGGL(ln_fwd_train_kernel<8>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(ln_fwd_train_kernel<16>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
+    default: return fail("mhada_layernorm_fwd: cols must be 256, 512 or 1024");
+  }
+  return check_launch("mhada_layernorm_fwd");
+}
+
+extern "C" int mhada_layernorm_bwd(const float* x, const float* dy, const float* stats, const float* gamma, float* dx,
+                                   float* dgamma, float* dbeta, float* work, long long work_floats, int rows, int cols,
+                                   mhada_stream_t s_) {
+  if (!x || !dy || !stats || !gamma || !dx || !dgamma || !dbeta || !work || rows <= 0)
+    return fail("mhada_layernorm_bwd: bad args");
+  if (!al16(x) || !al16(dy) || !al16(gamma) || !al16(dx) || !al16(work) || ((uintptr_t)stats & 7))
+    return fail("mhada_layernorm_bwd: 16-byte aligned operands");
+  const int nblk = (rows + kLnBwdRows - 1) / kLnBwdRows;
+  if (work_floats < (long long)nblk * 2 * cols + 2LL * cols) return fail("mhada_layernorm_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)s_;
+  switch (cols) {
+    case 256: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nblk), dim3(256), 0, s, x, dy, stats, gamma, dx, work, rows); break;
+    case 512: hipLaunchKernelGGL(ln_bwd_kernel<8>, dim3(nblk), dim3(256), 0, s, x, dy, stats, gamma, dx, work, rows); break;
+    case 1024: hipLaunchKernelGGL(ln_bwd_kernel<16>, dim3(nblk), dim3(256), 0, s, x, dy, stats, gamma, dx, work, rows); break;
+    default: return fail("mhada_layernorm_bwd: cols must be 256, 512 or 1024");
+  }
+  if (int rc = check_launch("mhada_layernorm_bwd")) return rc;
+  float* red = work + (long long)nblk * 2 * cols;  // [dgamma | dbeta]
+  hipLaunchKernelGGL(slab_reduce_kernel, grid1(2 * cols / 4), dim3(256), 0, s, work, red, 1LL, 2 * cols,
+                     (long long)(2 * cols), nblk);
+  if (int rc = check_launch("mhada_layernorm_bwd(reduce)")) return rc;
+  if (hipMemcpyAsync(dgamma, red, sizeof(float) * cols, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(dbeta, red + cols, sizeof(float) * cols, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail("mhada_layernorm_bwd: copy");
+  return 0;
+}
+
+extern "C" int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int oh, int ow,
+                                   mhada_stream_t s_) {
+  if (!g || !gpos || C <= 0 || bh <= 0 || bw <= 0 || oh <= 0 || ow <= 0) return fail("mhada_pos_embed_bwd: bad args");
+  hipLaunchKernelGGL(pos_embed_bwd_kernel, grid1((long long)C * bh * bw), dim3(256), 0, (hipStream_t)s_, g, gpos, C, bh,
+                     bw, oh, ow);
+  return check_launch("mhada_pos_embed_bwd");
 }
 
 extern "C" int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t s_) {

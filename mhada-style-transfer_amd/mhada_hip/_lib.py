@@ -78,6 +78,9 @@ SIGNATURES = {
     "mhada_rows_normalize": (_I, [_vp] * 4 + [_I, _I, _I, _I, _vp]),
     "mhada_gemm_tn": (_I, [ctypes.POINTER(GemmTnArgs), _vp, _c_ll, _vp]),
     "mhada_colsum": (_I, [_vp, _vp, _c_ll, _I, _vp, _c_ll, _vp]),
+    "mhada_layernorm_fwd": (_I, [_vp, _vp, _vp, _vp, _vp, _I, _I, _F, _vp]),
+    "mhada_layernorm_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _vp]),
+    "mhada_pos_embed_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
@@ -117,7 +120,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 def get_tuning(name: str) -> int:

@@ -38,8 +38,9 @@ def needs_grad(module: torch.nn.Module, *xs) -> bool:
 def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
     """VisionTransformer.forward on the HIP training kernels (train_fns): patch embedding and
     every Linear (MHA in/out projections, MLP with fused ReLU) on mhada_gemm forward and
-    mhada_gemm / mhada_gemm_tn / mhada_colsum backward; LayerNorm, the pos-embed interpolation and
-    the batch-axis softmax (L = B <= 8 keys per token) stay aten."""
+    mhada_gemm / mhada_gemm_tn / mhada_colsum backward; LayerNorm on mhada_layernorm_fwd/_bwd; the
+    pos-embed resize on mhada_pos_embed and its gather adjoint; the batch-axis attention core
+    (L = B <= 8 keys per token) on mhada_vit_batch_attn(_bwd)."""
     from . import train_fns
     B, _, H, W = x.shape
     p = vit.patch_size
@@ -48,16 +49,14 @@ def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
     t = train_fns.PatchEmbedFn.apply(x, vit.patch_embedding.conv_proj.weight, vit.patch_embedding.conv_proj.bias)
     C = t.shape[2]
     if vit.pos_embedding is not None:
-        pe = vit.pos_embedding.pos_embed
-        if (h, w) != tuple(pe.shape[2:]):
-            pe = F.interpolate(pe, size=(h, w), mode="bilinear", align_corners=False)
-        t = t + pe.reshape(1, C, N).permute(0, 2, 1)
+        t = t + train_fns.pos_embed(vit.pos_embedding.pos_embed, h, w).view(1, N, C)
     outs = []
+    ln_hip = C in (256, 512, 1024)
     for blk in vit.encoder:
         att = blk.attention
         heads = att.num_heads
         d = C // heads
-        y = blk.ln1(t).reshape(B * N, C)
+        y = train_fns.layernorm(t.reshape(B * N, C), blk.ln1) if ln_hip else blk.ln1(t).reshape(B * N, C)
         qkv = train_fns.linear(y, att.in_proj_weight, att.in_proj_bias)
         if d == 64 and B <= 8:  # the batch-axis attention core on HIP (L = B keys per token)
             o = train_fns.BatchAxisAttnFn.apply(qkv.view(B, N, 3 * C), heads).reshape(B * N, C)
@@ -66,7 +65,7 @@ def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
             a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (d ** -0.5), dim=-1)
             o = torch.matmul(a, v).permute(2, 0, 1, 3).reshape(B * N, C)
         t = t + train_fns.linear(o, att.out_proj.weight, att.out_proj.bias).view(B, N, C)
-        y2 = blk.ln2(t).reshape(B * N, C)
+        y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2) if ln_hip else blk.ln2(t).reshape(B * N, C)
         m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True)
         t = t + train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias).view(B, N, C)
         outs.append(t.permute(0, 2, 1).reshape(B, C, h, w))
@@ -140,10 +139,12 @@ class MHAdaAttnFn(torch.autograd.Function):
 
 
 def _fused_train_attn(blk, fc) -> bool:
-    """The HIP training kernels compute in fp32; under autocast MHAdaAttnFn casts its operands to
-    fp32 (custom_fwd), so a bf16/fp16 projection output still takes this path."""
-    return (fc.is_cuda and fc.is_floating_point() and blk.activation_name == "softmax"
-            and blk.head_dim == 64 and TRAIN_ATTN != "torch")
+    """The HIP training kernels compute in fp32.  An fp32 input takes this path; so does any
+    floating input inside a CUDA autocast region (MHAdaAttnFn's custom_fwd casts its operands to
+    fp32 there).  Outside autocast a bf16 / fp16 / fp64 block input (model.half(), a gradcheck)
+    runs the aten formula: the token-path statistics kernels read fp32 only."""
+    return (fc.is_cuda and (fc.dtype == torch.float32 or (fc.is_floating_point() and torch.is_autocast_enabled("cuda")))
+            and blk.activation_name == "softmax" and blk.head_dim == 64 and TRAIN_ATTN != "torch")
 
 
 def _head_proj(mods, t: torch.Tensor, H: int) -> torch.Tensor:

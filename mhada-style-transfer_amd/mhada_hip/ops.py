@@ -126,8 +126,12 @@ WINO = True
 
 
 def wino_eligible(x: torch.Tensor, w: torch.Tensor, upsample: bool) -> bool:
+    """The Winograd kernel's constraints (csrc/wino.hip): fp32, Cin % 8, Cout % 64, >= 2x2 pixels
+    and 32-bit element offsets (B*H*W*Cin and the output's B*H*W*Cout < 2^31); anything else runs
+    on the implicit-GEMM conv."""
     return (WINO and w.dtype == torch.float32 and x.dtype == torch.float32 and not upsample
-            and x.shape[-1] % 8 == 0 and w.shape[0] % 64 == 0 and x.shape[1] >= 2 and x.shape[2] >= 2)
+            and x.shape[-1] % 8 == 0 and w.shape[0] % 64 == 0 and x.shape[1] >= 2 and x.shape[2] >= 2
+            and x.numel() < 2 ** 31 and x.numel() // x.shape[-1] * w.shape[0] < 2 ** 31)
 
 
 def wino_weights(w: torch.Tensor) -> torch.Tensor:
@@ -238,9 +242,54 @@ def pos_embed(pos: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
     return out
 
 
+def pos_embed_bwd(g: torch.Tensor, bh: int, bw: int) -> torch.Tensor:
+    """``mhada_pos_embed_bwd``: token-major gradient g [oh][ow][C] -> (1, C, bh, bw)."""
+    _need_gpu(g)
+    oh, ow, C = g.shape
+    if g.dtype != torch.float32 or not g.is_contiguous():
+        raise ValueError("pos_embed_bwd needs a contiguous float32 [oh][ow][C] gradient")
+    out = torch.empty(1, C, bh, bw, device=g.device, dtype=torch.float32)
+    _call("mhada_pos_embed_bwd", g, g.data_ptr(), out.data_ptr(), C, bh, bw, oh, ow)
+    return out
+
+
+def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float):
+    """``mhada_layernorm_fwd``: fp32 rows [M][C] -> (y fp32, stats [M][2])."""
+    _need_gpu(x, gamma, beta)
+    for t in (x, gamma, beta):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("layernorm_fwd needs contiguous float32 operands")
+    M, C = x.shape
+    y = torch.empty_like(x)
+    st = torch.empty(M, 2, device=x.device, dtype=torch.float32)
+    _call("mhada_layernorm_fwd", x, x.data_ptr(), y.data_ptr(), st.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+          M, C, float(eps))
+    return y, st
+
+
+def layernorm_bwd(x: torch.Tensor, dy: torch.Tensor, st: torch.Tensor, gamma: torch.Tensor):
+    """``mhada_layernorm_bwd``: -> (dx, dgamma, dbeta)."""
+    _need_gpu(x, dy, st, gamma)
+    for t in (x, dy, st, gamma):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("layernorm_bwd needs contiguous float32 operands")
+    M, C = x.shape
+    dx = torch.empty_like(x)
+    dg = torch.empty(C, device=x.device, dtype=torch.float32)
+    db = torch.empty(C, device=x.device, dtype=torch.float32)
+    nw = ((M + 127) // 128 * 2 + 2) * C
+    work = torch.empty(nw, device=x.device, dtype=torch.float32)
+    _call("mhada_layernorm_bwd", x, x.data_ptr(), dy.data_ptr(), st.data_ptr(), gamma.data_ptr(), dx.data_ptr(),
+          dg.data_ptr(), db.data_ptr(), work.data_ptr(), nw, M, C)
+    return dx, dg, db
+
+
 def instnorm_stats(x: torch.Tensor, eps: float = 1e-5):
     """x [B][N][C] fp32 -> (mu, rstd) [B][C] fp32."""
     _need_gpu(x)
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 3:
+        raise ValueError(f"instnorm_stats needs contiguous float32 token rows [B][N][C], got {x.dtype} "
+                         f"{tuple(x.shape)}")
     B, N, C = x.shape
     splits = max(1, min(N // 32, 2048 // max(1, B * ((C + 63) // 64))))
     mu = torch.empty(B, C, device=x.device, dtype=torch.float32)
@@ -333,6 +382,13 @@ DS_SPILL_BYTES = 16 << 30
 DS_SPILL_MAX_ROWS = 0x7fff0000 // 4
 
 
+def _device_headroom(dev: torch.device) -> int:
+    """Bytes a new allocation can take without an OOM: free device memory plus what the caching
+    allocator holds reserved but unused (the dS buffer of the previous block is reused from there)."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    return free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+
+
 def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
     """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64).  With the dS spill
     (default when it fits DS_SPILL_BYTES and Ns % 4 == 0): ``mhada_attn_train_dkv`` writes dS and
@@ -344,7 +400,9 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
             or v.shape != k.shape:
         raise ValueError("attn_train_bwd: bad shapes")
     if spill is None:
-        spill = Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS
+        need = 4 * BH * Nc * Ns
+        spill = Ns % 4 == 0 and need <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS \
+            and need <= _device_headroom(q.device)
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)
@@ -530,7 +588,12 @@ def vgg_input_bwd(dout: torch.Tensor) -> torch.Tensor:
 def rows_normalize(x: torch.Tensor, mu: torch.Tensor, rs: torch.Tensor, unit: bool = False) -> torch.Tensor:
     """``mhada_rows_normalize``: (x - mu) * rs on token rows [B][N][C] (and / |row| if unit)."""
     _need_gpu(x, mu, rs)
+    for t in (x, mu, rs):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("rows_normalize needs contiguous float32 rows and statistics")
     B, N, C = x.shape
+    if mu.shape != (B, C) or rs.shape != (B, C):
+        raise ValueError(f"rows_normalize: statistics {tuple(mu.shape)} do not match rows {tuple(x.shape)}")
     out = torch.empty_like(x)
     _call("mhada_rows_normalize", x, x.data_ptr(), mu.data_ptr(), rs.data_ptr(), out.data_ptr(), int(unit), B, N, C)
     return out

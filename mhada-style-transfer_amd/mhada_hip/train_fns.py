@@ -19,6 +19,7 @@ the reference, and runs its forward and backward through libmhada_hip.so:
 """
 from __future__ import annotations
 
+import weakref
 from typing import Dict, Optional
 
 import torch
@@ -52,12 +53,30 @@ def _pack_dgrad(weight: torch.Tensor, cx: int, cg: int) -> torch.Tensor:
     return w.reshape(cx, 9 * cg).contiguous()
 
 
+# Packed / Winograd-transformed copies of frozen weights (VGG19), keyed by the weight tensor's
+# identity and checked against its version counter.  Held here, not on the Parameter: pickling,
+# deepcopy or torch.save(module) of the VGG then carry no extra GPU copies.  An entry dies with
+# its weight (weakref.finalize), and a recycled id() can never alias (the entry holds a weakref
+# whose referent is compared by identity).
+_PACK_CACHE: Dict[int, tuple] = {}
+
+
+def _pack_slot(weight: torch.Tensor) -> Dict:
+    key = id(weight)
+    ent = _PACK_CACHE.get(key)
+    if ent is None or ent[0]() is not weight:
+        ent = (weakref.ref(weight), {})
+        _PACK_CACHE[key] = ent
+        weakref.finalize(weight, _PACK_CACHE.pop, key, None)
+    return ent[1]
+
+
 def _cached(weight: torch.Tensor, kind: str, *dims) -> torch.Tensor:
-    """Packed weights of a frozen layer (VGG19), held on the weight tensor itself and keyed by
-    its version counter; trainable weights change every step and are packed per call."""
+    """Packed weights of a frozen layer (VGG19), cached per weight tensor and keyed by its
+    version counter; trainable weights change every step and are packed per call."""
     if weight.requires_grad:
         return _pack_fwd(weight, *dims) if kind == "f" else _pack_dgrad(weight, *dims)
-    cache = weight.__dict__.setdefault("_mhada_pack", {})
+    cache = _pack_slot(weight)
     key = (kind,) + dims
     hit = cache.get(key)
     if hit is not None and hit[0] == weight._version:
@@ -72,7 +91,7 @@ def _wino(weight: torch.Tensor, kind: str, packed: torch.Tensor, *dims) -> Optio
     None for trainable weights (ops.conv3x3 transforms them per call) or ineligible shapes."""
     if weight.requires_grad or packed.dtype != F32 or packed.shape[0] % 64 or (packed.shape[1] // 9) % 8:
         return None
-    cache = weight.__dict__.setdefault("_mhada_pack", {})
+    cache = _pack_slot(weight)
     key = ("u", kind) + dims
     hit = cache.get(key)
     if hit is not None and hit[0] == weight._version:
@@ -191,6 +210,53 @@ class InstanceNormTokensFn(torch.autograd.Function):
 
 def instance_norm_tokens(x: torch.Tensor) -> torch.Tensor:
     return InstanceNormTokensFn.apply(x)
+
+
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm (vit.py:54-55,58,62; the EncoderBlock's ln1 / ln2, eps 1e-6) on token rows
+    [M][C] fp32: mhada_layernorm_fwd (row statistics kept) and mhada_layernorm_bwd (dx per row,
+    dgamma / dbeta as fixed-order column sums)."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, weight, bias, eps: float):
+        x = x.contiguous()
+        y, st = ops.layernorm_fwd(x, weight.detach().contiguous(), bias.detach().contiguous(), eps)
+        ctx.save_for_backward(x, st, weight)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, st, weight = ctx.saved_tensors
+        dx, dg, db = ops.layernorm_bwd(x, dy.contiguous(), st, weight.detach().contiguous())
+        return dx, dg, db, None
+
+
+def layernorm(x2d: torch.Tensor, ln: torch.nn.LayerNorm) -> torch.Tensor:
+    return LayerNormFn.apply(x2d, ln.weight, ln.bias, ln.eps)
+
+
+class PosEmbedFn(torch.autograd.Function):
+    """PosEmbedding (vit.py:81-102): the (1, C, bh, bw) table bilinearly resized
+    (align_corners=False) to the token grid, token-major [h*w][C] — mhada_pos_embed forward, the
+    deterministic gather adjoint mhada_pos_embed_bwd backward."""
+
+    @staticmethod
+    def forward(ctx, pos, h: int, w: int):
+        ctx.shape = pos.shape
+        ctx.hw = (h, w)
+        return ops.pos_embed(pos.detach().float().contiguous(), h, w)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.hw
+        _, C, bh, bw = ctx.shape
+        return ops.pos_embed_bwd(g.contiguous().view(h, w, C), bh, bw), None, None
+
+
+def pos_embed(pos: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    return PosEmbedFn.apply(pos, h, w)
 
 
 class HeadProjFn(torch.autograd.Function):

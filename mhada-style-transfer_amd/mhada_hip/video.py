@@ -34,7 +34,15 @@ def cv2_to_tensor(img, resize: Optional[tuple] = None, device: Optional[torch.de
     through pinned memory to ``device``, default the current ROCm device) or a uint8 device
     tensor; ``resize`` = (width, height) as cv2.resize takes it.  Returns the fp32 (3, h, w)
     tensor in [0, 255] on the device (the reference returns it on the CPU and moves it with
-    .to(device) at infer_video.py:81)."""
+    .to(device) at infer_video.py:81).
+
+    Restriction: ``resize`` may only shrink the frame (every reference script downscales, e.g.
+    infer_video.py:80 takes 1080p to 512x256).  cv2.resize(INTER_AREA) also enlarges, with an
+    interpolation this kernel does not implement; a target larger than the frame raises
+    ValueError here instead of silently differing from cv2."""
+    if resize is not None and len(img.shape) == 3 and (int(resize[0]) > img.shape[1] or int(resize[1]) > img.shape[0]):
+        raise ValueError(f"cv2_to_tensor: resize {tuple(resize)} enlarges the {img.shape[1]}x{img.shape[0]} frame; "
+                         "INTER_AREA upscaling is not implemented (downscale only)")
     if not isinstance(img, torch.Tensor):
         t = torch.from_numpy(img)
         if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:

@@ -2,9 +2,10 @@
 
 ``AdaAttnMultiHead`` keeps the reference's per-head ``f_list/g_list/h_list`` 1x1 convs and
 ``out_conv`` (identical state_dict keys; the InstanceNorms and the activation modules carry
-no state).  Forward runs ``mhada_hip.engine.block_forward``: InstanceNorm statistics kernel,
-per-batch weight fold, two grouped projection GEMMs, the fused flash-style MHAda attention
-(M, S and S*IN(fcs)+M in its epilogue) and the out_conv GEMM.
+no state).  On a ROCm device the forward runs ``mhada_hip.engine.block_forward``: InstanceNorm
+statistics kernel, per-batch weight fold, two grouped projection GEMMs, the fused flash-style
+MHAda attention (M, S and S*IN(fcs)+M in its epilogue) and the out_conv GEMM.  CPU tensors (the
+reference's no-GPU branch, ``infer_image.py:48``) run the aten form in ``autograd_path``.
 """
 from typing import List
 
@@ -26,8 +27,9 @@ def _check_activation(activation: str) -> str:
 
 class AdaAttnForLoss(nn.Module):
     """Parameter-free AdaAttN used as the local-feature-loss target (``adaDecoder.py:38-81``).
-    Training-path component: evaluated with PyTorch-ROCm ops, query-chunked (its head width is
-    qk_dim = 448..1472, not the 64 of the fused MHAda kernel)."""
+    Training-path component: on a ROCm device the wide-head HIP kernel ``mhada_loss_attn``
+    (qk_dim = 448..1472, d_v 256/512, A never stored); under autograd or on the CPU the
+    reference expression with aten ops, query-chunked."""
 
     def __init__(self, v_dim, qk_dim, activation="softmax"):
         super().__init__()
@@ -55,9 +57,8 @@ class AdaAttnMultiHead(nn.Module):
         self.activation_name = _check_activation(activation)
 
     def forward(self, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
-        if autograd_path.needs_grad(self, fc, fs, fcs):
+        if not fc.is_cuda or autograd_path.needs_grad(self, fc, fs, fcs):  # autograd / CPU tensors
             return autograd_path.block_forward(self, fc, fs, fcs)
-        engine.require_device(fc, "AdaAttnMultiHead")
         dt = engine.resolve_compute_dtype(self)
         fcf = engine._Feat.from_nchw(fc)
         fsf = engine._Feat.from_nchw(fs)
@@ -86,6 +87,6 @@ class AdaAttnTransformerMultiHead(nn.Module):
             fc, fs = args
         fc: List[torch.Tensor] = list(fc)
         fs: List[torch.Tensor] = list(fs)
-        if autograd_path.needs_grad(self, *fc, *fs):
+        if not fc[0].is_cuda or autograd_path.needs_grad(self, *fc, *fs):  # autograd / CPU tensors
             return autograd_path.adaformer_forward(self, fc, fs)
         return engine.adaformer_forward(self, fc, fs)

@@ -1,8 +1,9 @@
 """Decoder — drop-in for ``MHAdaSTr/network/conv.py:23-100``.
 
-Same module nesting as the reference (``conv1.0.conv.conv.weight`` ...); ``Decoder.forward``
-runs the implicit-GEMM MFMA convolutions (reflect padding and the bilinear x2 fused into the
-next layer's operand gather) and the dedicated Cin->3 output kernel.
+Same module nesting as the reference (``conv1.0.conv.conv.weight`` ...).  On a ROCm device
+``Decoder.forward`` runs the HIP convolutions (fp32: Winograd F(2x2,3x3); bf16: implicit-GEMM
+MFMA and the 64->64 tile kernel with the bilinear x2 fused) and the dedicated Cin->3 output
+kernel; CPU tensors run the aten form in ``mhada_hip.autograd_path``.
 """
 import torch
 import torch.nn as nn
@@ -59,8 +60,7 @@ class Decoder(nn.Module):
         )
 
     def forward(self, fcs: torch.Tensor) -> torch.Tensor:
-        if autograd_path.needs_grad(self, fcs):
+        if not fcs.is_cuda or autograd_path.needs_grad(self, fcs):  # autograd / CPU tensors
             return autograd_path.decoder_forward(self, fcs)
-        engine.require_device(fcs, "Decoder")
         dt = engine.resolve_compute_dtype(self)
         return engine.decoder_forward_tokens(self, engine.to_tokens(fcs), dt)

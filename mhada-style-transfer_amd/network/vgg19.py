@@ -3,7 +3,8 @@
 The reference pulls ImageNet weights from torchvision at construction (a network fetch this
 environment cannot make); here the layers are built with the same indices so a locally
 saved ``slice{1..5}.{idx}.{weight,bias}`` state_dict loads strictly.  Forward = the training
-path's loss features (PyTorch-ROCm ops; gradients flow to the input image).
+path's loss features: on a ROCm device the HIP kernels (zero-pad Winograd / implicit-GEMM convs,
+fused ReLU, max-pool, fused normalise; gradients flow to the input image), on the CPU aten.
 """
 import torch.nn as nn
 

@@ -2,8 +2,10 @@
 
 Parameters live in the same torch containers the reference uses (``nn.Conv2d``,
 ``nn.MultiheadAttention``, ``nn.Linear``, ``nn.LayerNorm``) so the state_dict keys match
-exactly; the forward pass never calls their aten forwards — it runs
-``mhada_hip.engine.vit_forward`` (HIP kernels).
+exactly.  On a ROCm device the forward never calls their aten forwards — it runs
+``mhada_hip.engine.vit_forward`` (HIP kernels) for inference and the HIP training kernels under
+autograd; CPU tensors (the reference's no-GPU branch, ``infer_image.py:48``) run the aten CPU
+form in ``mhada_hip.autograd_path``.
 """
 from typing import List
 
@@ -61,6 +63,9 @@ class VisionTransformer(nn.Module):
             [EncoderBlock(num_heads=num_heads, hidden_dim=hidden_dim, mlp_dim=mlp_dim) for _ in range(num_layers)])
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
-        if autograd_path.needs_grad(self, x):  # training / feature inversion: autograd v1
+        # training / feature inversion (autograd over the HIP training kernels), or a CPU
+        # tensor: infer_image.py:48 runs the modules on "cpu" when no GPU is present, and the
+        # aten CPU form of the same expression serves that call
+        if not x.is_cuda or autograd_path.needs_grad(self, x):
             return autograd_path.vit_forward(self, x)
         return engine.vit_forward(self, x)

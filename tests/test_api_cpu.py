@@ -51,15 +51,24 @@ def test_constructor_errors_mirror_reference():
     network.AdaAttnTransformerMultiHead(activation="cosine")
 
 
-def test_forward_refuses_cpu_tensors():
-    """Inference (no autograd) runs only on the HIP kernels: no CPU fallback."""
+def test_cpu_tensors_take_the_aten_form_not_the_engine(monkeypatch):
+    """infer_image.py:48 picks "cpu" when no GPU is present: CPU tensors run the aten form of the
+    reference expression (autograd_path), never the HIP engine (whose launches would need device
+    pointers).  Device tensors are the only ones the engine sees."""
+    from mhada_hip import engine
+
+    def boom(*a, **k):
+        raise AssertionError("the HIP engine must not be called with CPU tensors")
+    for name in ("vit_forward", "adaformer_forward", "block_forward", "decoder_forward_tokens"):
+        monkeypatch.setattr(engine, name, boom)
     vit = network.VisionTransformer()
-    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
-        vit(torch.rand(1, 3, 64, 64) * 255)
     ada = network.AdaAttnTransformerMultiHead()
-    f = [torch.rand(1, 512, 8, 8)] * 3
-    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm device"):
-        ada(f, f)
+    with torch.no_grad():
+        f = vit(torch.rand(1, 3, 64, 64) * 255)
+        fcs, cs = ada(f, f)
+        blk = ada.adaAttnHead[0](f[0], f[0], f[0])
+    assert cs.shape == (1, 3, 64, 64) and torch.isfinite(cs).all()
+    assert blk.shape == (1, 512, 8, 8) and torch.isfinite(blk).all()
 
 
 def test_compute_dtype_resolution():
@@ -123,3 +132,12 @@ def test_abi_argument_errors_without_gpu():
     assert lib.mhada_gemm(args, None) == 1
     assert b"compute" in lib.mhada_last_error()
     assert lib.mhada_attn(*([None] * 8), 0, 1, 8, 64, 64, 0, None) == 1
+
+
+def test_wino_eligible_respects_32bit_offsets():
+    """shapes past the Winograd kernel's 32-bit element offsets fall back to the
+    implicit-GEMM conv instead of raising (meta tensors: no memory, no GPU)."""
+    from mhada_hip import ops
+    w = torch.empty(64, 9 * 64, dtype=torch.float32, device="meta")
+    assert ops.wino_eligible(torch.empty(8, 512, 512, 64, device="meta"), w, False)
+    assert not ops.wino_eligible(torch.empty(8, 2048, 2048, 64, device="meta"), w, False)

@@ -368,3 +368,65 @@ def test_instance_norm_tokens_vs_fp64(B, N, C):
     yd.backward(dy.double())
     assert rel(y, yd) < 2e-6
     assert rel(xs.grad, xd.grad) < 2e-5
+
+
+@pytest.mark.parametrize("M,C", [(32768, 512), (1000, 512), (37, 256), (300, 1024)])
+def test_layernorm_fn_vs_fp64(M, C):
+    """LayerNormFn (vit.py:54-55,58,62 under autograd) against fp64 F.layer_norm autograd: y, dx,
+    dgamma, dbeta; bit-identical on a second run (fixed-order column sums)."""
+    ln = torch.nn.LayerNorm(C, eps=1e-6).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(rnd(C, seed=5) * 0.5 + 1)
+        ln.bias.copy_(rnd(C, seed=6) * 0.1)
+    x = (rnd(M, C, seed=7) * 3 + 1).requires_grad_()
+    dy = rnd(M, C, seed=8)
+    outs = []
+    for _ in range(2):
+        ln.zero_grad()
+        x.grad = None
+        y = train_fns.layernorm(x, ln)
+        y.backward(dy)
+        outs.append((y.detach(), x.grad.clone(), ln.weight.grad.clone(), ln.bias.grad.clone()))
+    xd = x.detach().double().requires_grad_()
+    gd, bd = ln.weight.detach().double().requires_grad_(), ln.bias.detach().double().requires_grad_()
+    yd = F.layer_norm(xd, (C,), gd, bd, 1e-6)
+    yd.backward(dy.double())
+    for got, ref in zip(outs[0], (yd, xd.grad, gd.grad, bd.grad)):
+        assert rel(got, ref) < 1e-5
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("h,w", [(8, 8), (9, 16), (64, 64), (135, 240), (32, 32), (16, 40), (24, 5)])
+def test_pos_embed_fn_vs_fp64(h, w):
+    """PosEmbedFn (vit.py:91-92 under autograd): forward and the gather adjoint against fp64
+    F.interpolate(bilinear, align_corners=False) autograd; deterministic (bit-identical rerun)."""
+    pos = (rnd(1, 512, 32, 32, seed=9) * 0.02).requires_grad_()
+    g = rnd(h * w, 512, seed=10)
+    grads = []
+    for _ in range(2):
+        pos.grad = None
+        out = train_fns.pos_embed(pos, h, w)
+        out.backward(g)
+        grads.append(pos.grad.clone())
+    pd = pos.detach().double().requires_grad_()
+    ref = F.interpolate(pd, size=(h, w), mode="bilinear", align_corners=False)
+    ref = ref.reshape(512, h * w).t()
+    ref.backward(g.double())
+    assert rel(out, ref) < 1e-6
+    assert rel(grads[0], pd.grad) < 1e-6
+    assert torch.equal(grads[0], grads[1])
+
+
+def test_bf16_block_without_autocast_takes_aten_path():
+    """a bf16 MHAda block input outside autocast must not reach the fp32-only token
+    statistics kernels: it runs the aten formula and matches the fp32 block within bf16 rounding."""
+    import network
+    from mhada_hip.recipe import load_recipe
+    blk = load_recipe(network.AdaAttnMultiHead(512, 8), "blk").to(DEV).train()
+    fc, fs = rnd(2, 512, 4, 4, seed=11), rnd(2, 512, 3, 5, seed=12)
+    ref = blk(fc, fs, fc).detach()
+    blk16 = blk.to(torch.bfloat16)
+    out = blk16(fc.bfloat16(), fs.bfloat16(), fc.bfloat16())
+    assert out.dtype == torch.bfloat16 and torch.isfinite(out.float()).all()
+    assert rel(out.float(), ref) < 5e-2

@@ -78,6 +78,12 @@ def _dp_worker(rank, world, port, out_dir):
         grads = {n: p.grad.clone() for n, p in tr.ada.named_parameters()}
         grads.update({"vit_c." + n: p.grad.clone() for n, p in tr.vit_c.named_parameters()})
         torch.save(grads, os.path.join(out_dir, "dp_grads.pt"))
+    # after the Adam steps every rank holds the same parameters (bench.py's DP check)
+    for o in (tr.opt_vit_c, tr.opt_vit_s, tr.opt_ada):
+        o.step()
+    import bench
+    agree = bench.rank_agreement([tr.vit_c, tr.vit_s, tr.ada])
+    torch.save(agree, os.path.join(out_dir, f"agree_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -99,6 +105,9 @@ def test_data_parallel_allreduce_equals_accumulation(tmp_path):
     torch.set_num_threads(8)
     for n, g in acc.items():
         torch.testing.assert_close(dp[n], g, rtol=1e-4, atol=1e-5 * float(g.abs().max()))
+    for r in range(world):
+        agree = torch.load(tmp_path / f"agree_{r}.pt", weights_only=True)
+        assert agree["identical"] and agree["backend"] == "gloo" and agree["world"] == world, agree
 
 
 def _reducer_worker(rank, world, port, out_dir):
