@@ -413,8 +413,9 @@ def test_pos_embed_fn_vs_fp64(h, w):
     ref = F.interpolate(pd, size=(h, w), mode="bilinear", align_corners=False)
     ref = ref.reshape(512, h * w).t()
     ref.backward(g.double())
-    assert rel(out, ref) < 1e-6
-    assert rel(grads[0], pd.grad) < 1e-6
+    # fp32 source coordinates (the kernel, as aten's fp32 kernel) vs the fp64 reference's: 1e-5
+    assert rel(out, ref) < 1e-5
+    assert rel(grads[0], pd.grad) < 1e-5
     assert torch.equal(grads[0], grads[1])
 
 
