@@ -38,7 +38,9 @@ const Knob kKnobs[] = {
     {"out3_tile", &Tuning::out3_tile},               {"gemm_pp", &Tuning::gemm_pp},
     {"gemm_persist", &Tuning::gemm_persist},         {"gemm_pp128", &Tuning::gemm_pp128},
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
-    {"conv_c64", &Tuning::conv_c64},
+    {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
+    {"gemm_n64pp", &Tuning::gemm_n64pp},             {"attn_sched", &Tuning::attn_sched},
+    {"xknob", &Tuning::xknob},
 };
 
 Tuning g_tuning;
@@ -58,6 +60,7 @@ bool valid(const char* name, int v) {
   if (!strcmp(name, "attn_waves")) return v == 4 || v == 8;
   if (!strcmp(name, "attn_tk")) return v == 64 || v == 128;
   if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
+  if (!strcmp(name, "attn_sched") || !strcmp(name, "xknob")) return v >= 0 && v < 16;
   return v == 0 || v == 1;
 }
 }  // namespace

@@ -41,6 +41,10 @@ struct Tuning {
   int gemm_ldsepi = 1;       // ping-pong epilogue staged through LDS
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
+  int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
+  int gemm_n64pp = 1;        // N <= 64 bf16: 512x64 persistent ping-pong tile
+  int attn_sched = 0;        // bf16 fixed-shift attention: instruction-interleave variant (0 = compiler)
+  int xknob = 0;             // scratch knob for A/B experiments (no effect unless a kernel reads it)
 };
 const Tuning& tuning();
 

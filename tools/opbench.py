@@ -55,6 +55,11 @@ def gemm_suite():
                    "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
             fns["epi_direct"] = lambda: with_env("MHADA_GEMM_LDSEPI", "0", ops.linear, x, w, b, out, residual=r,
                                                  relu=relu)
+            if out == torch.bfloat16:
+                fns["epi8"] = lambda: with_env("MHADA_XKNOB", "1", ops.linear, x, w, b, out, residual=r, relu=relu)
+            if res:
+                fns["no_rinit"] = lambda: with_env("MHADA_GEMM_RINIT", "0", ops.linear, x, w, b, out, residual=r,
+                                                   relu=relu)
             if dt == torch.bfloat16:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
