@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_bf16_kernel(con
 // (attn_exact_half).  Branch-free clamped tile loads (keys past Ns re-read valid rows and are
 // masked in the last tile).
 // --------------------------------------------------------------------------------------
-template <int NW, int TK>
+template <int NW, int TK, bool EARLY = false>
 __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p) {
   constexpr int NT = 64 * NW, NKB = TK / 32;
   constexpr int LK = 72, LV = TK + 8;  // padded rows: conflict-free 16-B reads
@@ -561,6 +561,9 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
   for (int t = 1; t < NFULL; ++t) {
     const int cb = t & 1;
     issue(min(t + 1, NTILE - 1) * TK);
+    // EARLY: keep the next tile's global loads at the top of the iteration (hipcc otherwise sinks
+    // them next to their LDS writes, exposing the load latency right before the barrier)
+    if constexpr (EARLY) __builtin_amdgcn_sched_barrier(0);
     f32x16 S[NKB];
     qk(sK[cb], S, Cm);
     finish(sV[cb], S);
@@ -573,6 +576,313 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
     qk(sK[cb], S, Cm);
     mask_tile<MHADA_ACT_SOFTMAX, NKB>(S, NFULL * TK, Ns, h);
     finish(sV[cb], S);
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
+  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
+}
+
+// --------------------------------------------------------------------------------------
+// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3): attn_bf16_fs_kernel's loop with
+// the K / V'^T tiles staged by global_load_lds (16 B per lane) instead of through registers: no
+// staging registers, no LDS write pass, the next tile's DMA in flight for the whole iteration
+// (hipcc sinks the register-staged kernel's global loads next to their LDS writes).  LDS images
+// are lane-linear per wave-instruction and XOR-swizzled on the SOURCE address (rule 21): K rows
+// (128 B) keep 16-B chunk c at slot c ^ (row & 7); V'^T rows (256 B) at slot c ^ (row & 15); the
+// fragment reads apply the same XOR (conflict-free ds_read_b128).  2-slot ring, retired with
+// vmcnt(0) before the one barrier per tile.  Whole key tiles only.  (A second score set for
+// cross-tile pipelining at 128 keys spilled; attn_bf16_fsh_kernel pipelines by half tiles.)
+// --------------------------------------------------------------------------------------
+MHADA_DEV void attn_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p) {
+  constexpr int TK = 128, NKB = 4, NSL = 2;
+  constexpr int KSZ = TK * 64, VSZ = 128 * TK;  // bf16 elements per slot: K [128][64], V'^T [128][128]
+  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;  // 1-KiB pieces per wave
+  static_assert(KPW >= 1 && VPW >= 1, "tile config");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 96 KiB, the only LDS object
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r32 = lane & 31;
+  const int q = qb * (32 * NW) + wave * 32 + r32;
+  const long long bh = (long long)b * p.H + hh;
+  const int Ns = p.Ns;
+  const f32x16 zero = {};
+
+  bf16x8 qf[4];
+  {
+    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+      if (q >= p.Nc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
+      }
+    }
+  }
+  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
+  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
+  // per-lane source offsets (elements) of this wave's pieces, relative to the tile's first key
+  int ksrc[KPW], vsrc[VPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
+    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
+    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
+  }
+  auto stage = [&](int key0, int sl) {
+    bf16* kd = smem + sl * (KSZ + VSZ);
+    bf16* vd = kd + KSZ;
+    const bf16* ks = kvb + (long long)key0 * 128;
+    const bf16* vs = vtb + key0;
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
+  };
+  auto qk = [&](int sl, f32x16 (&S)[NKB], const f32x16& init) {
+    const bf16* ck = smem + sl * (KSZ + VSZ);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      const bf16* krow = ck + (kb * 32 + r32) * 64;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ (r32 & 7)));
+        S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[kb], 0, 0, 0);
+      }
+    }
+  };
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) O[i] = zero;
+  float l = 0.f;
+  auto finish = [&](int sl, const f32x16 (&S)[NKB]) {
+    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = fast_exp2(S[kb][8 * s + j]);
+          part[j & 3] += e;
+          pf[j] = (bf16)e;
+        }
+        const int ch = (4 * kb + 2 * s + h) ^ (r32 & 15);
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (blk * 32 + r32) * TK + 8 * ch);
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
+        }
+      }
+    }
+    l += (part[0] + part[1]) + (part[2] + part[3]);
+  };
+
+  const int NTILE = Ns / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16 Sa[NKB], Cm;
+  {  // tile 0: unshifted scores, m2 = their max, then shift
+    qk(0, Sa, zero);
+    const float m2 = tile_max_log2<NKB>(Sa);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Sa[kb][r] -= m2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Cm[r] = -m2;
+  }
+  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  {
+    // tile t+1's LDS-DMA into the other slot (last read in iteration t-1, before its barrier)
+    // flies during tile t's MFMAs; retired at the end of the iteration
+    if (NTILE > 1) stage(TK, 1);
+    finish(0, Sa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int t = 1; t < NTILE; ++t) {
+      if (t + 1 < NTILE) stage((t + 1) * TK, (t + 1) & 1);
+      qk(t & 1, Sa, Cm);
+      finish(t & 1, Sa);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
+  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
+}
+
+// --------------------------------------------------------------------------------------
+// Half-tile pipelined fixed-shift kernel (tuning attn_sched = 5, the bf16 softmax default when Ns % 128 == 0).  A 128-key tile's scores are
+// two halves, A (keys 0-63) and B (64-127), 32 registers each; iteration t runs
+//   step 1: QK^T of half B of tile t      beside  exp / row sum / pack / PV of half A of tile t
+//   step 2: QK^T of half A of tile t+1    beside  exp / row sum / pack / PV of half B of tile t
+// so every MFMA group has independent VALU next to it inside the wave, with the SAME 64 score
+// registers as the unpipelined kernel.  K / V'^T tiles arrive by LDS-DMA (attn_bf16_fsg_kernel's
+// swizzled images) into a 3-slot ring; the one barrier per tile sits between the two steps:
+// before it each wave retires tile t+1's pieces (vmcnt(0)), after it tile t+2 is issued into
+// the slot tile t-1 left (its last reads, step 2 of iteration t-1, precede the barrier).
+// --------------------------------------------------------------------------------------
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p) {
+  constexpr int TK = 128, NSL = 3;
+  constexpr int KSZ = TK * 64, VSZ = 128 * TK;
+  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;
+  static_assert(KPW >= 1 && VPW >= 1, "tile config");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 144 KiB, the only LDS object
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r32 = lane & 31;
+  const int q = qb * (32 * NW) + wave * 32 + r32;
+  const long long bh = (long long)b * p.H + hh;
+  const int Ns = p.Ns;
+  const f32x16 zero = {};
+
+  bf16x8 qf[4];
+  {
+    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+      if (q >= p.Nc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
+      }
+    }
+  }
+  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
+  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
+  int ksrc[KPW], vsrc[VPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
+    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
+    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
+  }
+  auto stage = [&](int key0, int sl) {
+    bf16* kd = smem + sl * (KSZ + VSZ);
+    bf16* vd = kd + KSZ;
+    const bf16* ks = kvb + (long long)key0 * 128;
+    const bf16* vs = vtb + key0;
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
+  };
+  // half hf (0: keys 0-63 = key blocks 0,1; 1: keys 64-127 = key blocks 2,3) of a tile
+  auto qk = [&](int sl, int hf, f32x16 (&S)[2], const f32x16& init) {
+    const bf16* ck = smem + sl * (KSZ + VSZ);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16* krow = ck + ((2 * hf + j) * 32 + r32) * 64;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ (r32 & 7)));
+        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[j], 0, 0, 0);
+      }
+    }
+  };
+  f32x16 O[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) O[i] = zero;
+  float l = 0.f;
+  auto finish = [&](int sl, int hf, const f32x16 (&S)[2]) {
+    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kb = 2 * hf + j;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pf;
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) {
+          const float e = fast_exp2(S[j][8 * s + e8]);
+          part[e8 & 3] += e;
+          pf[e8] = (bf16)e;
+        }
+        const int ch = (4 * kb + 2 * s + h) ^ (r32 & 15);
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (blk * 32 + r32) * TK + 8 * ch);
+          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
+        }
+      }
+    }
+    l += (part[0] + part[1]) + (part[2] + part[3]);
+  };
+
+  const int NTILE = Ns / TK;
+  stage(0, 0);
+  if (NTILE > 1) stage(TK, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (NTILE > 2) stage(2 * TK, 2);
+  f32x16 SA[2], SB[2], Cm;
+  {  // tile 0: unshifted scores of both halves, m2 = their max, then shift
+    qk(0, 0, SA, zero);
+    qk(0, 1, SB, zero);
+    float mx = SA[0][0];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(SA[j][r], SB[j][r]));
+    const float m2 = fmaxf(mx, __shfl_xor(mx, 32, 64));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        SA[j][r] -= m2;
+        SB[j][r] -= m2;
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Cm[r] = -m2;
+  }
+  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // iteration 0: half B's scores are already there
+  finish(0, 0, SA);
+  if (NTILE > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 2 (issued above) is tile t+2 here
+    __builtin_amdgcn_s_barrier();
+    qk(1, 0, SA, Cm);
+  }
+  finish(0, 1, SB);
+  int sl = 1;  // t % 3
+  for (int t = 1; t + 1 < NTILE; ++t) {
+    const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;
+    qk(sl, 1, SB, Cm);  // step 1
+    finish(sl, 0, SA);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (this wave's pieces)
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < NTILE) stage((t + 2) * TK, sl2);
+    qk(sl1, 0, SA, Cm);  // step 2
+    finish(sl, 1, SB);
+    sl = sl1;
+  }
+  if (NTILE > 1) {  // last tile
+    qk(sl, 1, SB, Cm);
+    finish(sl, 0, SA);
+    finish(sl, 1, SB);
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
@@ -596,6 +906,18 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
   } else {
     if constexpr (NW == 8) {
       if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift()) {
+        if (tuning().attn_sched == 3 && p.Ns % 128 == 0) {  // LDS-DMA staging, 128-key tiles
+          hipLaunchKernelGGL((attn_bf16_fsg_kernel<8>), grid, blk, 0, s, p);
+          return;
+        }
+        if (tuning().attn_sched == 5 && p.Ns % 128 == 0) {  // half-tile pipelined, LDS-DMA staging
+          hipLaunchKernelGGL((attn_bf16_fsh_kernel<8>), grid, blk, 0, s, p);
+          return;
+        }
+        if (tuning().attn_sched == 4 && attn_tk() == 128) {  // register staging, loads kept early
+          hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 128, true>), grid, blk, 0, s, p);
+          return;
+        }
         if (attn_tk() == 128) hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 128>), grid, blk, 0, s, p);
         else hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 64>), grid, blk, 0, s, p);
         return;

@@ -345,12 +345,21 @@ def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
     return out * f + mm + v_mu.double()[:, None]
 
 
-@pytest.mark.parametrize("kernel", ["fs", "w8"])
-@pytest.mark.parametrize("Nc,Ns", [(300, 700), (256, 128), (97, 33)])
+# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsh" (half-tile pipelined,
+# LDS-DMA; the default when Ns % 128 == 0), "fsg" (LDS-DMA), "fsE" (register staging, early
+# loads), "fs" (register staging; the default for ragged Ns) — and the online-max kernel "w8".
+# Variants that need whole 128-key tiles fall back to "fs" on ragged Ns.
+ATTN_VARIANTS = {"fsh": dict(attn_fixed_shift=1, attn_sched=5), "fsg": dict(attn_fixed_shift=1, attn_sched=3),
+                 "fsE": dict(attn_fixed_shift=1, attn_sched=4), "fs": dict(attn_fixed_shift=1, attn_sched=0),
+                 "w8": dict(attn_fixed_shift=0)}
+
+
+@pytest.mark.parametrize("kernel", list(ATTN_VARIANTS))
+@pytest.mark.parametrize("Nc,Ns", [(300, 700), (256, 128), (97, 33), (256, 1024), (97, 384)])
 def test_mhada_attn_late_max_jump(kernel, Nc, Ns):
     """A key far beyond the first tile's scores (> 2^64 in P against the first tile's max): the
-    fixed-shift kernel ("fs", attn.hip) must take its exact-recompute path, the online-max
-    kernel ("w8") its rescale branch; both against fp64 torch on the same bf16 operands."""
+    fixed-shift kernels must take their exact-recompute path, the online-max kernel ("w8") its
+    rescale branch; all against fp64 torch on the same bf16 operands."""
     B, H = 1, 8
     q = rnd(B, H, Nc, 64, seed=11)
     q = q / q.norm(dim=-1, keepdim=True) * 4.0
@@ -363,20 +372,20 @@ def test_mhada_attn_late_max_jump(kernel, Nc, Ns):
     fcs = rnd(B, Nc, 512, seed=13)
     mu, rs = ops.instnorm_stats(fcs)
     vmu = rnd(B, 512, seed=14)
-    with _lib.tuning(attn_fixed_shift=int(kernel == "fs")):
+    with _lib.tuning(**ATTN_VARIANTS[kernel]):
         y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
     ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
     assert torch.isfinite(y.float()).all()
     assert rel(y.float(), ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("kernel", ["fs", "w8"])
+@pytest.mark.parametrize("kernel", list(ATTN_VARIANTS))
 @pytest.mark.parametrize("B,Nc,Ns", [(1, 256, 64), (2, 300, 100), (1, 513, 128), (1, 97, 1000), (2, 1000, 777),
-                                     (1, 64, 4096)])
+                                     (1, 64, 4096), (2, 300, 256), (1, 97, 384), (1, 520, 1024)])
 def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
-    """The bf16 softmax kernels (fixed shift "fs", online max "w8") at 1..32 key tiles of 128,
-    ragged and whole, and partial query blocks: against fp64 torch on the same bf16 operands
-    (bf16 P: 1e-2)."""
+    """The bf16 softmax kernels (ATTN_VARIANTS) at 1..32 key tiles of 128, ragged and whole (1, 2,
+    3 and 8 whole tiles exercise the pipelined kernels' prologue, odd tile counts and the 3-slot
+    ring), and partial query blocks: against fp64 torch on the same bf16 operands (bf16 P: 1e-2)."""
     H = 8
     q = (rnd(B, H, Nc, 64, seed=15) * 0.35).bfloat16()
     kv = (rnd(B, H, Ns, 128, seed=16) * 0.35).bfloat16()
@@ -384,7 +393,7 @@ def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
     fcs = rnd(B, Nc, 512, seed=17)
     mu, rs = ops.instnorm_stats(fcs)
     vmu = rnd(B, 512, seed=18)
-    with _lib.tuning(attn_fixed_shift=int(kernel == "fs")):
+    with _lib.tuning(**ATTN_VARIANTS[kernel]):
         y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
     ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
     assert rel(y.float(), ref) < 1e-2

@@ -17,9 +17,13 @@ SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1
           ("ragged", 2, 1000, 777)]
 
 
-VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128},
-            "fs64": {"attn_fixed_shift": 1, "attn_tk": 64},
-            "w8": {"attn_fixed_shift": 0, "attn_tk": 128}}
+VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 0},
+            "fs64": {"attn_fixed_shift": 1, "attn_tk": 64, "attn_sched": 0},
+            "fsp64": {"attn_fixed_shift": 1, "attn_sched": 1},
+            "fsh": {"attn_fixed_shift": 1, "attn_sched": 5},
+            "fsg": {"attn_fixed_shift": 1, "attn_sched": 3},
+            "fsE": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 4},
+            "w8": {"attn_fixed_shift": 0, "attn_tk": 128, "attn_sched": 0}}
 
 
 def run(variant, args):
@@ -56,6 +60,8 @@ def main():
         print(f"{name:18s} " + "   ".join(f"{v} {med[v]:.3f} ms {fl / med[v] / 1e9:.0f} TF (err {errs[v]:.1e})"
                                            for v in VARIANTS), flush=True)
     # fp32 (one kernel; compare with the launch averages in profiles/r01_attn_launch_stats.txt)
+    if os.environ.get("ATTN_AB_NO_F32"):
+        return
     for name, B, nc, ns in SHAPES[1:]:
         q = torch.randn(B, H, nc, 64, device="cuda") * 0.35
         kv = torch.randn(B, H, ns, 128, device="cuda") * 0.35
