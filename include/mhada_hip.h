@@ -256,6 +256,18 @@ int mhada_layernorm_bwd(const float* x, const float* dy, const float* stats, con
 /* Adjoint of mhada_pos_embed (vit.py:91-92 under autograd; replaces aten's atomic
  * upsample_bilinear2d_backward): g token-major [oh*ow][C] -> gpos [C][bh][bw], a gather per source
  * pixel in a fixed order (deterministic). */
+/* InstanceNorm2d(affine=False) backward on token rows [B][N][C] (adaDecoder.py:147-149 under
+ * autograd; replaces ~7 aten ops): dx = (dy - mean_N dy - y mean_N(dy y)) * rstd, y the normalised
+ * forward output.  work: splits*B*C*2 doubles + B*C*2 floats; C % 4 == 0, 16-byte aligned. */
+int mhada_instnorm_bwd(const float* dy, const float* y, const float* rstd, float* dx, double* work,
+                       int B, int N, int C, int splits, mhada_stream_t stream);
+
+/* Elementwise head of the MHAda attention-core backward (adaDecoder.py:189-198 under autograd):
+ * rows of 64 channels; mo = [M' | E2'] (rows x 128), x = IN(fcs) head rows, dout; writes dx,
+ * dmo = [dM' | dVar] (rows x 128) and dd = rowsum(dM' M' + dVar E2') for mhada_attn_train_bwd. */
+int mhada_attn_train_bwd_prep(const float* dout, const float* x, const float* mo, float* dx, float* dmo,
+                              float* dd, long long rows, mhada_stream_t stream);
+
 int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int oh, int ow,
                         mhada_stream_t stream);
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */

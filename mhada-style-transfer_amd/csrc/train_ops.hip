@@ -17,6 +17,11 @@
 //   mhada_layernorm_fwd / mhada_layernorm_bwd  nn.LayerNorm (vit.py:54-55,58,62; eps 1e-6) with
 //                     the row statistics kept for the backward; dX per row, dGamma / dBeta as
 //                     per-block column partials summed in a fixed order.
+//   mhada_instnorm_bwd  InstanceNorm (no affine) adjoint on token rows: column sums of dY and dY*Y
+//                     (fp64 partials, fixed order) and dX = (dY - mean dY - Y mean dY*Y) * rstd.
+//   mhada_attn_train_bwd_prep  the elementwise head of the MHAda attention backward
+//                     (S = sqrt(max(E2' - M'^2, 1e-6)), out' = S x + M'): dX, d[M'|E2'] and the
+//                     per-row dot delta, one pass instead of ~12 aten ops.
 //   mhada_pos_embed_bwd  adjoint of the PosEmbedding bilinear resize (vit.py:91-92): a gather
 //                     per source pixel (fixed order) in place of ATen's atomic scatter.
 //   mhada_vgg_input / mhada_vgg_input_bwd  imageNet1k_normalize (vgg19.py:6-12) fused with the
@@ -440,6 +445,108 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ x
     a += part[3][which][i][ln];
     *reinterpret_cast<f32x4*>(slab + (long long)blockIdx.x * 2 * COLS + which * COLS + (i * 64 + ln) * 4) = a;
   }
+}
+
+// ======================================================================================
+// InstanceNorm backward on token rows [B][N][C] (adaDecoder.py:147-149,188-190 under autograd):
+// m1 = mean_N(dy), m2 = mean_N(dy * y) per (b, c) — fp64 partials per (split, b, c) summed in a
+// fixed order — then dx = (dy - m1 - y m2) * rstd.
+// ======================================================================================
+__global__ void __launch_bounds__(256) inb_partial_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                          double* __restrict__ work, int B, int N, int C, int splits) {
+  __shared__ double red[2][16][65];
+  const int quad = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + 4 * quad;
+  const int b = blockIdx.y, s = blockIdx.z;
+  const int per = (N + splits - 1) / splits;
+  const int r0 = s * per, r1 = min(N, r0 + per);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c0 < C) {
+    const long long base = (long long)b * N * C + c0;
+#pragma unroll 4
+    for (int r = r0 + ph; r < r1; r += 16) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(dy + base + (long long)r * C);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(y + base + (long long)r * C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += (double)g[e];
+        s2[e] += (double)(g[e] * v[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][ph][4 * quad + e] = s1[e];
+    red[1][ph][4 * quad + e] = s2[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int t = threadIdx.x & 63, which = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + t;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += red[which][k][t];
+    if (c < C) work[(((long long)s * B + b) * C + c) * 2 + which] = a;
+  }
+}
+
+__global__ void __launch_bounds__(256) inb_finalize_kernel(const double* __restrict__ work, float* __restrict__ mm,
+                                                           int BC, int N, int splits) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= BC) return;
+  double a = 0.0, q = 0.0;
+  for (int s = 0; s < splits; ++s) {
+    a += work[((long long)s * BC + idx) * 2];
+    q += work[((long long)s * BC + idx) * 2 + 1];
+  }
+  mm[2 * idx] = (float)(a / N);
+  mm[2 * idx + 1] = (float)(q / N);
+}
+
+__global__ void __launch_bounds__(256) inb_apply_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                        const float* __restrict__ mm, const float* __restrict__ rs,
+                                                        float* __restrict__ dx, int N, int C, long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const long long e0 = 4 * i;
+  const int c = (int)(e0 % C);
+  const int b = (int)(e0 / ((long long)N * C));
+  const f32x4 g = reinterpret_cast<const f32x4*>(dy)[i];
+  const f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
+  const f32x4 r = *reinterpret_cast<const f32x4*>(rs + (long long)b * C + c);
+  const float4 m01 = *reinterpret_cast<const float4*>(mm + 2 * ((long long)b * C + c));
+  const float4 m23 = *reinterpret_cast<const float4*>(mm + 2 * ((long long)b * C + c) + 4);
+  const float m1[4] = {m01.x, m01.z, m23.x, m23.z}, m2[4] = {m01.y, m01.w, m23.y, m23.w};
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (g[e] - m1[e] - v[e] * m2[e]) * r[e];
+  reinterpret_cast<f32x4*>(dx)[i] = o;
+}
+
+// ======================================================================================
+// MHAda attention backward head: per row (bh, query) of 64 channels, with m = M', e2 = E2':
+//   var = e2 - m^2, sd = sqrt(max(var, 1e-6)), dx = dout sd,
+//   dvar = dout x 0.5 / sd where var >= 1e-6 (0 where the clamp is active), dm = dout - 2 m dvar,
+//   dmo = [dm | dvar], dd = sum_c (dm m + dvar e2).   One wave per row, lane = channel.
+// ======================================================================================
+__global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const float* __restrict__ dout, const float* __restrict__ x,
+                                                            const float* __restrict__ mo, float* __restrict__ dx,
+                                                            float* __restrict__ dmo, float* __restrict__ dd,
+                                                            long long rows) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int c = threadIdx.x & 63;
+  const float m = mo[row * 128 + c], e2 = mo[row * 128 + 64 + c];
+  const float g = dout[row * 64 + c], xv = x[row * 64 + c];
+  const float var = e2 - m * m;
+  const float sd = sqrtf(fmaxf(var, 1e-6f));
+  const float dvar = var >= 1e-6f ? (g * xv) * (0.5f / sd) : 0.f;
+  const float dm = g - 2.0f * m * dvar;
+  dx[row * 64 + c] = g * sd;
+  dmo[row * 128 + c] = dm;
+  dmo[row * 128 + 64 + c] = dvar;
+  const float t = wave_sum(dm * m + dvar * e2);
+  if (c == 0) dd[row] = t;
 }
 
 // ======================================================================================
@@ -886,6 +993,31 @@ extern "C" int mhada_layernorm_bwd(const float* x, const float* dy, const float*
       hipMemcpyAsync(dbeta, red + cols, sizeof(float) * cols, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return fail("mhada_layernorm_bwd: copy");
   return 0;
+}
+
+extern "C" int mhada_instnorm_bwd(const float* dy, const float* y, const float* rstd, float* dx, double* work,
+                                  int B, int N, int C, int splits, mhada_stream_t s_) {
+  if (!dy || !y || !rstd || !dx || !work || B <= 0 || N <= 0 || C <= 0 || splits <= 0 || splits > 65535)
+    return fail("mhada_instnorm_bwd: bad args");
+  if (C % 4 || !al16(dy) || !al16(y) || !al16(rstd) || !al16(dx) || !al16(work))
+    return fail("mhada_instnorm_bwd: C % 4 == 0 and 16-byte aligned operands");
+  hipStream_t s = (hipStream_t)s_;
+  hipLaunchKernelGGL(inb_partial_kernel, dim3((C + 63) / 64, B, splits), dim3(256), 0, s, dy, y, work, B, N, C, splits);
+  if (int rc = check_launch("mhada_instnorm_bwd/partial")) return rc;
+  float* mm = reinterpret_cast<float*>(work + (long long)splits * B * C * 2);  // [B][C][2] means
+  hipLaunchKernelGGL(inb_finalize_kernel, grid1((long long)B * C), dim3(256), 0, s, work, mm, B * C, N, splits);
+  if (int rc = check_launch("mhada_instnorm_bwd/finalize")) return rc;
+  const long long n4 = (long long)B * N * C / 4;
+  hipLaunchKernelGGL(inb_apply_kernel, grid1(n4), dim3(256), 0, s, dy, y, mm, rstd, dx, N, C, n4);
+  return check_launch("mhada_instnorm_bwd/apply");
+}
+
+extern "C" int mhada_attn_train_bwd_prep(const float* dout, const float* x, const float* mo, float* dx, float* dmo,
+                                         float* dd, long long rows, mhada_stream_t s_) {
+  if (!dout || !x || !mo || !dx || !dmo || !dd || rows <= 0) return fail("mhada_attn_train_bwd_prep: bad args");
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)s_, dout, x,
+                     mo, dx, dmo, dd, rows);
+  return check_launch("mhada_attn_train_bwd_prep");
 }
 
 extern "C" int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int oh, int ow,

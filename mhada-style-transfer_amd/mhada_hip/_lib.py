@@ -81,6 +81,8 @@ SIGNATURES = {
     "mhada_layernorm_fwd": (_I, [_vp, _vp, _vp, _vp, _vp, _I, _I, _F, _vp]),
     "mhada_layernorm_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _vp]),
     "mhada_pos_embed_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_instnorm_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_attn_train_bwd_prep": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),

@@ -125,16 +125,10 @@ class MHAdaAttnFn(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dout):
         q, k, v, x, mo, lse = ctx.saved_tensors
-        dout = dout.contiguous()
-        m, e2 = mo[..., :64], mo[..., 64:]
-        var = e2 - m * m
-        sd = var.clamp(min=1e-6).sqrt()
-        dx = dout * sd
-        dvar = (dout * x) * (0.5 / sd) * (var >= 1e-6)  # clamp passes the gradient where var >= min
-        dm = dout - 2.0 * m * dvar
-        dmo = torch.cat([dm, dvar], dim=-1)
-        dd = (dm * m + dvar * e2).sum(dim=-1)
-        dq, dk, dv = ops.attn_train_bwd(q, k, v, lse, dmo.contiguous(), dd.contiguous())
+        # S = sqrt(max(E2' - M'^2, 1e-6)), out' = S x + M': dx = dout S, dVar = dout x / (2 S) where
+        # the clamp is inactive, dM' = dout - 2 M' dVar, dd = rowsum(dM' M' + dVar E2')  (one kernel)
+        dx, dmo, dd = ops.attn_train_bwd_prep(dout.contiguous(), x, mo)
+        dq, dk, dv = ops.attn_train_bwd(q, k, v, lse, dmo, dd)
         return dq, dk, dv, dx
 
 

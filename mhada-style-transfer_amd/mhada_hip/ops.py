@@ -253,6 +253,37 @@ def pos_embed_bwd(g: torch.Tensor, bh: int, bw: int) -> torch.Tensor:
     return out
 
 
+def instnorm_bwd(dy: torch.Tensor, y: torch.Tensor, rs: torch.Tensor) -> torch.Tensor:
+    """``mhada_instnorm_bwd``: token rows dy, y [B][N][C], rstd [B][C] -> dx."""
+    _need_gpu(dy, y, rs)
+    for t in (dy, y, rs):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("instnorm_bwd needs contiguous float32 operands")
+    B, N, C = y.shape
+    if dy.shape != y.shape or rs.shape != (B, C):
+        raise ValueError("instnorm_bwd: shape mismatch")
+    splits = max(1, min(N // 32, 2048 // max(1, B * ((C + 63) // 64))))
+    work = torch.empty(splits * B * C * 2 + B * C, device=y.device, dtype=torch.float64)
+    dx = torch.empty_like(y)
+    _call("mhada_instnorm_bwd", y, dy.data_ptr(), y.data_ptr(), rs.data_ptr(), dx.data_ptr(), work.data_ptr(), B, N, C,
+          splits)
+    return dx
+
+
+def attn_train_bwd_prep(dout: torch.Tensor, x: torch.Tensor, mo: torch.Tensor):
+    """``mhada_attn_train_bwd_prep``: (dx, dmo, dd) of the MHAda core's elementwise head."""
+    _rows64(dout, x, mo)
+    BH, Nc, _ = x.shape
+    if dout.shape != x.shape or mo.shape != (BH, Nc, 128):
+        raise ValueError("attn_train_bwd_prep: bad shapes")
+    dx = torch.empty_like(x)
+    dmo = torch.empty_like(mo)
+    dd = torch.empty(BH, Nc, device=x.device, dtype=torch.float32)
+    _call("mhada_attn_train_bwd_prep", x, dout.data_ptr(), x.data_ptr(), mo.data_ptr(), dx.data_ptr(), dmo.data_ptr(),
+          dd.data_ptr(), BH * Nc)
+    return dx, dmo, dd
+
+
 def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float):
     """``mhada_layernorm_fwd``: fp32 rows [M][C] -> (y fp32, stats [M][2])."""
     _need_gpu(x, gamma, beta)

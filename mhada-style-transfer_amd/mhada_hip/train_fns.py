@@ -202,10 +202,7 @@ class InstanceNormTokensFn(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
         y, rs = ctx.saved_tensors
-        dy = dy.contiguous()
-        m1 = dy.mean(dim=1, keepdim=True)
-        m2 = (dy * y).mean(dim=1, keepdim=True)
-        return (dy - m1 - y * m2) * rs.unsqueeze(1)
+        return ops.instnorm_bwd(dy.contiguous(), y, rs)
 
 
 def instance_norm_tokens(x: torch.Tensor) -> torch.Tensor:

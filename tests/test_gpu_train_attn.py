@@ -57,6 +57,26 @@ def test_attn_train_fwd_bwd_vs_fp64(BH, Nc, Ns, scale):
         assert err < max(2e-4, 3 * err32), (name, err, err32)
 
 
+def test_attn_train_bwd_with_clamped_variance():
+    """Channels whose attention-weighted variance is below the 1e-6 clamp (constant V' there): the
+    clamp's gradient is zero in those channels (mhada_attn_train_bwd_prep), as in fp64 autograd."""
+    g = torch.Generator().manual_seed(5)
+    BH, Nc, Ns = 2, 128, 96
+    q = torch.randn(BH, Nc, 64, generator=g) * 0.4
+    k = torch.randn(BH, Ns, 64, generator=g) * 0.4
+    v = torch.randn(BH, Ns, 64, generator=g) * 3
+    v = v - v.mean(dim=1, keepdim=True)
+    v[:, :, :5] = 0.0  # var = 0 < 1e-6: the clamp is active in channels 0-4
+    x = torch.randn(BH, Nc, 64, generator=g)
+    dout = torch.randn(BH, Nc, 64, generator=g)
+    ts = [t.double().requires_grad_() for t in (q, k, v, x)]
+    _ref(*ts).backward(dout.double())
+    gs = [t.cuda().contiguous().requires_grad_() for t in (q, k, v, x)]
+    autograd_path.MHAdaAttnFn.apply(*gs).backward(dout.cuda())
+    for name, a, b in zip("qkvx", gs, ts):
+        assert _rel(a.grad.double().cpu(), b.grad) < 2e-4, name
+
+
 @pytest.mark.parametrize("BH,Nc,Ns", [(2, 128, 64), (1, 37, 300), (3, 500, 256), (2, 33, 4)])
 def test_attn_train_bwd_ds_spill_matches_recompute(BH, Nc, Ns):
     """dS spilled by the dK/dV' kernel + dQ = dS K as a batched GEMM (ops.attn_train_bwd's default)
