@@ -355,7 +355,10 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[e] += q[e];
             }
-            *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+            if (p.lds_epi == 3)  // A/B: non-temporal stores (xknob bit 2)
+              __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4*>(crow + n));
+            else
+              *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
           } else {
             if (rrow) {
               const bf16x4 q = *reinterpret_cast<const bf16x4*>(rrow + n);
@@ -436,7 +439,10 @@ MHADA_DEV void store_tile_lds_bf16(const GemmP& p, const f32x16 (&acc)[TM][2], i
       if (m >= p.M) continue;
       bf16* crow = cbase + (long long)m * p.ldc;
       if (n + 7 < p.N && ((p.ldc & 7) == 0)) {
-        *reinterpret_cast<bf16x8*>(crow + n) = v[i];
+        if (p.lds_epi == 3)  // A/B: non-temporal stores (xknob bit 2)
+          __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&v[i]), reinterpret_cast<f32x4*>(crow + n));
+        else
+          *reinterpret_cast<bf16x8*>(crow + n) = v[i];
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -1035,7 +1041,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       if (p.lds_epi) {
         float* scr = reinterpret_cast<float*>(smem + NSLOT * TILE) + wave * 1024;
         if constexpr (sizeof(TO) == 2 && TN == 2) {
-          if (p.lds_epi == 1)
+          if (p.lds_epi != 2)
             store_tile_lds_bf16<4>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
           else
             store_tile_lds<TO, 4, TN>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
@@ -1078,7 +1084,7 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
   // 1: LDS-staged epilogue (bf16 output: 16-B stores), 2: LDS-staged with the 8-B bf16 stores (A/B
   // through xknob bit 0), 0: direct stores
-  p.lds_epi = tuning().gemm_ldsepi ? ((tuning().xknob & 1) ? 2 : 1) : 0;
+  p.lds_epi = tuning().gemm_ldsepi ? ((tuning().xknob & 1) ? 2 : ((tuning().xknob & 4) ? 3 : 1)) : 0;
   // residual rows preloaded into the accumulators: fp32 output with a residual, no ReLU (the
   // reference adds the residual after the activation), 16-B aligned rows
   p.rinit = (sizeof(TO) == 4 && p.r && !p.relu && tuning().gemm_rinit && ((uintptr_t)p.r & 15) == 0 &&

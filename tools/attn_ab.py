@@ -17,10 +17,9 @@ SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1
           ("ragged", 2, 1000, 777)]
 
 
-VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 0},
-            "fs64": {"attn_fixed_shift": 1, "attn_tk": 64, "attn_sched": 0},
-            "fsp64": {"attn_fixed_shift": 1, "attn_sched": 1},
-            "fsh": {"attn_fixed_shift": 1, "attn_sched": 5},
+VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 0, "attn_prio": 1},
+            "fsh": {"attn_fixed_shift": 1, "attn_sched": 5, "attn_prio": 1},
+            "fshP0": {"attn_fixed_shift": 1, "attn_sched": 5, "attn_prio": 0},
             "fsg": {"attn_fixed_shift": 1, "attn_sched": 3},
             "fsE": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 4},
             "w8": {"attn_fixed_shift": 0, "attn_tk": 128, "attn_sched": 0}}

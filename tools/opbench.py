@@ -57,6 +57,7 @@ def gemm_suite():
                                                  relu=relu)
             if out == torch.bfloat16:
                 fns["epi8"] = lambda: with_env("MHADA_XKNOB", "1", ops.linear, x, w, b, out, residual=r, relu=relu)
+            fns["epi_nt"] = lambda: with_env("MHADA_XKNOB", "4", ops.linear, x, w, b, out, residual=r, relu=relu)
             if res:
                 fns["no_rinit"] = lambda: with_env("MHADA_GEMM_RINIT", "0", ops.linear, x, w, b, out, residual=r,
                                                    relu=relu)
