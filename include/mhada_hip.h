@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 6 (LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 7 (gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -88,6 +88,15 @@ typedef struct mhada_gemm_args {
   void* c; int c_dtype; long long ldc, sc1, sc2;
   int relu;
   int pad;      /* CONV3X3_ZERO only: 1 or 2 (0 = 1) */
+  /* Optional second output (NULL = none): a bf16 copy of C (row stride ldc2, z-strides
+   * sc21/sc22), fp32 C only — the last MHAda block's fcs, fp32 for the caller and bf16 for the
+   * decoder's first conv. */
+  void* c2; long long ldc2, sc21, sc22;
+  /* Optional V' transpose (NULL = none; the MHAda K|V' projection, N = 128): columns 64..127
+   * are NOT written to C but to vt[o][pos(m)] = V'[m][o] and vt[64 + o][pos(m)] = V'[m][o]^2
+   * (dtype of C; row stride ldt >= M rounded up to 64, z-strides svt1/svt2; pos = the
+   * mhada_transpose_v key order; positions M..ldt-1 written 0).  Replaces mhada_transpose_v. */
+  void* vt; long long ldt, svt1, svt2;
 } mhada_gemm_args;
 
 int mhada_gemm(const mhada_gemm_args* args, mhada_stream_t stream);

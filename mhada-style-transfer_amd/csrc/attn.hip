@@ -583,13 +583,16 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 }
 
 // --------------------------------------------------------------------------------------
-// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3): attn_bf16_fs_kernel's loop with
+// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3, the bf16 softmax default when
+// Ns % 128 == 0; 4.5 % faster than register staging at 1024^2 B4): attn_bf16_fs_kernel's loop with
 // the K / V'^T tiles staged by global_load_lds (16 B per lane) instead of through registers: no
 // staging registers, no LDS write pass, the next tile's DMA in flight for the whole iteration
 // (hipcc sinks the register-staged kernel's global loads next to their LDS writes).  LDS images
 // are lane-linear per wave-instruction and XOR-swizzled on the SOURCE address (rule 21): K rows
-// (128 B) keep 16-B chunk c at slot c ^ (row & 7); V'^T rows (256 B) at slot c ^ (row & 15); the
-// fragment reads apply the same XOR (conflict-free ds_read_b128).  2-slot ring, retired with
+// (128 B, two per 256-B bank row) keep 16-B chunk c at slot c ^ ((row >> 1) & 7) — the rows of
+// a ds_read_b128 lane group then land on 16 distinct slots (c ^ (row & 7) left them 2-way
+// conflicted: PMC SQ_LDS_BANK_CONFLICT 1.3e8 cycles per launch); V'^T rows (256 B) at slot
+// c ^ (row & 15); the fragment reads apply the same XOR (conflict-free ds_read_b128).  2-slot ring, retired with
 // vmcnt(0) before the one barrier per tile.  Whole key tiles only.  (A second score set for
 // cross-tile pipelining at 128 keys spilled; attn_bf16_fsh_kernel pipelines by half tiles.)
 // --------------------------------------------------------------------------------------
@@ -633,7 +636,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
 #pragma unroll
   for (int i = 0; i < KPW; ++i) {
     const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+    ksrc[i] = row * 128 + 8 * (slot ^ ((row >> 1) & 7));
   }
 #pragma unroll
   for (int i = 0; i < VPW; ++i) {
@@ -657,7 +660,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
       const bf16* krow = ck + (kb * 32 + r32) * 64;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ (r32 & 7)));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ ((r32 >> 1) & 7)));
         S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[kb], 0, 0, 0);
       }
     }
@@ -728,7 +731,8 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
 }
 
 // --------------------------------------------------------------------------------------
-// Half-tile pipelined fixed-shift kernel (tuning attn_sched = 5, the bf16 softmax default when Ns % 128 == 0).  A 128-key tile's scores are
+// Half-tile pipelined fixed-shift kernel (tuning attn_sched = 5; 1.2 % slower than the LDS-DMA kernel
+// once the K image's bank conflicts were fixed, kept as the measured alternative).  A 128-key tile's scores are
 // two halves, A (keys 0-63) and B (64-127), 32 registers each; iteration t runs
 //   step 1: QK^T of half B of tile t      beside  exp / row sum / pack / PV of half A of tile t
 //   step 2: QK^T of half A of tile t+1    beside  exp / row sum / pack / PV of half B of tile t
@@ -737,7 +741,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
 // swizzled images) into a 3-slot ring; the one barrier per tile sits between the two steps:
 // before it each wave retires tile t+1's pieces (vmcnt(0)), after it tile t+2 is issued into
 // the slot tile t-1 left (its last reads, step 2 of iteration t-1, precede the barrier).
-// Measured: +4.4 % over the register-staged kernel at 1024^2 B4; an explicit sched_group_barrier
+// Measured (before the K swizzle fix): +4.4 % over the register-staged kernel at 1024^2 B4; an explicit sched_group_barrier
 // interleave of each step (1 MFMA : 1 LDS read : 1-2 exp : 2 VALU) measured 5.8 % SLOWER, and the
 // static priority of the younger wave half makes no difference here (both kept out / as is).
 // --------------------------------------------------------------------------------------
@@ -775,7 +779,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p
 #pragma unroll
   for (int i = 0; i < KPW; ++i) {
     const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+    ksrc[i] = row * 128 + 8 * (slot ^ ((row >> 1) & 7));
   }
 #pragma unroll
   for (int i = 0; i < VPW; ++i) {
@@ -800,7 +804,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p
       const bf16* krow = ck + ((2 * hf + j) * 32 + r32) * 64;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ (r32 & 7)));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ ((r32 >> 1) & 7)));
         S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[j], 0, 0, 0);
       }
     }

@@ -43,6 +43,14 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   p.r = a->r; p.ldr = a->ldr; p.sr1 = a->sr1; p.sr2 = a->sr2;
   p.c = a->c; p.ldc = a->ldc; p.sc1 = a->sc1; p.sc2 = a->sc2;
   p.relu = a->relu;
+  p.c2 = a->c2; p.ldc2 = a->ldc2; p.sc21 = a->sc21; p.sc22 = a->sc22;
+  p.vt = a->vt; p.ldt = a->ldt; p.svt1 = a->svt1; p.svt2 = a->svt2;
+  if (a->c2 && (a->c_dtype != MHADA_F32 || ((uintptr_t)a->c2 & 7) || a->ldc2 % 4 || a->sc21 % 4 || a->sc22 % 4))
+    return fail("mhada_gemm: c2 (bf16 copy) needs fp32 C, 8-byte alignment and strides that are multiples of 4");
+  if (a->vt && (a->N != 128 || a->a_mode != MHADA_A_ROWS || a->relu || a->r || a->c2 || !aligned16(a->vt) ||
+                a->ldt % 64 || a->ldt < a->M || a->svt1 % 8 || a->svt2 % 8))
+    return fail("mhada_gemm: vt needs the K|V' projection shape (ROWS, N == 128, no ReLU/residual), a 16-byte "
+                "aligned image and ldt a multiple of 64 covering M");
   switch (a->a_mode) {
     case MHADA_A_ROWS:
       if (a->lda % ea) return fail("mhada_gemm: lda must be a multiple of 16 bytes");
@@ -85,7 +93,7 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   const int nz = a->nb1 * a->nb2;
   if (nz > 65535) return fail("mhada_gemm: too many batch entries");
   // the decoder's 64 -> 64 layer (with its fused upsample): direct tile kernel (conv_tile.hip)
-  if (tuning().conv_c64 && a->compute == MHADA_BF16 && a->a_dtype == MHADA_BF16 && a->c_dtype == MHADA_BF16 &&
+  if (!a->c2 && !a->vt && tuning().conv_c64 && a->compute == MHADA_BF16 && a->a_dtype == MHADA_BF16 && a->c_dtype == MHADA_BF16 &&
       (a->a_mode == MHADA_A_CONV3X3 || a->a_mode == MHADA_A_CONV3X3_UP2) && a->img_c == 64 && a->N == 64 &&
       a->ldc == 64 && a->ldw == 576 && a->bias && !a->r)
     return conv3x3_c64(a->a, a->w, a->bias, a->c, a->M / (p.out_h * p.out_w), p.out_h, p.out_w,

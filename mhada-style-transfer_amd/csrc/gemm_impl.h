@@ -37,6 +37,8 @@ struct GemmP {
   int relu, tiles_n, ntiles;
   int lds_epi;  // ping-pong kernels: stage the output through LDS (tuning gemm_ldsepi = 0: direct stores)
   int rinit;    // persistent ping-pong, fp32 C, no ReLU: residual + bias loaded into the accumulators
+  void* c2; long long ldc2, sc21, sc22;  // optional bf16 copy of an fp32 C
+  void* vt; long long ldt, svt1, svt2;   // optional transposed V' image (K|V' projection, N = 128)
 };
 
 template <typename TC> struct Cfg {
@@ -268,6 +270,9 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
               for (int e = 0; e < 4; ++e) v[e] += rr[e];
             }
             *reinterpret_cast<f32x4*>(crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+            if (p.c2)
+              *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 +
+                                         (long long)m * p.ldc2 + n) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
           } else {
             if (rrow) {
               const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rrow + n);
@@ -359,6 +364,9 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
               __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4*>(crow + n));
             else
               *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+            if (p.c2)
+              *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 +
+                                         (long long)m * p.ldc2 + n) = bf16x4{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
           } else {
             if (rrow) {
               const bf16x4 q = *reinterpret_cast<const bf16x4*>(rrow + n);
@@ -372,6 +380,87 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
           for (int e = 0; e < 4; ++e) {
             if (n + e < p.N) crow[n + e] = from_f32<TO>(x[e] + (rrow ? to_f32<TO>(rrow[n + e]) : 0.f));
           }
+        }
+      }
+    }
+  }
+}
+
+// The K|V' projection's V' half written as the attention's transposed operand image (replaces
+// mhada_transpose_v): for a wave sub-tile of 32*TM keys x 64 channels o (TN = 2),
+//   vt[o][pos(m)] = V'[m][o],  vt[64 + o][pos(m)] = V'[m][o]^2,
+// bf16: pos permutes keys inside groups of 16 (bits 2 and 3 swapped, the order the 32x32x16 PV
+// operand reads) and V'^2 is the square of the bf16-rounded V' (as mhada_transpose_v); fp32:
+// natural order.  Each 32 x 32 block is transposed through the wave's 4-KiB scratch and stored
+// as 16-B chunks of key positions; positions >= M (up to ldt) are written 0.
+template <typename TO, int TM>
+MHADA_DEV void store_vt_tile(const GemmP& p, const f32x16 (&acc)[TM][2], int z1, int z2, int mrow0, int ncol0,
+                             int lane, float* scr) {
+  TO* vbase = reinterpret_cast<TO*>(p.vt) + z1 * p.svt1 + z2 * p.svt2;
+  const float* bbase = p.bias ? p.bias + z1 * p.sb1 + z2 * p.sb2 : nullptr;
+  const int h = lane >> 5, r32 = lane & 31;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m0 = mrow0 + 32 * mi;
+    if (m0 >= p.ldt) break;  // ldt % 64 == 0: a 32-key block is wholly inside or outside
+    const bool mv = m0 + r32 < p.M;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      if constexpr (sizeof(TO) == 2) {
+        bf16* sb = reinterpret_cast<bf16*>(scr);
+        const int pos = (r32 & ~12) | ((r32 & 4) << 1) | ((r32 & 8) >> 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ol = 8 * g + 4 * h + e;
+            float x = acc[mi][ni][4 * g + e] + (bbase ? bbase[ncol0 + 32 * ni + ol] : 0.f);
+            sb[ol * 32 + pos] = mv ? (bf16)x : (bf16)0.0f;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bf16x8 v[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = lane + 64 * j;
+          v[j] = *reinterpret_cast<const bf16x8*>(sb + (c >> 2) * 32 + 8 * (c & 3));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = lane + 64 * j, ol = c >> 2, part = c & 3;
+          TO* dst = vbase + (long long)(32 * ni + ol) * p.ldt + m0 + 8 * part;
+          *reinterpret_cast<bf16x8*>(dst) = v[j];
+          bf16x8 sq;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)v[j][e];
+            sq[e] = (bf16)(f * f);
+          }
+          *reinterpret_cast<bf16x8*>(dst + 64 * p.ldt) = sq;
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ol = 8 * g + 4 * h + e;
+            const float x = acc[mi][ni][4 * g + e] + (bbase ? bbase[ncol0 + 32 * ni + ol] : 0.f);
+            scr[ol * 32 + r32] = mv ? x : 0.f;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = lane + 64 * j;
+          v[j] = *reinterpret_cast<const f32x4*>(scr + (c >> 3) * 32 + 4 * (c & 7));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = lane + 64 * j, ol = c >> 3, part = c & 7;
+          float* dst = reinterpret_cast<float*>(vbase) + (long long)(32 * ni + ol) * p.ldt + m0 + 4 * part;
+          *reinterpret_cast<f32x4*>(dst) = v[j];
+          *reinterpret_cast<f32x4*>(dst + 64 * p.ldt) = v[j] * v[j];
         }
       }
     }
@@ -601,6 +690,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
 
   // epilogue: through a per-wave 4-KiB LDS scratch carved from the (now idle) staging buffers —
   // whole-row stores (16 B per lane) instead of 32 rows x 8-16 B per store instruction
+  if (p.vt && n0 + wn * (BN / WN) >= 64) {  // the V' half of the K|V' projection -> vt image
+    if constexpr (TN == 2) {
+      store_vt_tile<TO, TM>(p, acc, z1, z2, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane,
+                            reinterpret_cast<float*>(smem) + wave * 1024);
+    }
+    return;
+  }
   if (p.lds_epi) {
     float* scr = reinterpret_cast<float*>(smem) + wave * 1024;
     if constexpr (sizeof(TO) == 2 && TN == 2) {
@@ -1141,6 +1237,14 @@ static bool pp_offsets_fit(const GemmP& p, int amode) {
 // under the ~34 TB/s L2 ceiling at MFMA rate.
 template <typename TC, typename TA, typename TO, int AMODE>
 static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
+  // the vt epilogue needs waves owning 64 columns of a 128-column tile (checked on the host:
+  // N == 128, ROWS mode)
+  if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred) {
+    if (p.vt) {
+      if constexpr (sizeof(TC) == 2) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
+      else return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
+    }
+  }
   // N <= 64: 128x64 tiles of 4 waves x (32x64), two workgroups per CU (55 KiB of LDS each), whose
   // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (tuning gemm_n64 = 256
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower

@@ -35,6 +35,8 @@ class GemmArgs(ctypes.Structure):
         ("r", _vp), ("r_dtype", ctypes.c_int), ("ldr", _c_ll), ("sr1", _c_ll), ("sr2", _c_ll),
         ("c", _vp), ("c_dtype", ctypes.c_int), ("ldc", _c_ll), ("sc1", _c_ll), ("sc2", _c_ll),
         ("relu", ctypes.c_int), ("pad", ctypes.c_int),
+        ("c2", _vp), ("ldc2", _c_ll), ("sc21", _c_ll), ("sc22", _c_ll),
+        ("vt", _vp), ("ldt", _c_ll), ("svt1", _c_ll), ("svt2", _c_ll),
     ]
 
 
@@ -122,7 +124,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def get_tuning(name: str) -> int:

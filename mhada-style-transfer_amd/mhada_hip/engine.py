@@ -212,6 +212,7 @@ class _Feat:
     def __init__(self, t: torch.Tensor, h: int, w: int):
         self.t, self.h, self.w = t, h, w  # t: [B][N][C]
         self._stats = None
+        self.t16 = None  # optional bf16 copy of t (written by the producing GEMM)
 
     @classmethod
     def from_nchw(cls, x: torch.Tensor):
@@ -226,12 +227,14 @@ class _Feat:
 
 
 def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dtype,
-                  side: Optional[dict] = None) -> _Feat:
+                  side: Optional[dict] = None, want_bf16: bool = False) -> _Feat:
     """AdaAttnMultiHead.forward (adaDecoder.py:162-206).
 
     ``side`` carries the block's style-only tensors (IN statistics of fs, the K|V' projection and
     its V'^T image): when it is filled they are reused (fs may then be None), when it is an empty
-    dict they are computed and stored into it (the per-style cache of adaformer_forward)."""
+    dict they are computed and stored into it (the per-style cache of adaformer_forward).
+    ``want_bf16``: the out_conv GEMM also writes a bf16 copy of the block output (``.t16``) for
+    the decoder's first conv (the last block of a bf16 forward)."""
     if blk.head_dim != HEAD_DIM:
         raise ValueError(f"the HIP MHAda kernels implement head_dim={HEAD_DIM} (qkv_dim/num_heads), "
                          f"got {blk.head_dim}")
@@ -262,22 +265,31 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
              bias=prep["bf"], sb=(0, HEAD_DIM), ldc=HEAD_DIM, sc=(H * Nc * HEAD_DIM, Nc * HEAD_DIM))
     if not cached:
         Ns = fs.t.shape[1]
+        # K|V' projection: K rows into kv[..., :64] (the attention's K operand), V' straight into
+        # the transposed V'^T | V'^2^T image vt (the GEMM's vt epilogue; kv[..., 64:] unused)
         kv = torch.empty(B, H, Ns, 2 * HEAD_DIM, device=dev, dtype=dt)
+        ldt = (Ns + 63) // 64 * 64
+        vt = torch.empty(B, H, 2 * HEAD_DIM, ldt, device=dev, dtype=dt)
         ops.gemm(a=fs.t, w=wkv, c=kv, M=Ns, N=2 * HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Ns * C, HEAD_DIM),
                  nb=(B, H), a_mu=mu_s, smu=(C, HEAD_DIM), ldw=HEAD_DIM,
                  sw=(H * 2 * HEAD_DIM * HEAD_DIM, 2 * HEAD_DIM * HEAD_DIM), bias=bkv, sb=(0, 2 * HEAD_DIM),
-                 ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM))
+                 ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM),
+                 vt=vt, ldt=ldt, svt=(H * 2 * HEAD_DIM * ldt, 2 * HEAD_DIM * ldt))
         if act == ACT_COSINE:
             ops.cosine_prep(None, kv)
-        vt = ops.transpose_v(kv)
         if side is not None:
             side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt)
     if act == ACT_COSINE:
         ops.cosine_prep(q, None)
     with _timed("mhada_attn"):
         att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
-    out = ops.linear(att.view(B * Nc, C), prep["w_out"], prep["b_out"], torch.float32)
-    return _Feat(out.view(B, Nc, C), fc.h, fc.w)
+    out = torch.empty(B * Nc, C, device=dev, dtype=torch.float32)
+    t16 = torch.empty(B * Nc, C, device=dev, dtype=torch.bfloat16) if want_bf16 else None
+    ops.gemm(a=att.view(B * Nc, C), w=prep["w_out"], c=out, M=B * Nc, N=C, K=C, compute=dt, lda=C, ldw=C,
+             bias=prep["b_out"], ldc=C, c2=t16, ldc2=C)
+    f = _Feat(out.view(B, Nc, C), fc.h, fc.w)
+    f.t16 = None if t16 is None else t16.view(B, Nc, C)
+    return f
 
 
 def style_cache(ada, fs: Sequence[torch.Tensor], dt: torch.dtype):
@@ -322,10 +334,13 @@ def decoder_prep(dec, dtype):
     return cached_prep(dec, dtype, build)
 
 
-def decoder_forward_tokens(dec, x_nhwc: torch.Tensor, dt: torch.dtype, clamp255: bool = False) -> torch.Tensor:
-    """Decoder.forward (conv.py:96-100) on NHWC input; returns NCHW fp32 (B,3,8h,8w)."""
+def decoder_forward_tokens(dec, x_nhwc: torch.Tensor, dt: torch.dtype, clamp255: bool = False,
+                           x16: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decoder.forward (conv.py:96-100) on NHWC input; returns NCHW fp32 (B,3,8h,8w).  ``x16``: a
+    bf16 copy of the input (bf16 compute: the first conv then runs on the bf16 ping-pong GEMM
+    instead of converting fp32 rows on load)."""
     prep = decoder_prep(dec, dt)
-    x = x_nhwc
+    x = x16 if (x16 is not None and dt == torch.bfloat16) else x_nhwc
     for w, b, up, u in prep["layers"]:
         if up and not _fuse_upsample(dt, w):
             x = ops.upsample2x(x)
@@ -345,7 +360,9 @@ def adaformer_forward(ada, fc: Sequence[torch.Tensor], fs: Sequence[torch.Tensor
     fcs = fcf[0]
     for i in range(L):
         fcs = block_forward(ada.adaAttnHead[2 * i], fcf[i], fsf[i], fcs, dt, sides[2 * i])
-        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fsf[i], fcs, dt, sides[2 * i + 1])
+        fcs = block_forward(ada.adaAttnHead[2 * i + 1], fcs, fsf[i], fcs, dt, sides[2 * i + 1],
+                            want_bf16=(dt == torch.bfloat16 and i == L - 1))
     B, N, C = fcs.t.shape
-    cs = decoder_forward_tokens(ada.decoder, fcs.t.view(B, fcs.h, fcs.w, C), dt)
+    x16 = None if fcs.t16 is None else fcs.t16.view(B, fcs.h, fcs.w, C)
+    cs = decoder_forward_tokens(ada.decoder, fcs.t.view(B, fcs.h, fcs.w, C), dt, x16=x16)
     return tokens_to_nchw(fcs.t, fcs.h, fcs.w), cs

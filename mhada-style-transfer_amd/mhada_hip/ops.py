@@ -60,9 +60,16 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
          a_mu: Optional[torch.Tensor] = None, smu=(0, 0), img=(0, 0, 0),
          ldw: int = 0, sw=(0, 0), bias: Optional[torch.Tensor] = None, sb=(0, 0),
          r: Optional[torch.Tensor] = None, ldr: int = 0, sr=(0, 0),
-         ldc: int = 0, sc=(0, 0), relu: bool = False, pad: int = 0) -> torch.Tensor:
-    """``mhada_gemm``: C[z] = act(A[z] W[z]^T + bias[z]) + R[z]; strides in elements."""
-    _need_gpu(a, w, c, a_mu, bias, r)
+         ldc: int = 0, sc=(0, 0), relu: bool = False, pad: int = 0,
+         c2: Optional[torch.Tensor] = None, ldc2: int = 0, sc2=(0, 0),
+         vt: Optional[torch.Tensor] = None, ldt: int = 0, svt=(0, 0)) -> torch.Tensor:
+    """``mhada_gemm``: C[z] = act(A[z] W[z]^T + bias[z]) + R[z]; strides in elements.  Optional
+    c2 (a bf16 copy of an fp32 C) and vt (the transposed V' image of the K|V' projection)."""
+    _need_gpu(a, w, c, a_mu, bias, r, c2, vt)
+    if c2 is not None and (c2.dtype != torch.bfloat16 or c.dtype != torch.float32):
+        raise ValueError("c2 is the bf16 copy of an fp32 C")
+    if vt is not None and vt.dtype != c.dtype:
+        raise ValueError("vt has the dtype of C")
     if w.dtype != compute:
         raise ValueError("W must already be in the compute dtype")
     for t in (a_mu, bias):
@@ -92,6 +99,10 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     args.sc1, args.sc2 = sc
     args.relu = int(relu)
     args.pad = int(pad)
+    args.c2, args.ldc2 = _ptr(c2), ldc2
+    args.sc21, args.sc22 = sc2
+    args.vt, args.ldt = _ptr(vt), ldt
+    args.svt1, args.svt2 = svt
     _call("mhada_gemm", c, ctypes.byref(args))
     return c
 

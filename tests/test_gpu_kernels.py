@@ -76,6 +76,47 @@ def test_grouped_centred_projection(cdt):
 
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Ns", [4096, 200, 1000, 64, 37])
+def test_kv_projection_vt_epilogue_matches_transpose_v(cdt, Ns):
+    """The K|V' projection's vt epilogue (V'^T | V'^2^T written by the GEMM, keys permuted for
+    bf16, zero padding to ldt) is bit-identical to the separate mhada_transpose_v of the same
+    GEMM's kv output; the K half of kv is unchanged."""
+    B, H, C = 2, 8, 512
+    x = rnd(B, Ns, C, seed=7) * 3 + 1.5
+    mu = x.mean(dim=1)
+    w = rnd(B, H, 128, 64, scale=0.125, seed=8, dtype=cdt)
+    bias = rnd(H, 128, seed=9)
+    args = dict(a=x, w=w, M=Ns, N=128, K=64, compute=cdt, lda=C, sa=(Ns * C, 64), nb=(B, H), a_mu=mu,
+                smu=(C, 64), ldw=64, sw=(H * 128 * 64, 128 * 64), bias=bias, sb=(0, 128), ldc=128,
+                sc=(H * Ns * 128, Ns * 128))
+    kv = torch.empty(B, H, Ns, 128, device=DEV, dtype=cdt)
+    ops.gemm(c=kv, **args)
+    ref = ops.transpose_v(kv)
+    ldt = ref.shape[-1]
+    kv2 = torch.empty_like(kv)
+    vt = torch.full((B, H, 128, ldt), float("nan"), device=DEV, dtype=cdt)
+    ops.gemm(c=kv2, vt=vt, ldt=ldt, svt=(H * 128 * ldt, 128 * ldt), **args)
+    assert torch.equal(vt, ref)
+    assert torch.equal(kv2[..., :64], kv[..., :64])
+
+
+def test_gemm_bf16_copy_output():
+    """The optional bf16 copy (c2) of an fp32-output GEMM equals the fp32 result rounded once."""
+    x = rnd(4096, 512, seed=1, dtype=torch.bfloat16)
+    w = rnd(512, 512, scale=512 ** -0.5, seed=2, dtype=torch.bfloat16)
+    b = rnd(512, seed=3)
+    for M in (4096, 1000):
+        c = torch.empty(M, 512, device=DEV)
+        c2 = torch.empty(M, 512, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(a=x, w=w, c=c, M=M, N=512, K=512, compute=torch.bfloat16, lda=512, ldw=512, bias=b, ldc=512,
+                 c2=c2, ldc2=512)
+        assert torch.equal(c2, c.bfloat16())
+        c3 = torch.empty(M, 512, device=DEV)
+        ops.gemm(a=x, w=w, c=c3, M=M, N=512, K=512, compute=torch.bfloat16, lda=512, ldw=512, bias=b, ldc=512)
+        assert torch.equal(c, c3)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H,W", [(64, 64), (72, 128), (16, 24)])
 def test_patch_embed(cdt, H, W):
     B = 2
@@ -345,9 +386,9 @@ def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
     return out * f + mm + v_mu.double()[:, None]
 
 
-# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsh" (half-tile pipelined,
-# LDS-DMA; the default when Ns % 128 == 0), "fsg" (LDS-DMA), "fsE" (register staging, early
-# loads), "fs" (register staging; the default for ragged Ns) — and the online-max kernel "w8".
+# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsg" (LDS-DMA; the default
+# when Ns % 128 == 0), "fsh" (half-tile pipelined, LDS-DMA), "fsE" (register staging, early loads),
+# "fs" (register staging; the default for ragged Ns) — and the online-max kernel "w8".
 # Variants that need whole 128-key tiles fall back to "fs" on ragged Ns.
 ATTN_VARIANTS = {"fsh": dict(attn_fixed_shift=1, attn_sched=5), "fsg": dict(attn_fixed_shift=1, attn_sched=3),
                  "fsE": dict(attn_fixed_shift=1, attn_sched=4), "fs": dict(attn_fixed_shift=1, attn_sched=0),
