@@ -331,9 +331,11 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
   const int key = (t % p.nb) * 32 * NW + wave * 32 + r32;
   const bool kv = key < p.Ns;
-  float kr[32], vr[32];
+  float kr[32], vr[32], vr2[32];
   load_half_row(kr, p.k + bh * p.Ns * 64, key, kv, h, kLog2e);
   load_half_row(vr, p.v + bh * p.Ns * 64, key, kv, h, 1.0f);
+#pragma unroll
+  for (int s = 0; s < 32; ++s) vr2[s] = vr[s] * vr[s];  // V'^2 once (the wave's keys are fixed)
   const float* qb = p.q + bh * p.Nc * 64;
   const float* ob = p.dmo + bh * p.Nc * 128;
   const float* lb = p.lse + bh * p.Nc;
@@ -397,7 +399,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
         const int s = 4 * i + e;
         S = mfma(qq[e], kr[s], S);
         dA = mfma(o1[e], vr[s], dA);
-        dA = mfma(o2[e], vr[s] * vr[s], dA);
+        dA = mfma(o2[e], vr2[s], dA);
       }
     }
     f32x16 P, dS;

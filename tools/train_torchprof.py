@@ -28,7 +28,8 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stac
     torch.cuda.synchronize()
 out = open(sys.argv[1], "w") if len(sys.argv) > 1 else sys.stdout
 print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60), file=out)
-for op in ("aten::copy_", "aten::add_", "aten::add"):
+for op in ("aten::copy_", "aten::add_", "aten::add", "aten::sum", "aten::mean", "aten::mul", "aten::sub",
+           "aten::mse_loss", "aten::mse_loss_backward", "aten::std", "aten::div", "aten::cat"):
     rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key == op]
     rows.sort(key=lambda e: -e.self_device_time_total)
     print(f"\n==== {op}: top input shapes by device time", file=out)
