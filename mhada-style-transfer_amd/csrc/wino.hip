@@ -14,22 +14,23 @@
 // transforms only add / subtract (G's 1/2 is exact): the direct correlation up to fp32 rounding
 // of 4-term sums.
 //
-// Workgroup = 4 waves (one per SIMD, 512 registers each) = 64 Winograd tiles (8 x 8 tiles =
-// 16 x 16 output pixels) x 64 output channels; wave w owns tiles 32(w&1).. x channels 32(w>>1)..
-// for ALL 16 positions (16 accumulator blocks = 256 AGPRs), so the output transform runs in
-// registers.  The input channels stream in chunks of 4; per chunk:
-//   * the raw 18 x 18-pixel input patch (16 B per pixel, padding resolved at the load) and the
-//     transformed-filter slice U [16][64 co][4 ci] (16 KiB, contiguous, prepacked by
-//     mhada_wino_weights) arrive in registers one chunk ahead and are written to LDS;
-//   * beside the wave's 32 MFMAs of chunk k (2 k-steps x 16 positions) it transforms the raw
-//     patch of chunk k+1 (16 LDS reads, the B^T d B adds, 16 LDS writes per thread) into the
-//     other V buffer; one barrier per chunk.
-// The first version (32 tiles x 64 channels per workgroup, 8-channel chunks, 16 scalar gathers
-// per thread, all-position exchange through LDS in the epilogue) was L2-bandwidth bound: its
-// loads alone took as long as its MFMAs (ablation builds).  Here the filter slice is
-// reused by twice the tiles and the input arrives as whole 16-B pixels.
-// LDS operand rows are 16 B (4 channels) with the two 8-B halves swapped for rows 16..31 of every
-// 32, so the ds_read_b64 of 32 consecutive rows is conflict-free.
+// Workgroup = 8 waves (two per SIMD) = 64 Winograd tiles (8 x 8 tiles = 16 x 16 output pixels)
+// x 64 output channels.  Wave w = (e, th, ch) = (w >> 2, w & 1, (w >> 1) & 1) accumulates the
+// 8 positions xi = 8e .. 8e+7 for tiles 32 th.. x channels 32 ch.. (8 accumulator blocks = 128
+// registers); positions 8..15 reach waves 0-3 through LDS for the output transform.  The input
+// channels stream in chunks of 8; per chunk k:
+//   * LDS-DMA (global_load_lds) brings U(k+1) [16][64 co][8 ci] (32 KiB, prepacked
+//     [Cin/8][16][Cout][8] by mhada_wino_weights) and the raw 18 x 18-pixel patch of chunk k+2
+//     (32 B per pixel; padding pixels load a clamped pixel and are zeroed in the transform);
+//   * the wave's 32 MFMAs of chunk k (8 positions x 4 k-steps) run beside every thread's
+//     transform V = B^T d B of one (tile, channel) of chunk k+1 into the other V buffer;
+//   * one counted vmcnt(0) + workgroup barrier.
+// Earlier forms, measured and replaced: 4 waves x 32 tiles with scalar gathers
+// (L2 bound), and 4 waves x 64 tiles holding all 16 positions in 256 AGPRs (one wave per SIMD:
+// the transform and loads serialised with the MFMAs).
+// LDS operand rows are 32 B (8 channels) with the two 16-B halves swapped on rows with bit 3
+// set (swz), so the ds_read_b128 of 32 consecutive rows is conflict-free; the raw patch's 16-B
+// slots are XOR-swizzled (rswz) so the transform's ds_read_b32 hit distinct banks.
 #include "common.h"
 
 #ifndef WINO_DBG

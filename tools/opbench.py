@@ -88,6 +88,22 @@ def gemm_k_suite():
         fl = 2 * M * N * K
         print(f"gemmK bf16 M={M} N={N} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF"
                                                              for k, v in t.items()))
+    # the fp32-out residual form (ViT out_proj / MLP2, MHAda out_conv): HBM rate vs K, with and
+    # without the residual, so the fixed per-tile R-load / C-store cost separates from the K loop
+    N = 512
+    for K in (512, 1024, 2048):
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device=dev)
+        r = torch.randn(M, N, device=dev)
+        t = bench({"res": lambda: ops.linear(x, w, b, torch.float32, residual=r),
+                   "nores": lambda: ops.linear(x, w, b, torch.float32),
+                   "bf16out": lambda: ops.linear(x, w, b, torch.bfloat16),
+                   "no_rinit": lambda: with_env("MHADA_GEMM_RINIT", "0", ops.linear, x, w, b, torch.float32, residual=r)})
+        by = {"res": M * K * 2 + 2 * M * N * 4, "nores": M * K * 2 + M * N * 4, "bf16out": M * K * 2 + M * N * 2,
+              "no_rinit": M * K * 2 + 2 * M * N * 4}
+        print(f"gemmR bf16 M={M} N={N} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {by[k] / v / 1e6:7.1f} GB/s"
+                                                             for k, v in t.items()))
 
 
 def out3_suite():
