@@ -42,7 +42,6 @@ struct Tuning {
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
-  int gemm_n64pp = 1;        // N <= 64 bf16: 512x64 persistent ping-pong tile
   int attn_sched = 3;        // bf16 fixed-shift attention (Ns % 128 == 0): 3 LDS-DMA staging, 5 half-tile
                              // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int xknob = 0;             // scratch knob for A/B experiments (no effect unless a kernel reads it)

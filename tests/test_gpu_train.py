@@ -40,6 +40,25 @@ def test_train_step_256_b2_losses_match_oracle_and_grads_match_cpu():
         np.testing.assert_allclose(grad_summary(m_gpu), g_ref, rtol=2e-3, atol=1e-5 * g_ref.max())
 
 
+def test_batched_adaformer_step_matches_per_call_step():
+    """Trainer.batch_adaformer (the three AdaFormer calls of train_image.py:105-110 as one call
+    over the concatenated batch) against the reference's three separate calls: the same losses
+    and gradients up to fp32 summation order (the weight gradients reduce over 3B images in one
+    GEMM instead of three partial GEMMs added by autograd)."""
+    from test_train_cpu import grad_summary
+    c = seeded_image(2, 128, 128, 51).cuda()
+    s = seeded_image(2, 128, 128, 52).cuda()
+    outs, grads = [], []
+    for batched in (True, False):
+        tr = Trainer(*build("cuda"))
+        tr.batch_adaformer = batched
+        out = tr.backward(c, s)
+        outs.append(np.array([float(out[k].detach()) for k in ("loss_gs", "loss_lf", "loss_id1", "loss_id2")]))
+        grads.append(np.concatenate([grad_summary(m) for m in (tr.vit_c, tr.vit_s, tr.ada)]))
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-5)
+    np.testing.assert_allclose(grads[0], grads[1], rtol=1e-4, atol=1e-6 * grads[1].max())
+
+
 def test_train_step_full_size_runs():
     tr = Trainer(*build("cuda"))
     c = seeded_image(8, 512, 512, 100).cuda()
