@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 7 (gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 8 (mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -279,6 +279,13 @@ int mhada_attn_train_bwd_prep(const float* dout, const float* x, const float* mo
 
 int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int oh, int ow,
                         mhada_stream_t stream);
+/* Gradient of the loss terms on one VGG feature map x, NHWC rows [B][P][C] (P = H*W), in one pass
+ * (replaces the ATen backward of lossfn.py:7-23 mean/std distances and lossfn.py:26-34,41-47 MSEs):
+ *   g = alpha[b][c] + beta[b][c] * (x - mu[b][c]) + ks * kp[0] * (x - t)
+ * alpha / beta / mu [B][C] (all null: no statistics term), t [B][P][C] (null: no MSE term), kp a
+ * device scalar (null: 1); C % 4 == 0, 16-byte aligned pointers. */
+int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha, const float* beta,
+                        const float* kp, float ks, float* g, int B, long long P, int C, mhada_stream_t stream);
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */
 int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t stream);
 /* Adjoint of ReflectionPad2d(1) (conv.py:27,31): dxp [B][H+2][W+2][C] (the full-correlation

@@ -24,6 +24,11 @@
 //                     per-row dot delta, one pass instead of ~12 aten ops.
 //   mhada_pos_embed_bwd  adjoint of the PosEmbedding bilinear resize (vit.py:91-92): a gather
 //                     per source pixel (fixed order) in place of ATen's atomic scatter.
+//   mhada_feat_loss_bwd  the gradient of every loss term on one VGG feature map in one pass:
+//                     the global-style mean / unbiased-std distances (lossfn.py:7-23) and an MSE
+//                     against a target (local feature loss lossfn.py:26-34, identity loss 2
+//                     lossfn.py:41-47), replacing ATen's mse_backward, std / mean backward chains
+//                     and the adds that sum them.
 //   mhada_vgg_input / mhada_vgg_input_bwd  imageNet1k_normalize (vgg19.py:6-12) fused with the
 //                     NCHW -> NHWC layout change (channels zero padded to a multiple of 32 so the
 //                     first conv runs on the implicit-GEMM kernel), and its adjoint.
@@ -616,6 +621,37 @@ __global__ void __launch_bounds__(256) relu_bwd_kernel(const float* __restrict__
   reinterpret_cast<f32x4*>(dx)[i] = o;
 }
 
+// g = alpha[b][c] + beta[b][c] * (x - mu[b][c]) + ks * kp[0] * (x - t) on NHWC rows x [B][P][C]
+// (either term optional: alpha == null / t == null; kp == null reads as 1); 4 channels per thread.
+// kp is a device scalar (the upstream gradient of the MSE term), so no host sync is needed.
+__global__ void __launch_bounds__(256) feat_loss_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                                            const float* __restrict__ mu,
+                                                            const float* __restrict__ alpha,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ kp, float ks,
+                                                            float* __restrict__ g, long long PC4, int C4,
+                                                            long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float k = kp ? ks * kp[0] : ks;
+  const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  if (alpha) {
+    const long long bc = (i / PC4) * C4 + i % C4;  // (b, 4-channel group)
+    const f32x4 a = reinterpret_cast<const f32x4*>(alpha)[bc];
+    const f32x4 be = reinterpret_cast<const f32x4*>(beta)[bc];
+    const f32x4 m = reinterpret_cast<const f32x4*>(mu)[bc];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = a[e] + be[e] * (v[e] - m[e]);
+  }
+  if (t) {
+    const f32x4 w = reinterpret_cast<const f32x4*>(t)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] += k * (v[e] - w[e]);
+  }
+  reinterpret_cast<f32x4*>(g)[i] = o;
+}
+
 // dX[b][y][x] = sum of dXp[b][py][px] over the padded positions whose reflection is (y, x):
 // py = y + 1, plus py = 0 when y == 1 and py = H + 1 when y == H - 2 (same in x).
 __global__ void __launch_bounds__(256) reflect_fold_kernel(const float* __restrict__ dxp, float* __restrict__ dx, int B,
@@ -1033,6 +1069,19 @@ extern "C" int mhada_relu_bwd(const float* dy, const float* y, float* dx, long l
     return fail("mhada_relu_bwd: bad args (n % 4 == 0, 16-byte aligned)");
   hipLaunchKernelGGL(relu_bwd_kernel, grid1(n / 4), dim3(256), 0, (hipStream_t)s_, dy, y, dx, n / 4);
   return check_launch("mhada_relu_bwd");
+}
+
+extern "C" int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha,
+                                   const float* beta, const float* kp, float ks, float* g, int B, long long P,
+                                   int C, mhada_stream_t s_) {
+  if (!x || !g || B <= 0 || P <= 0 || C <= 0 || C % 4 || !al16(x) || !al16(g) || (t && !al16(t)))
+    return fail("mhada_feat_loss_bwd: bad args (C % 4 == 0, 16-byte aligned)");
+  if (alpha && (!beta || !mu || !al16(alpha) || !al16(beta) || !al16(mu)))
+    return fail("mhada_feat_loss_bwd: alpha needs beta and mu (16-byte aligned)");
+  const long long n4 = (long long)B * P * (C / 4);
+  hipLaunchKernelGGL(feat_loss_bwd_kernel, grid1(n4), dim3(256), 0, (hipStream_t)s_, x, t, mu, alpha, beta, kp, ks,
+                     g, P * (C / 4), C / 4, n4);
+  return check_launch("mhada_feat_loss_bwd");
 }
 
 extern "C" int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t s_) {

@@ -579,6 +579,30 @@ def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return dx
 
 
+def feat_loss_bwd(x: torch.Tensor, mu: Optional[torch.Tensor], alpha: Optional[torch.Tensor],
+                  beta: Optional[torch.Tensor], t: Optional[torch.Tensor], ks: float,
+                  kp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``mhada_feat_loss_bwd`` on NHWC storage x [B][H][W][C] fp32 (t the same shape, or None;
+    mu / alpha / beta [B][C] fp32, or all None; kp a one-element fp32 device tensor or None):
+    alpha + beta (x - mu) + ks * kp (x - t)."""
+    _need_gpu(x)
+    B, H, W, C = x.shape
+    for u in (x, t, mu, alpha, beta, kp):
+        if u is not None and (u.dtype != torch.float32 or not u.is_contiguous()):
+            raise ValueError("feat_loss_bwd: contiguous fp32 operands")
+    if kp is not None and kp.numel() != 1:
+        raise ValueError("feat_loss_bwd: kp is one element")
+    if t is not None and t.shape != x.shape:
+        raise ValueError("feat_loss_bwd: target shape")
+    if alpha is not None and not (alpha.shape == beta.shape == mu.shape == (B, C)):
+        raise ValueError("feat_loss_bwd: statistics [B][C]")
+    g = torch.empty_like(x)
+    ptr = lambda u: None if u is None else u.data_ptr()  # noqa: E731
+    _call("mhada_feat_loss_bwd", x, x.data_ptr(), ptr(t), ptr(mu), ptr(alpha), ptr(beta), ptr(kp), float(ks),
+          g.data_ptr(), B, H * W, C)
+    return g
+
+
 def reflect_fold(dxp: torch.Tensor) -> torch.Tensor:
     _need_gpu(dxp)
     B, Hp, Wp, C = dxp.shape

@@ -37,6 +37,8 @@ class Trainer:
             p.requires_grad_(False)
         self.mse = nn.MSELoss(reduction="mean")
         self.batch_adaformer = True  # see losses()
+        # one backward pass per VGG feature map for the gs / lf / id2 terms (HIP; see _feature_losses)
+        self.fused_feature_losses = dev.type == "cuda"
         self.opt_vit_c = torch.optim.Adam(vit_c.parameters(), lr=lr)
         self.opt_vit_s = torch.optim.Adam(vit_s.parameters(), lr=lr)
         self.opt_ada = torch.optim.Adam(ada.parameters(), lr=lr)
@@ -90,11 +92,35 @@ class Trainer:
         vgg_fcs = self.vgg(cs)
         vgg_fcc = self.vgg(cc)
         vgg_fss = self.vgg(ss)
-        gs = L.global_style_loss(vgg_fcs, vgg_fs, self.mse) * LAMBDA_GS
-        lf = L.local_feature_loss(vgg_fc, vgg_fs, vgg_fcs, self.no_learn, self.mse) * LAMBDA_LF
+        if self.fused_feature_losses:
+            gs, lf, id2 = self._feature_losses(vgg_fc, vgg_fs, vgg_fcs, vgg_fcc, vgg_fss)
+            gs, lf, id2 = gs * LAMBDA_GS, lf * LAMBDA_LF, id2 * LAMBDA_ID2
+        else:
+            gs = L.global_style_loss(vgg_fcs, vgg_fs, self.mse) * LAMBDA_GS
+            lf = L.local_feature_loss(vgg_fc, vgg_fs, vgg_fcs, self.no_learn, self.mse) * LAMBDA_LF
+            id2 = L.identity_loss_2(vgg_fcc, vgg_fc, vgg_fss, vgg_fs, self.mse) * LAMBDA_ID2
         id1 = L.identity_loss_1(cc, content, ss, style, self.mse) * LAMBDA_ID1
-        id2 = L.identity_loss_2(vgg_fcc, vgg_fc, vgg_fss, vgg_fs, self.mse) * LAMBDA_ID2
         return {"loss_gs": gs, "loss_lf": lf, "loss_id1": id1, "loss_id2": id2, "loss": gs + lf + id1 + id2}
+
+    def _feature_losses(self, fc, fs, fcs, fcc, fss):
+        """global_style_loss, local_feature_loss and identity_loss_2 (lossfn.py:7-47) with each
+        VGG feature map's terms on train_fns.FeatureLossFn: the same loss values, summed in the
+        reference's order, and one backward pass per feature map."""
+        from .train_fns import feature_loss_terms
+        gs = lf = id2 = 0
+        for i in (1, 2, 3, 4, 5):
+            k = f"relu{i}_1"
+            t = None
+            if i >= 3:  # lossfn.py:26-34: the AdaAttN target of the content / style features
+                t = self.no_learn[i - 3](fc[k], fs[k], L.feature_down_sample(fc, i), L.feature_down_sample(fs, i))
+            lm, ls, lmse = feature_loss_terms(fcs[k], fs[k].mean(dim=(2, 3)), fs[k].std(dim=(2, 3)), t)
+            gs = gs + lm + ls
+            if t is not None:
+                lf = lf + lmse
+            a = feature_loss_terms(fcc[k], t=fc[k])[2]
+            b = feature_loss_terms(fss[k], t=fs[k])[2]
+            id2 = id2 + a + b
+        return gs, lf, id2
 
     def zero_grad(self) -> None:
         for o in (self.opt_vit_c, self.opt_vit_s, self.opt_ada):

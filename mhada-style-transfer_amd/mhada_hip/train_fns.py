@@ -387,6 +387,63 @@ class VggInputFn(torch.autograd.Function):
         return ops.vgg_input_bwd(g.contiguous())
 
 
+class FeatureLossFn(torch.autograd.Function):
+    """The loss terms of train_image.py on ONE VGG feature map x (an NCHW view of NHWC storage):
+      l_mean = mse(mean_hw(x), ref_mean), l_std = mse(std_hw(x), ref_std)  (lossfn.py:7-23; ref given)
+      l_mse  = mse(x, t)                            (lossfn.py:26-34 and 41-47; t given)
+    The forward evaluates them with the reference's own aten expressions (same values); the
+    backward writes dL/dx = g_mean 2(mu - mu_r) / (BC HW) + g_std 2(sd - sd_r)(x - mu) / (BC (HW-1) sd)
+    + g_mse 2(x - t) / numel in ONE mhada_feat_loss_bwd pass, in place of ATen's mse / std / mean
+    backward chains and the adds that sum the terms of a feature map."""
+
+    @staticmethod
+    def forward(ctx, x, ref_mean, ref_std, t):
+        if any(ctx.needs_input_grad[1:]):
+            raise ValueError("FeatureLossFn: the reference statistics and the target take no gradient")
+        ctx.set_materialize_grads(False)
+        zero = x.new_zeros(())
+        lm = ls = lmse = zero
+        mu = sd = None
+        if ref_mean is not None:
+            mu = x.mean(dim=(2, 3))
+            sd = x.std(dim=(2, 3))
+            lm = F.mse_loss(mu, ref_mean)
+            ls = F.mse_loss(sd, ref_std)
+        if t is not None:
+            lmse = F.mse_loss(x, t)
+        ctx.save_for_backward(x, t, mu, sd, ref_mean, ref_std)
+        return lm, ls, lmse
+
+    @staticmethod
+    def backward(ctx, g_mean, g_std, g_mse):
+        x, t, mu, sd, rm, rs = ctx.saved_tensors
+        B, C, H, W = x.shape
+        P = H * W
+        xs = x.permute(0, 2, 3, 1)
+        xs = xs if xs.is_contiguous() else xs.contiguous()
+        alpha = beta = None
+        if mu is not None and (g_mean is not None or g_std is not None):
+            zero = x.new_zeros(())
+            gm = g_mean if g_mean is not None else zero
+            gs = g_std if g_std is not None else zero
+            alpha = (gm * (2.0 / (B * C * P)) * (mu - rm)).contiguous()
+            beta = (gs * (2.0 / (B * C * (P - 1))) * (sd - rs) / sd).contiguous()
+        tt = None
+        if t is not None and g_mse is not None:
+            tt = t.permute(0, 2, 3, 1)
+            tt = tt if tt.is_contiguous() else tt.contiguous()
+        if alpha is None and tt is None:
+            return None, None, None, None
+        kp = g_mse.reshape(1).float().contiguous() if tt is not None else None
+        g = ops.feat_loss_bwd(xs, mu.contiguous() if alpha is not None else None, alpha, beta, tt, 2.0 / x.numel(), kp)
+        return g.permute(0, 3, 1, 2), None, None, None
+
+
+def feature_loss_terms(x, ref_mean=None, ref_std=None, t=None):
+    """(l_mean, l_std, l_mse) of one feature map (FeatureLossFn)."""
+    return FeatureLossFn.apply(x, ref_mean, ref_std, t)
+
+
 def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True):
     return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu)
 

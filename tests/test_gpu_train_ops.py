@@ -431,3 +431,34 @@ def test_bf16_block_without_autocast_takes_aten_path():
     out = blk16(fc.bfloat16(), fs.bfloat16(), fc.bfloat16())
     assert out.dtype == torch.bfloat16 and torch.isfinite(out.float()).all()
     assert rel(out.float(), ref) < 5e-2
+
+
+@pytest.mark.parametrize("stats,target", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("B,C,H,W", [(2, 64, 33, 20), (3, 512, 8, 8)])
+def test_feature_loss_fn_matches_aten_autograd(stats, target, B, C, H, W):
+    """FeatureLossFn (mhada_feat_loss_bwd) against fp64 autograd of the reference expressions it
+    replaces: mse(mean_hw), mse(std_hw) (lossfn.py:7-23) and mse(x, t) (lossfn.py:26-47), each
+    term scaled by its own upstream gradient; x an NCHW view of NHWC storage as the VGG emits it."""
+    x = rnd(B, H, W, C, seed=11).permute(0, 3, 1, 2).requires_grad_(True)
+    ref_f = rnd(B, C, H, W, seed=12) * 0.7 + 0.3
+    t = rnd(B, H, W, C, seed=13).permute(0, 3, 1, 2) if target else None
+    rm, rsd = (ref_f.mean(dim=(2, 3)), ref_f.std(dim=(2, 3))) if stats else (None, None)
+    w = (70.0, 3.5, 15.0)
+    lm, ls, lmse = train_fns.feature_loss_terms(x, rm, rsd, t)
+    (w[0] * lm + w[1] * ls + w[2] * lmse).backward()
+    xd = x.detach().double().requires_grad_(True)
+    tot = 0
+    refs = []
+    if stats:
+        a = F.mse_loss(xd.mean(dim=(2, 3)), rm.double())
+        b = F.mse_loss(xd.std(dim=(2, 3)), rsd.double())
+        tot = tot + w[0] * a + w[1] * b
+        refs += [(lm, a), (ls, b)]
+    if target:
+        c = F.mse_loss(xd, t.double())
+        tot = tot + w[2] * c
+        refs.append((lmse, c))
+    tot.backward()
+    for got, want in refs:
+        assert abs(got.item() - want.item()) <= 1e-5 * abs(want.item())
+    assert rel(x.grad, xd.grad) < 1e-5
