@@ -236,6 +236,7 @@ typedef struct mhada_gemm_tn_args {
   int b_mode;
   int img_c, img_h, img_w, pad;
   float* c; long long ldc;
+  float* colsum;  /* optional [M]: sum_k A[k][m] (the bias gradient), fused into the GEMM's A staging */
 } mhada_gemm_tn_args;
 int mhada_gemm_tn_splits(int M, int N, int K);
 int mhada_gemm_tn(const mhada_gemm_tn_args* args, float* work, long long work_floats, mhada_stream_t stream);

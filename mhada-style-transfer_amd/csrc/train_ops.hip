@@ -48,6 +48,7 @@ struct TnP {
   const float* b; long long ldb;          // ROWS: B[k * ldb + n]
   int img_c, img_h, img_w, out_h, out_w, pad;  // CONV: k = output pixel (b, oy, ox), n = tap*Cin + ci
   float* slab;                            // [splits][M][N]
+  float* cslab;                           // [splits][M] column sums of A (null: none)
   int kchunk, tiles_n;
 };
 
@@ -163,10 +164,19 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  // fused bias gradient (p.cslab): the column-0 tiles also sum their staged A rows; a thread's A
+  // chunks all cover columns m0 + 4 (tid % (BM/4)) .. +3 (256 is a multiple of BM/4)
+  const bool csum = p.cslab && tn == 0;
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+  auto add_cs = [&]() {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) cs += ra[i];
+  };
 
   const int nst = (kend - kbeg + kTnBK - 1) / kTnBK;
   if (nst > 0) {
     issue(kbeg);
+    if (csum) add_cs();
     commit(0);
   }
   __syncthreads();
@@ -188,10 +198,24 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[ni], av[mi], acc[mi][ni], 0, 0, 0);
     }
-    if (more) commit(buf ^ 1);
+    if (more) {
+      if (csum) add_cs();  // beside the commit: the loads were waited for there anyway
+      commit(buf ^ 1);
+    }
     __syncthreads();
   }
 
+  if (csum) {  // the 256 / (BM/4) threads of one column quad, summed in thread order through LDS
+    f32x4* part = reinterpret_cast<f32x4*>(&sA[0][0][0]);
+    part[tid] = cs;
+    __syncthreads();
+    if (tid < BM / 4) {
+      f32x4 v = part[tid];
+      for (int j = 1; j < 256 / (BM / 4); ++j) v += part[tid + j * (BM / 4)];
+      const int m = m0 + 4 * tid;
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.cslab + (long long)blockIdx.y * p.M + m) = v;  // M % 4 == 0
+    }
+  }
   float* slab = p.slab + (long long)blockIdx.y * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < TMW; ++mi) {
@@ -936,9 +960,12 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
     default:
       return fail("mhada_gemm_tn: bad b_mode");
   }
+  // fused bias gradient (colsum of A) on the MFMA kernel's vector A path; otherwise mhada_colsum's
+  // kernel after the GEMM (the 3-channel layer, unaligned A)
+  const bool fuse_cs = a->colsum && vec_a && p.M > 4;
   int S = tn_splits(p.M, p.N, p.K);
-  const long long per = (long long)p.M * p.N;
-  if (work_floats < per) return fail("mhada_gemm_tn: workspace smaller than M*N floats");
+  const long long per = (long long)p.M * p.N + (fuse_cs ? p.M : 0);
+  if (work_floats < per) return fail("mhada_gemm_tn: workspace smaller than M*N (+M) floats");
   S = (int)std::min<long long>(S, work_floats / per);
   p.kchunk = ((p.K + S - 1) / S + kTnBK - 1) / kTnBK * kTnBK;
   S = (p.K + p.kchunk - 1) / p.kchunk;
@@ -946,6 +973,7 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   const int bm = tn_bm(p.M);
   const int tiles = ((p.M + bm - 1) / bm) * p.tiles_n;
   p.slab = work;
+  p.cslab = fuse_cs ? work + (long long)S * p.M * p.N : nullptr;
   if (S > 65535) return fail("mhada_gemm_tn: too many splits");
   const dim3 grid((unsigned)tiles, (unsigned)S);
   const dim3 gsk((unsigned)S, (unsigned)((p.N / 4 + 255) / 256));
@@ -966,8 +994,18 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   else TN_LAUNCH(MHADA_A_CONV3X3_ZERO);
 #undef TN_LAUNCH
   if (int rc = check_launch("mhada_gemm_tn")) return rc;
-  hipLaunchKernelGGL(slab_reduce_kernel, grid1(per / 4), dim3(256), 0, s, work, a->c, (long long)p.M, p.N, a->ldc, S);
-  return check_launch("mhada_gemm_tn(reduce)");
+  const long long mn = (long long)p.M * p.N;
+  hipLaunchKernelGGL(slab_reduce_kernel, grid1(mn / 4), dim3(256), 0, s, work, a->c, (long long)p.M, p.N, a->ldc, S);
+  if (int rc = check_launch("mhada_gemm_tn(reduce)")) return rc;
+  if (!a->colsum) return 0;
+  if (fuse_cs) {
+    hipLaunchKernelGGL(slab_reduce_kernel, grid1(p.M / 4), dim3(256), 0, s, p.cslab, a->colsum, 1LL, p.M,
+                       (long long)p.M, S);
+    return check_launch("mhada_gemm_tn(colsum reduce)");
+  }
+  // unfused: the column sums of A [K][lda] over its first M columns (the workspace is free again)
+  if (a->lda != p.M || p.M % 4 || !al16(a->a)) return fail("mhada_gemm_tn: colsum needs a dense, aligned A");
+  return mhada_colsum(a->a, a->colsum, p.K, p.M, work, work_floats, s_);
 }
 
 extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, float* work, long long work_floats,

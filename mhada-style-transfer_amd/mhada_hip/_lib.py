@@ -46,7 +46,7 @@ class GemmTnArgs(ctypes.Structure):
         ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
         ("a", _vp), ("lda", _c_ll), ("b", _vp), ("ldb", _c_ll), ("b_mode", ctypes.c_int),
         ("img_c", ctypes.c_int), ("img_h", ctypes.c_int), ("img_w", ctypes.c_int), ("pad", ctypes.c_int),
-        ("c", _vp), ("ldc", _c_ll),
+        ("c", _vp), ("ldc", _c_ll), ("colsum", _vp),
     ]
 
 

@@ -9,10 +9,11 @@ the reference, and runs its forward and backward through libmhada_hip.so:
   forward: the implicit-GEMM conv (mhada_gemm, CONV3X3 / CONV3X3_ZERO, bias+ReLU epilogue);
   backward: ReLU mask (mhada_relu_bwd), input gradient = the conv of dY with the flipped,
   transposed weights (zero pad 1, or the full correlation + mhada_reflect_fold for the reflect
-  pad), weight gradient = mhada_gemm_tn over the im2col of the input, bias = mhada_colsum.
+  pad), weight gradient = mhada_gemm_tn over the im2col of the input, bias = the column sums of
+  dY from the same mhada_gemm_tn pass.
 * ``linear`` — nn.Linear / the 1x1 out_conv on token rows (vit.py:49-63 MHA projections and MLP,
   adaDecoder.py:152,205), optional fused ReLU: forward mhada_gemm; backward dX = dY W (mhada_gemm
-  with W^T), dW = dY^T X (mhada_gemm_tn), db = mhada_colsum.
+  with W^T), dW = dY^T X and db = colsum(dY) in one mhada_gemm_tn pass.
 * ``patch_embed`` — the 8x8 / stride-8 patch conv (vit.py:105-117): forward mhada_gemm PATCH8,
   weight gradient mhada_gemm_tn PATCH8 (the input image needs no gradient in training).
 * ``maxpool2``, ``upsample2x`` (conv.py:71), ``vgg_input`` (vgg19.py:6-12) and their adjoints.
@@ -142,10 +143,14 @@ class Conv3x3Fn(torch.autograd.Function):
                                                   pad=2, wino_u=ut))
         if ctx.needs_input_grad[1]:
             mode = A_CONV3X3 if ctx.pad_mode == "reflect" else A_CONV3X3_ZERO
-            # M = ldc (the zero-padded channel columns of g) keeps the vectorised A loads
-            dw = ops.gemm_tn(g, x, M=ldc, N=9 * cx, K=B * H * W, lda=ldc, b_mode=mode, img=(cx, H, W), pad=1)
+            # M = ldc (the zero-padded channel columns of g) keeps the vectorised A loads; the bias
+            # gradient (column sums of g) comes out of the same pass
+            dw, cs = ops.gemm_tn(g, x, M=ldc, N=9 * cx, K=B * H * W, lda=ldc, b_mode=mode, img=(cx, H, W), pad=1,
+                                 colsum=True)
             gw = dw.view(ldc, 3, 3, cx)[:co, :, :, :weight.shape[1]].permute(0, 3, 1, 2).contiguous()
-        if ctx.needs_input_grad[2]:
+            if ctx.needs_input_grad[2]:
+                gb = cs[:co].contiguous()
+        elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)[:co].contiguous()
         return gx, gw, gb, None, None
 
@@ -172,8 +177,10 @@ class LinearFn(torch.autograd.Function):
             gx = ops.linear(g, weight.detach().t().contiguous(), None, F32)
         if ctx.needs_input_grad[1]:
             M, N = g.shape
-            gw = ops.gemm_tn(g, x, M=N, N=x.shape[1], K=M, lda=N, ldb=x.shape[1], b_mode=A_ROWS)
-        if ctx.needs_input_grad[2]:
+            gw, cs = ops.gemm_tn(g, x, M=N, N=x.shape[1], K=M, lda=N, ldb=x.shape[1], b_mode=A_ROWS, colsum=True)
+            if ctx.needs_input_grad[2]:
+                gb = cs
+        elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)
         return gx, gw, gb, None
 
@@ -292,10 +299,13 @@ class HeadProjFn(torch.autograd.Function):
             ops.gemm(a=gy, w=weight.detach().transpose(1, 2).contiguous(), c=gx, M=T, N=64, K=64, compute=F32,
                      lda=64, sa=(T * 64, 0), nb=(H, 1), ldw=64, sw=(4096, 0), ldc=C, sc=(64, 0))
         if ctx.needs_input_grad[1]:
-            gw = torch.stack([ops.gemm_tn(gy[i], x[:, 64 * i:], M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS)
-                              for i in range(H)])
-        if ctx.needs_input_grad[2]:
-            gb = gy.sum(dim=1)  # one reduction over the tokens for all heads (8 colsum launches cost more)
+            res = [ops.gemm_tn(gy[i], x[:, 64 * i:], M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS, colsum=True)
+                   for i in range(H)]
+            gw = torch.stack([r[0] for r in res])
+            if ctx.needs_input_grad[2]:
+                gb = torch.stack([r[1] for r in res])  # the column sums came out of the TN passes
+        elif ctx.needs_input_grad[2]:
+            gb = gy.sum(dim=1)
         return gx, gw, gb
 
 
@@ -346,9 +356,12 @@ class PatchEmbedFn(torch.autograd.Function):
         g = gy.contiguous().view(-1, C)
         gw = gb = None
         if ctx.needs_input_grad[1]:
-            gw = ops.gemm_tn(g, img, M=C, N=64 * Ci, K=g.shape[0], lda=C, b_mode=A_PATCH8,
-                             img=(Ci, H, W)).view_as(weight)
-        if ctx.needs_input_grad[2]:
+            gw, cs = ops.gemm_tn(g, img, M=C, N=64 * Ci, K=g.shape[0], lda=C, b_mode=A_PATCH8, img=(Ci, H, W),
+                                 colsum=True)
+            gw = gw.view_as(weight)
+            if ctx.needs_input_grad[2]:
+                gb = cs
+        elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)
         return None, gw, gb
 

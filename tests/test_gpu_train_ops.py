@@ -36,6 +36,21 @@ def test_gemm_tn_rows(M, N, K):
     assert torch.equal(c, ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS))
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 576, 5000), (512, 2048, 333), (4, 128, 700), (132, 260, 64), (128, 64, 70000)])
+def test_gemm_tn_fused_colsum(M, N, K):
+    """The bias gradient from the TN GEMM's own A staging (mhada_gemm_tn_args.colsum): the column
+    sums of A against fp64, the GEMM unchanged by it, bits stable across calls (split-K slabs and
+    the per-tile partials are summed in a fixed order).  M = 4 takes the unfused fallback."""
+    a = rnd(K, M, seed=3)
+    b = rnd(K, N, seed=4)
+    c, cs = ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS, colsum=True)
+    assert rel(c, a.double().T @ b.double()) < 1e-5
+    assert rel(cs, a.double().sum(0)) < 1e-6
+    assert torch.equal(c, ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS))
+    c2, cs2 = ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=N, b_mode=A_ROWS, colsum=True)
+    assert torch.equal(c, c2) and torch.equal(cs, cs2)
+
+
 @pytest.mark.parametrize("rows,C", [(100000, 64), (37, 2048), (4096, 3 * 4)])
 def test_colsum(rows, C):
     x = rnd(rows, C, seed=3)
