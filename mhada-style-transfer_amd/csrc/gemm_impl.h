@@ -553,8 +553,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(const GemmP p) {
   constexpr int A_CH = BM / RS, B_CH = BN / RS;
   static_assert(A_CH >= 1 && B_CH >= 1 && TM >= 1 && TN >= 1, "tile config");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  TC* sA = reinterpret_cast<TC*>(smem);  // [2][BM][LS]
-  TC* sB = sA + 2 * BM * LS;             // [2][BN][LS]
+  // [nbuf][BM][LS] then [nbuf][BN][LS]: one K-step problems (the MHAda projections, K = 64) stage a
+  // single buffer, half the LDS, so more workgroups share a CU
+  const int nbuf = p.K > BK ? 2 : 1;
+  TC* sA = reinterpret_cast<TC*>(smem);
+  TC* sB = sA + nbuf * BM * LS;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -1211,11 +1214,14 @@ static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
                (size_t)2 * (BM + BN) * Cfg<TC>::LS * sizeof(TC) >= (size_t)WM * WN * 4096) ? 1 : 0;
   const int tiles_m = (p.M + BM - 1) / BM;
   p.ntiles = tiles_m * p.tiles_n;
-  const size_t lds = (size_t)2 * (BM + BN) * Cfg<TC>::LS * sizeof(TC);
+  const size_t lds2 = (size_t)2 * (BM + BN) * Cfg<TC>::LS * sizeof(TC);
+  // one staging buffer when K fits one step (the kernel's nbuf), at least the epilogue scratch
+  const size_t lds = p.K > Cfg<TC>::BK ? lds2
+                                       : std::max(lds2 / 2, (size_t)(p.lds_epi || p.vt ? WM * WN * 4096 : 0));
   static std::once_flag attr_once;  // per instantiation: allow > 64 KiB dynamic LDS
   std::call_once(attr_once, [&] {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<TC, TA, TO, AMODE, BM, BN, WM, WN>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
   });
   hipLaunchKernelGGL((gemm_kernel<TC, TA, TO, AMODE, BM, BN, WM, WN>), dim3(p.ntiles, nz), dim3(64 * WM * WN),
                      lds, stream, p);
@@ -1241,6 +1247,7 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // N == 128, ROWS mode)
   if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred) {
     if (p.vt) {
+      // (bf16: the 128x128 tile measured 5 % slower than 256x128)
       if constexpr (sizeof(TC) == 2) return launch_gemm<TC, TA, TO, AMODE, 256, 128, 4, 2>(p, nz, s);
       else return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);
     }

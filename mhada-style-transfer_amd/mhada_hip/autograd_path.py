@@ -1,10 +1,12 @@
 """Differentiable forward passes for the training path.
 
 When a forward needs gradients (``torch.is_grad_enabled()`` and a parameter or input requires
-grad — ``train_image.py:93-144``, feature-inversion scripts), the ``network`` modules route
-here instead of to the inference engine.  The MHAda attention core runs on the HIP training
-kernels (``MHAdaAttnFn``: csrc/attn_train.hip forward + backward); the remaining ops use
-PyTorch-ROCm autograd.
+grad — ``train_image.py:93-144``, feature-inversion scripts) or runs on CPU tensors (the
+reference scripts' no-GPU branch, ``infer_image.py:48``), the ``network`` modules route here
+instead of to the inference engine.  On ROCm device tensors every conv / linear / attention /
+normalisation runs on the HIP training kernels through the autograd Functions of
+``train_fns`` (and ``MHAdaAttnFn``: csrc/attn_train.hip forward + backward); on CPU tensors the
+same functions evaluate the reference's aten expression.
 Each function evaluates the reference algorithm on the module's own parameter containers
 (the same ``nn.Conv2d`` / ``nn.MultiheadAttention`` / ``nn.Linear`` / ``nn.LayerNorm`` objects
 whose state_dict keys match the reference), so autograd reaches exactly those parameters.
