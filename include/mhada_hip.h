@@ -237,6 +237,9 @@ typedef struct mhada_gemm_tn_args {
   int img_c, img_h, img_w, pad;
   float* c; long long ldc;
   float* colsum;  /* optional [M]: sum_k A[k][m] (the bias gradient), fused into the GEMM's A staging */
+  int nb;         /* batch of nb problems (0 / 1: one): A and B advance by sza / szb elements, C is
+                     [nb][M][N] (ldc == N), colsum [nb][M]; ROWS mode, M > 4 */
+  long long sza, szb;
 } mhada_gemm_tn_args;
 int mhada_gemm_tn_splits(int M, int N, int K);
 int mhada_gemm_tn(const mhada_gemm_tn_args* args, float* work, long long work_floats, mhada_stream_t stream);

@@ -39,7 +39,7 @@ const Knob kKnobs[] = {
     {"gemm_persist", &Tuning::gemm_persist},         {"gemm_pp128", &Tuning::gemm_pp128},
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
     {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
-    {"attn_sched", &Tuning::attn_sched},
+    {"attn_sched", &Tuning::attn_sched},             {"tn_skinny_lds", &Tuning::tn_skinny_lds},
     {"xknob", &Tuning::xknob},
 };
 

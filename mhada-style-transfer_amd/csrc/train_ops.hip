@@ -50,6 +50,7 @@ struct TnP {
   float* slab;                            // [splits][M][N]
   float* cslab;                           // [splits][M] column sums of A (null: none)
   int kchunk, tiles_n;
+  int nb; long long sza, szb;             // batch (blockIdx.z): A / B element strides; slabs [S][nb][M][N]
 };
 
 constexpr int kTnBN = 128, kTnBK = 32;
@@ -75,6 +76,9 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
   const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * kTnBN;
   const int kbeg = blockIdx.y * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int zb = blockIdx.z;
+  const float* __restrict__ pa = p.a + zb * p.sza;
+  const float* __restrict__ pb = p.b + zb * p.szb;
 
   // staging: chunk c = tid + 256 i (i < 4) -> tile row c >> 5 = (tid >> 5) + 8 i, 4 columns at 4 (c & 31)
   const int col = 4 * (tid & 31), row0 = tid >> 5;
@@ -94,6 +98,20 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
     tap_dx = tap - (tap / 3) * 3 - 1;
   }
   f32x4 ra[ACH], rb[4];
+  // CONV: output pixel (b, y, x) of this thread's B rows k0 + row0 + 8i, advanced by kTnBK per
+  // issue() (issue runs on k0 = kbeg, kbeg + kTnBK, ...) instead of divided out of k each time
+  int cbb[4] = {}, cyy[4] = {}, cxx[4] = {};
+  if constexpr (BMODE == MHADA_A_CONV3X3 || BMODE == MHADA_A_CONV3X3_ZERO) {
+    const int hw = p.out_h * p.out_w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kbeg + row0 + 8 * i;
+      cbb[i] = k / hw;
+      const int rem = k - cbb[i] * hw;
+      cyy[i] = rem / p.out_w;
+      cxx[i] = rem - cyy[i] * p.out_w;
+    }
+  }
   auto issue = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {  // A: chunk c = tid + 256 i -> row c / (BM/4), 4 columns at 4 (c % (BM/4))
@@ -102,10 +120,10 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       const int m = m0 + 4 * (c % (BM / 4));
       const bool kok = k < kend;
       if constexpr (VEC_A) {
-        ra[i] = (kok && m < p.M) ? *reinterpret_cast<const f32x4*>(p.a + (long long)k * p.lda + m) : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[i] = (kok && m < p.M) ? *reinterpret_cast<const f32x4*>(pa + (long long)k * p.lda + m) : f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ra[i][e] = (kok && m + e < p.M) ? p.a[(long long)k * p.lda + m + e] : 0.f;
+        for (int e = 0; e < 4; ++e) ra[i][e] = (kok && m + e < p.M) ? pa[(long long)k * p.lda + m + e] : 0.f;
       }
     }
 #pragma unroll
@@ -114,24 +132,30 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       const bool kok = k < kend;
       // B
       if constexpr (BMODE == MHADA_A_ROWS) {
-        rb[i] = (kok && bcol_ok) ? *reinterpret_cast<const f32x4*>(p.b + (long long)k * p.ldb + n0 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rb[i] = (kok && bcol_ok) ? *reinterpret_cast<const f32x4*>(pb + (long long)k * p.ldb + n0 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
       } else if constexpr (BMODE == MHADA_A_PATCH8) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (kok && bcol_ok) {
           const int gw = p.img_w / 8, gh = p.img_h / 8;
           const int bb = k / (gh * gw), rem = k - bb * (gh * gw);
           const int py = rem / gw, px = rem - py * gw;
-          v = *reinterpret_cast<const f32x4*>(p.b + (((long long)bb * p.img_c + ci) * p.img_h + py * 8 + tap_dy) * p.img_w +
+          v = *reinterpret_cast<const f32x4*>(pb + (((long long)bb * p.img_c + ci) * p.img_h + py * 8 + tap_dy) * p.img_w +
                                              px * 8 + tap_dx);
         }
         rb[i] = v;
       } else {
         bool ok = kok && bcol_ok;
         long long src = 0;
+        const int bb = cbb[i], oy = cyy[i], ox = cxx[i];
+        cxx[i] += kTnBK;  // the next issue's row
+        while (cxx[i] >= p.out_w) {
+          cxx[i] -= p.out_w;
+          if (++cyy[i] == p.out_h) {
+            cyy[i] = 0;
+            ++cbb[i];
+          }
+        }
         if (ok) {
-          const int hw = p.out_h * p.out_w;
-          const int bb = k / hw, rem = k - bb * hw;
-          const int oy = rem / p.out_w, ox = rem - oy * p.out_w;
           int Y, X;
           if constexpr (BMODE == MHADA_A_CONV3X3_ZERO) {
             Y = oy + tap_dy + 1 - p.pad;
@@ -143,7 +167,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
           }
           src = (((long long)bb * p.img_h + Y) * p.img_w + X) * p.img_c + ci;
         }
-        rb[i] = ok ? *reinterpret_cast<const f32x4*>(p.b + src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rb[i] = ok ? *reinterpret_cast<const f32x4*>(pb + src) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
@@ -213,10 +237,10 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       f32x4 v = part[tid];
       for (int j = 1; j < 256 / (BM / 4); ++j) v += part[tid + j * (BM / 4)];
       const int m = m0 + 4 * tid;
-      if (m < p.M) *reinterpret_cast<f32x4*>(p.cslab + (long long)blockIdx.y * p.M + m) = v;  // M % 4 == 0
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.cslab + ((long long)blockIdx.y * p.nb + zb) * p.M + m) = v;  // M % 4 == 0
     }
   }
-  float* slab = p.slab + (long long)blockIdx.y * p.M * p.N;
+  float* slab = p.slab + ((long long)blockIdx.y * p.nb + zb) * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < TMW; ++mi) {
     const int m = m0 + wm * (BM / 2) + mi * 32 + r32;
@@ -320,6 +344,83 @@ __global__ void __launch_bounds__(256) tn_skinny_kernel(const TnP p) {
       for (int j = 1; j < groups; ++j) s4 += part[j * tpc + t][m];
       if (m < p.M) *reinterpret_cast<f32x4*>(p.slab + ((long long)blockIdx.x * p.M + m) * p.N + n) = s4;
     }
+  }
+}
+
+// M <= 4, CONV modes, Cin % 64 == 0 (the 3-channel last decoder layer, conv.py:92, whose weight
+// gradient the gather form above reads 9x from L2: one 16-B tap load per (pixel, tap, channel
+// quad)).  Here a persistent block stages a 4 x 32 output-pixel tile's (4+2) x (32+2) input patch
+// of 64 channels (52 KiB) and the tile's dY rows in LDS once, and each thread (channel ci = t % 64,
+// tap group t / 64: taps {g, g+4, g+8} < 9) accumulates its 12 (tap, m) sums from LDS; blocks walk
+// the tiles w = blockIdx.x + i * gridDim.x in a fixed order, one slab row per block.
+constexpr int kSkTY = 4, kSkTX = 32, kSkPY = kSkTY + 2, kSkPX = kSkTX + 2;
+template <int BMODE>
+__global__ void __launch_bounds__(256) tn_skinny_lds_kernel(const TnP p, int ntiles_x, int ntiles) {
+  __shared__ __attribute__((aligned(16))) float sx[kSkPY * kSkPX * 64];
+  __shared__ f32x4 sdy[kSkTY * kSkTX];
+  const int t = threadIdx.x, ci = t & 63, tg = t >> 6;
+  const int cblk = blockIdx.y;  // 64-channel block of the input
+  const int P = BMODE == MHADA_A_CONV3X3_ZERO ? p.pad : 1;
+  const int tiles_img = ntiles / (p.K / (p.out_h * p.out_w));
+  float acc[3][4] = {};
+  for (int w = blockIdx.x; w < ntiles; w += gridDim.x) {
+    const int b = w / tiles_img, r = w - b * tiles_img;
+    const int y0 = (r / ntiles_x) * kSkTY, x0 = (r - (r / ntiles_x) * ntiles_x) * kSkTX;
+    // input patch rows y0 - P .. y0 - P + 5, columns x0 - P .. x0 - P + 33 (16 B per thread-item)
+    for (int e = t; e < kSkPY * kSkPX * 16; e += 256) {
+      const int px = e >> 4, q = e & 15;
+      const int py = px / kSkPX, pxx = px - py * kSkPX;
+      int Y = y0 - P + py, X = x0 - P + pxx;
+      bool ok = true;
+      if constexpr (BMODE == MHADA_A_CONV3X3_ZERO) {
+        ok = Y >= 0 && Y < p.img_h && X >= 0 && X < p.img_w;
+      } else {
+        Y = tn_reflect(Y, p.img_h);
+        X = tn_reflect(X, p.img_w);
+      }
+      Y = min(max(Y, 0), p.img_h - 1);  // rows / columns past a ragged tile edge feed no pixel
+      X = min(max(X, 0), p.img_w - 1);
+      const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(p.b + (((long long)b * p.img_h + Y) * p.img_w + X) * p.img_c +
+                                                          64 * cblk + 4 * q)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(&sx[px * 64 + 4 * q]) = v;
+    }
+    {  // dY of the tile's pixels (lda == 4): zero past the grid edge
+      const int oy = y0 + t / kSkTX, ox = x0 + t % kSkTX;
+      f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      if (t < kSkTY * kSkTX && oy < p.out_h && ox < p.out_w) {
+        d = *reinterpret_cast<const f32x4*>(p.a + (((long long)b * p.out_h + oy) * p.out_w + ox) * 4);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) d[m] = m < p.M ? d[m] : 0.f;
+      }
+      if (t < kSkTY * kSkTX) sdy[t] = d;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < kSkTY * kSkTX; ++q) {
+      const f32x4 d = sdy[q];
+      const int py = q / kSkTX, px = q - py * kSkTX;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int tap = tg + 4 * j;
+        if (tap < 9) {
+          const int dy = tap / 3, dx = tap - (tap / 3) * 3;  // patch offset of tap (dy-1, dx-1) is (dy, dx)
+          const float xv = sx[((py + dy) * kSkPX + px + dx) * 64 + ci];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[j][m] += d[m] * xv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = p.slab + (long long)blockIdx.x * p.M * p.N;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tap = tg + 4 * j;
+    if (tap < 9)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (m < p.M) slab[(long long)m * p.N + tap * p.img_c + 64 * cblk + ci] = acc[j][m];
   }
 }
 
@@ -936,6 +1037,13 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   TnP p{};
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.a = a->a; p.lda = a->lda; p.b = a->b; p.ldb = a->ldb;
+  // batch of nb independent problems (blockIdx.z; A / B advance by sza / szb elements, C and the
+  // column sums are [nb][M][N] / [nb][M] contiguous): the MFMA kernel, ROWS mode
+  p.nb = a->nb > 1 ? a->nb : 1;
+  p.sza = a->sza; p.szb = a->szb;
+  if (p.nb > 1 && (a->b_mode != MHADA_A_ROWS || a->M <= 4 || a->ldc != a->N || (a->sza | a->szb) % 4))
+    return fail("mhada_gemm_tn: batched form needs ROWS mode, M > 4, ldc == N, 16-B batch strides");
+  if (p.nb > 65535) return fail("mhada_gemm_tn: batch too large");
   const bool vec_a = al16(a->a) && a->lda % 4 == 0 && a->M % 4 == 0;
   switch (a->b_mode) {
     case MHADA_A_ROWS:
@@ -963,9 +1071,9 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   // fused bias gradient (colsum of A) on the MFMA kernel's vector A path; otherwise mhada_colsum's
   // kernel after the GEMM (the 3-channel layer, unaligned A)
   const bool fuse_cs = a->colsum && vec_a && p.M > 4;
-  int S = tn_splits(p.M, p.N, p.K);
-  const long long per = (long long)p.M * p.N + (fuse_cs ? p.M : 0);
-  if (work_floats < per) return fail("mhada_gemm_tn: workspace smaller than M*N (+M) floats");
+  int S = std::max(1, tn_splits(p.M, p.N, p.K) / p.nb);
+  const long long per = ((long long)p.M * p.N + (fuse_cs ? p.M : 0)) * p.nb;
+  if (work_floats < per) return fail("mhada_gemm_tn: workspace smaller than nb*(M*N (+M)) floats");
   S = (int)std::min<long long>(S, work_floats / per);
   p.kchunk = ((p.K + S - 1) / S + kTnBK - 1) / kTnBK * kTnBK;
   S = (p.K + p.kchunk - 1) / p.kchunk;
@@ -973,10 +1081,31 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   const int bm = tn_bm(p.M);
   const int tiles = ((p.M + bm - 1) / bm) * p.tiles_n;
   p.slab = work;
-  p.cslab = fuse_cs ? work + (long long)S * p.M * p.N : nullptr;
+  p.cslab = fuse_cs ? work + (long long)S * p.nb * p.M * p.N : nullptr;
   if (S > 65535) return fail("mhada_gemm_tn: too many splits");
-  const dim3 grid((unsigned)tiles, (unsigned)S);
+  const dim3 grid((unsigned)tiles, (unsigned)S, (unsigned)p.nb);
   const dim3 gsk((unsigned)S, (unsigned)((p.N / 4 + 255) / 256));
+  // the 3-channel layer (M <= 4, 3x3 conv, Cin % 64 == 0, dY rows of 4 floats): LDS-tiled kernel
+  if (p.M <= 4 && (a->b_mode == MHADA_A_CONV3X3 || a->b_mode == MHADA_A_CONV3X3_ZERO) && p.img_c % 64 == 0 &&
+      a->lda == 4 && al16(a->a) && tuning().tn_skinny_lds) {
+    const int ntx = (p.out_w + kSkTX - 1) / kSkTX, nty = (p.out_h + kSkTY - 1) / kSkTY;
+    const long long nt = (long long)(p.K / (p.out_h * p.out_w)) * ntx * nty;
+    if (nt < (1LL << 31)) {
+      const int G = (int)std::min<long long>(nt, std::min<long long>(1024, work_floats / per));
+      p.slab = work;
+      const dim3 gl((unsigned)G, (unsigned)(p.img_c / 64));
+      if (a->b_mode == MHADA_A_CONV3X3)
+        hipLaunchKernelGGL(tn_skinny_lds_kernel<MHADA_A_CONV3X3>, gl, dim3(256), 0, s, p, ntx, (int)nt);
+      else
+        hipLaunchKernelGGL(tn_skinny_lds_kernel<MHADA_A_CONV3X3_ZERO>, gl, dim3(256), 0, s, p, ntx, (int)nt);
+      if (int rc = check_launch("mhada_gemm_tn(skinny lds)")) return rc;
+      hipLaunchKernelGGL(slab_reduce_kernel, grid1((long long)p.M * p.N / 4), dim3(256), 0, s, work, a->c,
+                         (long long)p.M, p.N, a->ldc, G);
+      if (int rc = check_launch("mhada_gemm_tn(reduce)")) return rc;
+      if (!a->colsum) return 0;
+      return mhada_colsum(a->a, a->colsum, p.K, p.M, work, work_floats, s_);
+    }
+  }
 #define TN_LAUNCH(MODE)                                                                             \
   do {                                                                                              \
     if (p.M <= 4) hipLaunchKernelGGL((tn_skinny_kernel<MODE>), gsk, dim3(256), 0, s, p);           \
@@ -994,15 +1123,17 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
   else TN_LAUNCH(MHADA_A_CONV3X3_ZERO);
 #undef TN_LAUNCH
   if (int rc = check_launch("mhada_gemm_tn")) return rc;
-  const long long mn = (long long)p.M * p.N;
-  hipLaunchKernelGGL(slab_reduce_kernel, grid1(mn / 4), dim3(256), 0, s, work, a->c, (long long)p.M, p.N, a->ldc, S);
+  const long long mn = (long long)p.nb * p.M * p.N;
+  hipLaunchKernelGGL(slab_reduce_kernel, grid1(mn / 4), dim3(256), 0, s, work, a->c, (long long)p.nb * p.M, p.N,
+                     a->ldc, S);
   if (int rc = check_launch("mhada_gemm_tn(reduce)")) return rc;
   if (!a->colsum) return 0;
   if (fuse_cs) {
-    hipLaunchKernelGGL(slab_reduce_kernel, grid1(p.M / 4), dim3(256), 0, s, p.cslab, a->colsum, 1LL, p.M,
-                       (long long)p.M, S);
+    hipLaunchKernelGGL(slab_reduce_kernel, grid1((long long)p.nb * p.M / 4), dim3(256), 0, s, p.cslab, a->colsum, 1LL,
+                       p.nb * p.M, (long long)p.nb * p.M, S);
     return check_launch("mhada_gemm_tn(colsum reduce)");
   }
+  if (p.nb > 1) return fail("mhada_gemm_tn: batched column sums need 16-B aligned A with M % 4 == 0");
   // unfused: the column sums of A [K][lda] over its first M columns (the workspace is free again)
   if (a->lda != p.M || p.M % 4 || !al16(a->a)) return fail("mhada_gemm_tn: colsum needs a dense, aligned A");
   return mhada_colsum(a->a, a->colsum, p.K, p.M, work, work_floats, s_);

@@ -47,6 +47,7 @@ class GemmTnArgs(ctypes.Structure):
         ("a", _vp), ("lda", _c_ll), ("b", _vp), ("ldb", _c_ll), ("b_mode", ctypes.c_int),
         ("img_c", ctypes.c_int), ("img_h", ctypes.c_int), ("img_w", ctypes.c_int), ("pad", ctypes.c_int),
         ("c", _vp), ("ldc", _c_ll), ("colsum", _vp),
+        ("nb", ctypes.c_int), ("sza", _c_ll), ("szb", _c_ll),
     ]
 
 

@@ -542,18 +542,21 @@ def frame_ingest(frames: torch.Tensor, out_hw=None, bgr: bool = True) -> torch.T
 
 # ---- training path (fp32, NHWC): backward helpers (include/mhada_hip.h) ------------------
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, lda: int, ldb: int = 0,
-            b_mode: int = A_ROWS, img=(0, 0, 0), pad: int = 0, colsum: bool = False):
+            b_mode: int = A_ROWS, img=(0, 0, 0), pad: int = 0, colsum: bool = False, nb: int = 1,
+            sza: int = 0, szb: int = 0):
     """``mhada_gemm_tn``: C[M][N] = sum_k A[k][m] B[k][n] (fp32), deterministic split-K.  With
     ``colsum`` also the column sums of A (sum_k A[k][m], the bias gradient) from the same pass:
-    returns (C, colsum)."""
+    returns (C, colsum).  ``nb`` > 1: a batch of problems whose A / B start sza / szb elements
+    apart (ROWS mode); C is [nb][M][N] and the column sums [nb][M]."""
     _need_gpu(a, b)
     if a.dtype != torch.float32 or b.dtype != torch.float32:
         raise ValueError("gemm_tn is fp32")
     lib = _lib.load()
     splits = lib.mhada_gemm_tn_splits(M, N, K)
-    work = torch.empty(max(1, splits) * (M * N + (M if colsum else 0)), device=a.device, dtype=torch.float32)
-    c = torch.empty(M, N, device=a.device, dtype=torch.float32)
-    cs = torch.empty(M, device=a.device, dtype=torch.float32) if colsum else None
+    work = torch.empty(max(1, splits) * (M * N + (M if colsum else 0)) if nb == 1 else
+                       max(1, splits // nb) * nb * (M * N + (M if colsum else 0)), device=a.device, dtype=torch.float32)
+    c = torch.empty(*((nb,) if nb > 1 else ()), M, N, device=a.device, dtype=torch.float32)
+    cs = torch.empty(*((nb,) if nb > 1 else ()), M, device=a.device, dtype=torch.float32) if colsum else None
     args = GemmTnArgs()
     args.M, args.N, args.K = M, N, K
     args.a, args.lda, args.b, args.ldb, args.b_mode = a.data_ptr(), lda, b.data_ptr(), ldb, b_mode
@@ -561,6 +564,7 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, lda: int, 
     args.pad = pad
     args.c, args.ldc = c.data_ptr(), N
     args.colsum = cs.data_ptr() if colsum else None
+    args.nb, args.sza, args.szb = nb, sza, szb
     _call("mhada_gemm_tn", a, ctypes.byref(args), work.data_ptr(), work.numel())
     return (c, cs) if colsum else c
 

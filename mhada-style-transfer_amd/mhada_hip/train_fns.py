@@ -299,11 +299,12 @@ class HeadProjFn(torch.autograd.Function):
             ops.gemm(a=gy, w=weight.detach().transpose(1, 2).contiguous(), c=gx, M=T, N=64, K=64, compute=F32,
                      lda=64, sa=(T * 64, 0), nb=(H, 1), ldw=64, sw=(4096, 0), ldc=C, sc=(64, 0))
         if ctx.needs_input_grad[1]:
-            res = [ops.gemm_tn(gy[i], x[:, 64 * i:], M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS, colsum=True)
-                   for i in range(H)]
-            gw = torch.stack([r[0] for r in res])
+            # all heads in one batched TN launch (head i: A = gy[i], B = x[:, 64i:]), the bias
+            # gradients from the same pass
+            gw, cs = ops.gemm_tn(gy, x, M=64, N=64, K=T, lda=64, ldb=C, b_mode=A_ROWS, colsum=True, nb=H,
+                                 sza=T * 64, szb=64)
             if ctx.needs_input_grad[2]:
-                gb = torch.stack([r[1] for r in res])  # the column sums came out of the TN passes
+                gb = cs
         elif ctx.needs_input_grad[2]:
             gb = gy.sum(dim=1)
         return gx, gw, gb

@@ -51,6 +51,22 @@ def test_gemm_tn_fused_colsum(M, N, K):
     assert torch.equal(c, c2) and torch.equal(cs, cs2)
 
 
+@pytest.mark.parametrize("nb,M,N,K", [(8, 64, 64, 9000), (3, 128, 256, 700)])
+def test_gemm_tn_batched(nb, M, N, K):
+    """The batched TN form (HeadProjFn's per-head weight gradients in one launch): head i uses
+    A = a[i] and B = the column block b[:, N i:], exactly the per-problem results (bits), and the
+    column sums."""
+    a = rnd(nb, K, M, seed=5)
+    b = rnd(K, nb * N, seed=6)
+    c, cs = ops.gemm_tn(a, b, M=M, N=N, K=K, lda=M, ldb=nb * N, b_mode=A_ROWS, colsum=True, nb=nb,
+                        sza=K * M, szb=N)
+    for i in range(nb):
+        ci, csi = ops.gemm_tn(a[i], b[:, N * i:], M=M, N=N, K=K, lda=M, ldb=nb * N, b_mode=A_ROWS, colsum=True)
+        assert rel(c[i], a[i].double().T @ b[:, N * i:N * (i + 1)].double()) < 1e-5
+        assert rel(cs[i], a[i].double().sum(0)) < 1e-6
+        assert rel(c[i], ci) < 1e-6 and rel(cs[i], csi) < 1e-6
+
+
 @pytest.mark.parametrize("rows,C", [(100000, 64), (37, 2048), (4096, 3 * 4)])
 def test_colsum(rows, C):
     x = rnd(rows, C, seed=3)
@@ -311,9 +327,11 @@ def test_vit_training_forward_matches_aten_autograd():
 
 
 @pytest.mark.parametrize("M,N,K,mode", [(64, 576, 30000, "reflect"), (4, 576, 20000, "reflect"), (3, 576, 5000, "zero"),
-                                        (256, 2304, 8000, "zero")])
+                                        (4, 576, 7500, "zero"), (4, 1152, 5000, "reflect"), (256, 2304, 8000, "zero")])
 def test_gemm_tn_conv_tiles(M, N, K, mode):
-    """Weight-gradient tiles: the 64-row variant, the skinny (M <= 4) VALU kernel and 128 rows."""
+    """Weight-gradient tiles: the 64-row variant, the skinny (M <= 4) kernels — LDS-tiled for
+    Cin % 64 == 0 with 4-float dY rows, the gather form otherwise (M = 3) — and 128 rows; 50 x 50
+    images leave ragged 4 x 32 tiles."""
     from mhada_hip._lib import A_CONV3X3, A_CONV3X3_ZERO
     ci = N // 9
     H = W = 50
@@ -328,6 +346,12 @@ def test_gemm_tn_conv_tiles(M, N, K, mode):
     cols = cols.view(B, ci, 9, H * W).permute(0, 3, 2, 1).reshape(K, 9 * ci)  # -> [pixel][tap*ci + c]
     ref = g.double().T @ cols
     assert rel(c, ref) < 1e-5
+    if M == 4:  # the gather form on the same operands
+        from mhada_hip import _lib
+        with _lib.tuning(tn_skinny_lds=0):
+            c0 = ops.gemm_tn(g, x, M=M, N=N, K=K, lda=M, b_mode=A_CONV3X3 if mode == "reflect" else A_CONV3X3_ZERO,
+                             img=(ci, H, W), pad=1)
+        assert rel(c0, ref) < 1e-5
 
 
 @pytest.mark.parametrize("L", [1, 2, 3, 8])
