@@ -338,6 +338,18 @@ int mhada_frame_ingest(const void* frames, int B, int H, int W, long long row_by
  * bias [Cout] or NULL, y NHWC [B][Ho][Wo][ldc] (ldc >= Cout), optional ReLU.
  * Cin % 8 == 0, Cout % 64 == 0. */
 int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, mhada_stream_t stream);
+/* Weight (and bias) gradient of the same 3x3 conv (pad 1: MHADA_PAD_REFLECT as the decoder's
+ * ReflectionPad2d(1), or MHADA_PAD_ZERO), Winograd F(2x2,3x3) on the fp32 MFMA (replaces the
+ * im2col mhada_gemm_tn for the decoder convs of train_image.py:139):
+ *   dw [Cout][3][3][Cin] = sum over pixels of g[b][y][x][co] * x_pad[b][y+ky-1][x+kx-1][ci],
+ *   db [Cout] = sum of g (null: not computed).
+ * x NHWC [B][H][W][Cin], g NHWC [B][H][W][ldg] (ldg >= Cout, % 4).  Cin % 64 == 0, Cout % 64 == 0,
+ * H even, W % 16 == 0.  Tile-split partial sums in work (>= splits * (16*Cout*Cin + Cout) floats,
+ * splits = mhada_conv3x3_wgrad_wino_splits(...)), summed in a fixed order: deterministic. */
+int mhada_conv3x3_wgrad_wino_splits(int B, int H, int W, int Cin, int Cout);
+int mhada_conv3x3_wgrad_wino(const float* x, const float* g, float* dw, float* db, float* work, long long work_floats,
+                             int B, int H, int W, int Cin, int Cout, long long ldg, int pad_mode,
+                             mhada_stream_t stream);
 int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
                        int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
                        mhada_stream_t stream);

@@ -33,6 +33,8 @@
 // slots are XOR-swizzled (rswz) so the transform's ds_read_b32 hit distinct banks.
 #include "common.h"
 
+#include <algorithm>
+
 #ifndef WINO_DBG
 #define WINO_DBG 0  // ablation builds (tools/wino_dbg.py): 1 no MFMA, 2 no loads, 4 no transform
 #endif
@@ -313,11 +315,323 @@ __global__ void wino_weights_kernel(const float* __restrict__ w, float* __restri
     for (int j = 0; j < 4; ++j) ub[(long long)(4 * r + j) * Cout * kCK] = v[j];
   }
 }
+// ------------------------------------------------------------------------------------
+// Weight gradient of the same conv, Winograd F(2x2, 3x3) (the decoder's Conv2d weight / bias
+// gradients in train_image.py:139; replaces the im2col TN GEMM, 2.25x fewer products).
+// With U = G g G^T and Y_t = A^T (U . V_t) A for output tile t (V_t = B^T d_t B):
+//   dU[co][ci] = sum_t (A dY_t A^T)[co] . V_t[ci]      (16 positions, elementwise in xi)
+//   dg = G^T dU G                                        (4x4 -> 3x3 per (co, ci))
+// so per position xi the tile sum is a GEMM [Cout x tiles] x [tiles x Cin]: the forward kernel's
+// MFMA structure with the tiles as the reduction axis.  Workgroup = (64 co, 64 ci) x a split of the
+// tile chunks; a chunk = 8 consecutive tiles of one tile row (16 output columns).  Per chunk:
+//   * LDS-DMA of the output-gradient rows (2 x 16 px x 64 co, 8 KiB) and the input patch
+//     (4 x 18 px x 64 ci, 18 KiB), one chunk ahead, single-buffered (consumed by the transforms of
+//     the next chunk, after the barrier);
+//   * every thread transforms one (tile, co) item Yh = A dY A^T and one (tile, ci) item
+//     V = B^T d B of the NEXT chunk into the other buffers (raw pixels' 64 channels XOR-swizzled by
+//     pixel so the 8 tiles' reads hit distinct banks);
+//   * 32 MFMAs per wave of this chunk (8 positions x 4 k-steps of 2 tiles), one barrier.
+// Partial dU of each split goes to work [S][16][Cout][Cin], the bias gradient (sum of dY, from the
+// dY transform of the ci-block-0 workgroups) to [S][Cout]; wgrad_finish sums the splits in a fixed
+// order and applies G^T . G.  Deterministic.
+// ------------------------------------------------------------------------------------
+constexpr int kWgT = 8;                 // tiles per chunk (the MFMA reduction axis)
+constexpr int kWgS = 16 * 64 * kWgT;    // Yh / V buffer (floats): [16][64 rows][8 tiles]
+constexpr int kWgRX = 4 * 18 * 64;      // raw input patch (floats): [72 px][64 ci]
+constexpr int kWgRY = 2 * 16 * 64;      // raw output gradient (floats): [32 px][64 co]
+
+struct WgP {
+  const float* x;    // NHWC [B][H][W][Cin] (the conv input)
+  const float* g;    // NHWC [B][H][W][ldg] (the output gradient, ReLU mask applied)
+  float* slab;       // [S][16][Cout][Cin]
+  float* cslab;      // [S][Cout] or null
+  int B, H, W, Cin, Cout, zero;
+  long long ldg;
+  int crow, nchunk, cps;  // chunks per tile row, all chunks, chunks per split
+};
+
+// 64-channel pixel rows XOR-swizzled in units of 8 floats by pixel: channel c of pixel px at
+// px * 64 + (c ^ (8 * ((px >> 1) & 7)))
+MHADA_DEV int wg_px(int px, int c) { return px * 64 + (c ^ (8 * ((px >> 1) & 7))); }
+
+__global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * kWgS + kWgRX + kWgRY];  // 154 KiB
+  auto sYh = [&](int i) { return lds + i * kWgS; };
+  auto sVb = [&](int i) { return lds + (2 + i) * kWgS; };
+  float* sRX = lds + 4 * kWgS;
+  float* sRY = sRX + kWgRX;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int e = wave >> 2, coh = wave & 1, cih = (wave >> 1) & 1;
+  const int nib = p.Cin / 64;
+  const int cb = blockIdx.x / nib, ib = blockIdx.x - cb * nib;
+  const int co0 = cb * 64, ci0 = ib * 64;
+  const int c_beg = blockIdx.y * p.cps, c_end = min(p.nchunk, c_beg + p.cps);
+  const int P = 1;  // pad 1: reflect (decoder) or zero
+
+  auto chunk_pos = [&](int c, int& b, int& ty, int& tx0) {
+    const int per_img = (p.H / 2) * p.crow;
+    b = c / per_img;
+    const int r = c - b * per_img;
+    ty = r / p.crow;
+    tx0 = (r - ty * p.crow) * kWgT;
+  };
+  auto src_pix = [&](int b, int Y, int X, bool& ok) -> long long {
+    ok = true;
+    if (p.zero) {
+      ok = Y >= 0 && Y < p.H && X >= 0 && X < p.W;
+      Y = min(max(Y, 0), p.H - 1);
+      X = min(max(X, 0), p.W - 1);
+    } else {
+      Y = reflect_clamp(Y, p.H);
+      X = reflect_clamp(X, p.W);
+    }
+    return ((long long)b * p.H + Y) * p.W + X;
+  };
+  // LDS-DMA of chunk c's raw rows: dY 32 px x 16 quads (8 instructions, one per wave), X 72 px x 16
+  // quads (18 instructions: waves 0-7, then 0-7, then 0-1); slot (px, q) holds source quad
+  // q ^ (2 * ((px >> 1) & 7)); zero-padding pixels of X load a clamped pixel (zeroed in the transform)
+  auto dma = [&](int c) {
+#if WINO_DBG & 2
+    return;
+#endif
+    int b, ty, tx0;
+    chunk_pos(min(c, p.nchunk - 1), b, ty, tx0);
+    {
+      const int px = 4 * wave + (lane >> 4), q = lane & 15;
+      const int sq = q ^ (2 * ((px >> 1) & 7));
+      const int Y = 2 * ty + (px >> 4), X = 2 * tx0 + (px & 15);
+      glds16(p.g + (((long long)b * p.H + Y) * p.W + X) * p.ldg + co0 + 4 * sq, sRY + wave * 256);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int ins = wave + 8 * j;
+      if (ins < 18) {
+        const int px = 4 * ins + (lane >> 4), q = lane & 15;
+        const int sq = q ^ (2 * ((px >> 1) & 7));
+        bool ok;
+        const long long pix = src_pix(b, 2 * ty - P + px / 18, 2 * tx0 - P + px % 18, ok);
+        glds16(p.x + pix * p.Cin + ci0 + 4 * sq, sRX + ins * 256);
+      }
+    }
+  };
+  // transforms of the chunk whose raw rows are in sRY / sRX into buffer slot n: item (t, row) with
+  // t = lane & 7 and row = 8 * wave + (lane >> 3) (both the co of Yh and the ci of V)
+  const int it = lane & 7, irow = 8 * wave + (lane >> 3);
+  const int wdst = swz(irow, it >> 2) + (it & 3);
+  float bsum = 0.f;  // bias gradient partial of co = co0 + irow (ci block 0)
+  auto transform = [&](int c, int n) {
+#if WINO_DBG & 4
+    return;
+#endif
+    int b, ty, tx0;
+    chunk_pos(c, b, ty, tx0);
+    // Yh = A dY A^T, A = [[1,0],[1,1],[1,-1],[0,-1]]
+    float d[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) d[i][j] = sRY[wg_px(16 * i + 2 * it + j, irow)];
+    if (ib == 0) bsum += (d[0][0] + d[0][1]) + (d[1][0] + d[1][1]);
+    float a[4][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      a[0][j] = d[0][j];
+      a[1][j] = d[0][j] + d[1][j];
+      a[2][j] = d[0][j] - d[1][j];
+      a[3][j] = -d[1][j];
+    }
+    float* yh = sYh(n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      yh[(4 * i + 0) * 512 + wdst] = a[i][0];
+      yh[(4 * i + 1) * 512 + wdst] = a[i][0] + a[i][1];
+      yh[(4 * i + 2) * 512 + wdst] = a[i][0] - a[i][1];
+      yh[(4 * i + 3) * 512 + wdst] = -a[i][1];
+    }
+    // V = B^T d B on the 4 x 4 patch of tile it (input rows 2ty-1 .. 2ty+2)
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int px = 18 * i + 2 * it + j;
+        float val = sRX[wg_px(px, irow)];
+        if (p.zero) {
+          const int Y = 2 * ty - P + i, X = 2 * tx0 - P + 2 * it + j;
+          if (Y < 0 || Y >= p.H || X < 0 || X >= p.W) val = 0.f;
+        }
+        v[4 * i + j] = val;
+      }
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[0 * 4 + j] = v[0 * 4 + j] - v[2 * 4 + j];
+      t[1 * 4 + j] = v[1 * 4 + j] + v[2 * 4 + j];
+      t[2 * 4 + j] = v[2 * 4 + j] - v[1 * 4 + j];
+      t[3 * 4 + j] = v[1 * 4 + j] - v[3 * 4 + j];
+    }
+    float* sv = sVb(n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sv[(4 * i + 0) * 512 + wdst] = t[4 * i + 0] - t[4 * i + 2];
+      sv[(4 * i + 1) * 512 + wdst] = t[4 * i + 1] + t[4 * i + 2];
+      sv[(4 * i + 2) * 512 + wdst] = t[4 * i + 2] - t[4 * i + 1];
+      sv[(4 * i + 3) * 512 + wdst] = t[4 * i + 1] - t[4 * i + 3];
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[x][q] = 0.f;
+  // A operand = Yh rows (co 32 coh + r32), B operand = V rows (ci 32 cih + r32); k-step s of lane
+  // half h takes tile 4h + s
+  const int arow = swz(32 * coh + r32, h) + 8 * e * 512, brow = swz(32 * cih + r32, h) + 8 * e * 512;
+  auto mfmas = [&](int n) {
+#if WINO_DBG & 1
+    return;
+#endif
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(sYh(n) + x * 512 + arow);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(sVb(n) + x * 512 + brow);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x], 0, 0, 0);
+    }
+  };
+  auto publish = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  if (c_beg < c_end) {
+    dma(c_beg);
+    publish();
+    transform(c_beg, 0);
+    __syncthreads();
+    // chunk c: DMA of c+1's raw rows (the raw buffers were last read by transform(c) before the
+    // barrier), MFMAs on slot c&1, then (after its DMA landed) transform c+1 into the other slot
+    for (int c = c_beg; c < c_end; ++c) {
+      const int k = c - c_beg, cur = k & 1;
+      const bool more = c + 1 < c_end;
+      if (more) dma(c + 1);
+      mfmas(cur);
+      if (more) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's pieces of c+1 landed
+        transform(c + 1, cur ^ 1);
+      }
+      __syncthreads();
+    }
+  }
+  // partial dU of this split: acc[x] <-> position 8e + x, co = 32 coh + (r & 3) + 8 (r >> 2) + 4h,
+  // ci = 32 cih + r32
+  float* sl = p.slab + (long long)blockIdx.y * 16 * p.Cout * p.Cin;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + 32 * coh + (r & 3) + 8 * (r >> 2) + 4 * h, ci = ci0 + 32 * cih + r32;
+      sl[((long long)(8 * e + x) * p.Cout + co) * p.Cin + ci] = acc[x][r];
+    }
+  if (p.cslab && ib == 0) {  // the 8 tile lanes of a co are consecutive lanes: fixed-order xor tree
+    bsum += __shfl_xor(bsum, 1, 64);
+    bsum += __shfl_xor(bsum, 2, 64);
+    bsum += __shfl_xor(bsum, 4, 64);
+    if (it == 0) p.cslab[(long long)blockIdx.y * p.Cout + co0 + irow] = bsum;
+  }
+}
+
+// dW[co][tap][ci] = G^T (sum_s dU[s][.][co][ci]) G, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]];
+// db[co] = sum_s cslab[s][co] (threads with ci == 0)
+__global__ void __launch_bounds__(256) wino_wgrad_finish_kernel(const float* __restrict__ slab,
+                                                                const float* __restrict__ cslab, float* __restrict__ dw,
+                                                                float* __restrict__ db, int Cout, int Cin, int S) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)Cout * Cin) return;
+  const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+  const long long st = (long long)Cout * Cin;
+  float u[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) u[x] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const float* q = slab + (long long)s * 16 * st + i;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) u[x] += q[x * st];
+  }
+  // m = G^T u (3 x 4): row a of G^T is column a of G
+  float m[3][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    m[0][c] = u[0 * 4 + c] + 0.5f * (u[1 * 4 + c] + u[2 * 4 + c]);
+    m[1][c] = 0.5f * (u[1 * 4 + c] - u[2 * 4 + c]);
+    m[2][c] = 0.5f * (u[1 * 4 + c] + u[2 * 4 + c]) + u[3 * 4 + c];
+  }
+  float* o = dw + (long long)co * 9 * Cin + ci;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    o[(3 * a + 0) * Cin] = m[a][0] + 0.5f * (m[a][1] + m[a][2]);
+    o[(3 * a + 1) * Cin] = 0.5f * (m[a][1] - m[a][2]);
+    o[(3 * a + 2) * Cin] = 0.5f * (m[a][1] + m[a][2]) + m[a][3];
+  }
+  if (db && cslab && ci == 0) {
+    float sb = 0.f;
+    for (int s = 0; s < S; ++s) sb += cslab[(long long)s * Cout + co];
+    db[co] = sb;
+  }
+}
 }  // namespace
 
 }  // namespace mhada
 
 using namespace mhada;
+
+extern "C" int mhada_conv3x3_wgrad_wino_splits(int B, int H, int W, int Cin, int Cout) {
+  if (B <= 0 || H < 2 || W < 16 || Cin <= 0 || Cout <= 0 || Cin % 64 || Cout % 64) return 0;
+  const long long nchunk = (long long)B * (H / 2) * (W / 16);
+  const long long blocks = (long long)(Cout / 64) * (Cin / 64);
+  // about two workgroups per CU over the grid, at least 16 chunks per split
+  const long long s = std::max<long long>(1, std::min<long long>((512 + blocks - 1) / blocks, nchunk / 16));
+  return (int)std::min<long long>(s, 65535);
+}
+
+extern "C" int mhada_conv3x3_wgrad_wino(const float* x, const float* g, float* dw, float* db, float* work,
+                                        long long work_floats, int B, int H, int W, int Cin, int Cout, long long ldg,
+                                        int pad_mode, mhada_stream_t s_) {
+  if (!x || !g || !dw || !work || B <= 0 || H < 2 || W < 2 || Cin <= 0 || Cout <= 0)
+    return fail("mhada_conv3x3_wgrad_wino: bad args");
+  if (Cin % 64 || Cout % 64 || H % 2 || W % 16)
+    return fail("mhada_conv3x3_wgrad_wino: needs Cin % 64 == 0, Cout % 64 == 0, H even, W % 16 == 0");
+  if (pad_mode != MHADA_PAD_REFLECT && pad_mode != MHADA_PAD_ZERO) return fail("mhada_conv3x3_wgrad_wino: bad pad_mode");
+  if (ldg < Cout || ldg % 4) return fail("mhada_conv3x3_wgrad_wino: ldg >= Cout, ldg % 4 == 0");
+  if (((uintptr_t)x | (uintptr_t)g | (uintptr_t)work) & 15) return fail("mhada_conv3x3_wgrad_wino: 16-byte aligned x, g, work");
+  if ((long long)B * H * W * std::max<long long>(Cin, ldg) > (1LL << 31) - 1)
+    return fail("mhada_conv3x3_wgrad_wino: problem too large for 32-bit indexing");
+  WgP p;
+  p.x = x; p.g = g;
+  p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.ldg = ldg;
+  p.zero = pad_mode == MHADA_PAD_ZERO;
+  p.crow = W / 16;
+  p.nchunk = B * (H / 2) * p.crow;
+  int S = mhada_conv3x3_wgrad_wino_splits(B, H, W, Cin, Cout);
+  const long long per = 16LL * Cout * Cin + (db ? Cout : 0);
+  S = (int)std::min<long long>(S, work_floats / per);
+  if (S < 1) return fail("mhada_conv3x3_wgrad_wino: workspace smaller than 16*Cout*Cin (+Cout) floats");
+  p.cps = (p.nchunk + S - 1) / S;
+  S = (p.nchunk + p.cps - 1) / p.cps;
+  p.slab = work;
+  p.cslab = db ? work + (long long)S * 16 * Cout * Cin : nullptr;
+  const dim3 grid((unsigned)((Cout / 64) * (Cin / 64)), (unsigned)S);
+  hipLaunchKernelGGL(wino_wgrad_kernel, grid, dim3(512), 0, (hipStream_t)s_, p);
+  if (int rc = check_launch("mhada_conv3x3_wgrad_wino")) return rc;
+  const long long n = (long long)Cout * Cin;
+  hipLaunchKernelGGL(wino_wgrad_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s_,
+                     p.slab, p.cslab, dw, db, Cout, Cin, S);
+  return check_launch("mhada_conv3x3_wgrad_wino(finish)");
+}
 
 extern "C" int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, mhada_stream_t s_) {
   if (!w || !u || Cout <= 0 || Cin <= 0 || Cin % kCK) return fail("mhada_wino_weights: bad args (Cin % 8 == 0)");

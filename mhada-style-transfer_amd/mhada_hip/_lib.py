@@ -96,6 +96,8 @@ SIGNATURES = {
     "mhada_vgg_input": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_wino_weights": (_I, [_vp, _vp, _I, _I, _vp]),
+    "mhada_conv3x3_wgrad_wino_splits": (_I, [_I, _I, _I, _I, _I]),
+    "mhada_conv3x3_wgrad_wino": (_I, [_vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _I, _I, _I, _c_ll, _I, _vp]),
     "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp]),
 }
 

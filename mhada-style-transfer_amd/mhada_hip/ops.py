@@ -145,6 +145,41 @@ def wino_eligible(x: torch.Tensor, w: torch.Tensor, upsample: bool) -> bool:
             and x.numel() < 2 ** 31 and x.numel() // x.shape[-1] * w.shape[0] < 2 ** 31)
 
 
+# Winograd weight gradients for the eligible training convs (tests flip this to compare with the TN GEMM)
+WINO_WGRAD = True
+
+
+def wgrad_wino_eligible(x: torch.Tensor, g: torch.Tensor, cout: int) -> bool:
+    """mhada_conv3x3_wgrad_wino's constraints: fp32 NHWC x [B][H][W][Cin] and g [B][H][W][ldg],
+    Cin % 64 == 0, Cout % 64 == 0, H even, W % 16 == 0, 32-bit element offsets."""
+    if not (WINO_WGRAD and x.is_cuda and x.dtype == torch.float32 and g.dtype == torch.float32):
+        return False
+    B, H, W, ci = x.shape
+    return (ci % 64 == 0 and cout % 64 == 0 and H % 2 == 0 and W % 16 == 0 and g.shape[:3] == x.shape[:3]
+            and g.shape[3] >= cout and g.shape[3] % 4 == 0 and x.is_contiguous() and g.is_contiguous()
+            and B * H * W * max(ci, g.shape[3]) < 2 ** 31)
+
+
+def conv3x3_wgrad_wino(x: torch.Tensor, g: torch.Tensor, cout: int, pad_mode: str = "reflect",
+                       bias: bool = True):
+    """``mhada_conv3x3_wgrad_wino``: the weight gradient [Cout][9*Cin] (k = tap*Cin + ci, the
+    gemm_tn layout) and the bias gradient [Cout] (or None) of a pad-1 3x3 conv, from its input x
+    and output gradient g (NHWC fp32)."""
+    _need_gpu(x, g)
+    B, H, W, ci = x.shape
+    lib = _lib.load()
+    S = lib.mhada_conv3x3_wgrad_wino_splits(B, H, W, ci, cout)
+    if S <= 0:
+        raise ValueError("conv3x3_wgrad_wino: ineligible shape")
+    work = torch.empty(S * (16 * cout * ci + (cout if bias else 0)), device=x.device, dtype=torch.float32)
+    dw = torch.empty(cout, 9 * ci, device=x.device, dtype=torch.float32)
+    db = torch.empty(cout, device=x.device, dtype=torch.float32) if bias else None
+    _call("mhada_conv3x3_wgrad_wino", x, x.data_ptr(), g.data_ptr(), dw.data_ptr(),
+          db.data_ptr() if bias else None, work.data_ptr(), work.numel(), B, H, W, ci, cout, g.shape[3],
+          _lib.PAD_REFLECT if pad_mode == "reflect" else _lib.PAD_ZERO)
+    return dw, db
+
+
 def wino_weights(w: torch.Tensor) -> torch.Tensor:
     """``mhada_wino_weights``: w packed [Cout][9*Cin] fp32 -> U [Cin/8][16][Cout][8]."""
     _need_gpu(w)

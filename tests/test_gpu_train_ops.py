@@ -501,3 +501,22 @@ def test_feature_loss_fn_matches_aten_autograd(stats, target, B, C, H, W):
     for got, want in refs:
         assert abs(got.item() - want.item()) <= 1e-5 * abs(want.item())
     assert rel(x.grad, xd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("pad_mode", ["reflect", "zero"])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldg", [(2, 8, 16, 64, 64, 64), (1, 18, 32, 128, 256, 256), (3, 6, 48, 64, 128, 132)])
+def test_conv3x3_wgrad_wino(pad_mode, B, H, W, Ci, Co, ldg):
+    """mhada_conv3x3_wgrad_wino (the decoder's weight / bias gradients) against fp64: dW[co][tap][ci]
+    = sum_pixels g * x_pad (the same im2col contraction the TN GEMM computes) and db = sum g; a
+    padded output-gradient row stride (ldg > Cout) and several tile-chunk splits; bits stable."""
+    x = rnd(B, H, W, Ci, seed=41)
+    gfull = rnd(B, H, W, ldg, seed=42)
+    dw, db = ops.conv3x3_wgrad_wino(x, gfull, Co, pad_mode, bias=True)
+    g = gfull[..., :Co].double()
+    xp = F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect" if pad_mode == "reflect" else "constant")
+    cols = F.unfold(xp, 3).view(B, Ci, 9, H * W).permute(0, 3, 2, 1).reshape(B * H * W, 9 * Ci)
+    ref = g.reshape(-1, Co).T @ cols
+    assert rel(dw, ref) < 2e-6
+    assert rel(db, g.reshape(-1, Co).sum(0)) < 1e-6
+    dw2, db2 = ops.conv3x3_wgrad_wino(x, gfull, Co, pad_mode, bias=True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
