@@ -14,7 +14,7 @@ y = torch.empty(B, H, H, Co, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 flop = 2.0 * 9 * Ci * Co * B * H * H
 for v in bits:
-    lib = ctypes.CDLL(os.path.join(REPO, "mhada-style-transfer_amd", "build_dbg", f"libwino_{v}.so"))
+    lib = ctypes.CDLL(os.path.join(REPO, "mhada-style-transfer_amd", os.environ.get("WINO_LIB_DIR", "build_dbg"), f"libwino_{v}.so"))
     lib.mhada_conv3x3_wino.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_longlong] + \
         [ctypes.c_int] * 3 + [ctypes.c_void_p]
     lib.mhada_wino_weights.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
