@@ -210,12 +210,30 @@ def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tens
     return blk.out_conv(o)
 
 
+def _cosine_moments(q, k, v):
+    """(A V, A V^2) for the cosine activation (adaDecoder.py:20-34) WITHOUT forming A: with unit
+    rows q^ and columns k^, A[i][j] = (q^_i . k^_j + 1) / l_i and l_i = q^_i . sum_j k^_j + Ns, so
+      A V   = (q^ (K^ V)   + 1 sum_j v_j)   / l,   A V^2 = (q^ (K^ V^2) + 1 sum_j v_j^2) / l
+    with d x d products (O(N d^2) instead of the N_c x N_s matrix) — the same quantities as the
+    reference expression up to fp32 summation order, and a backward that autograd derives without
+    the N_c x N_s intermediates.  q (B, Nc, d), k (B, d, Ns), v (B, Ns, d)."""
+    qn = q / q.norm(dim=-1, keepdim=True)
+    kn = k / k.norm(dim=1, keepdim=True)
+    v2 = v * v
+    l = torch.matmul(qn, kn.sum(dim=-1, keepdim=True)) + k.shape[-1]          # (B, Nc, 1)
+    m = (torch.bmm(qn, torch.bmm(kn, v)) + v.sum(dim=1, keepdim=True)) / l
+    e2 = (torch.bmm(qn, torch.bmm(kn, v2)) + v2.sum(dim=1, keepdim=True)) / l
+    return m, e2
+
+
 def block_forward(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) -> torch.Tensor:
-    """AdaAttnMultiHead.forward (adaDecoder.py:162-206)."""
+    """AdaAttnMultiHead.forward (adaDecoder.py:162-206).  On a ROCm device the cosine activation
+    trains on its linear form (_cosine_moments); CPU tensors evaluate the reference expression."""
     if _fused_train_attn(blk, fc):
         return block_forward_fused(blk, fc, fs, fcs)
     B, _, h, w = fc.shape
     d = blk.head_dim
+    linear_cos = fc.is_cuda and blk.activation_name == "cosine"
     outs = []
     for i in range(blk.num_heads):
         sl = slice(i * d, (i + 1) * d)
@@ -223,9 +241,13 @@ def block_forward(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tensor) ->
         k = blk.g_list[i](F.instance_norm(fs[:, sl]))
         k = k.reshape(B, d, -1)
         v = blk.h_list[i](fs[:, sl]).reshape(B, d, -1).permute(0, 2, 1)
-        a = _softmax_or_cosine(q, k, blk.activation_name)
-        m = torch.bmm(a, v)
-        s = torch.sqrt((torch.bmm(a, v * v) - m * m).clamp(min=1e-6))
+        if linear_cos:
+            m, e2 = _cosine_moments(q, k, v)
+            s = torch.sqrt((e2 - m * m).clamp(min=1e-6))
+        else:
+            a = _softmax_or_cosine(q, k, blk.activation_name)
+            m = torch.bmm(a, v)
+            s = torch.sqrt((torch.bmm(a, v * v) - m * m).clamp(min=1e-6))
         m = m.reshape(B, h, w, d).permute(0, 3, 1, 2)
         s = s.reshape(B, h, w, d).permute(0, 3, 1, 2)
         outs.append(s * F.instance_norm(fcs[:, sl]) + m)

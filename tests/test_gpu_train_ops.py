@@ -520,3 +520,23 @@ def test_conv3x3_wgrad_wino(pad_mode, B, H, W, Ci, Co, ldg):
     assert rel(db, g.reshape(-1, Co).sum(0)) < 1e-6
     dw2, db2 = ops.conv3x3_wgrad_wino(x, gfull, Co, pad_mode, bias=True)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+def test_cosine_block_training_linear_form_matches_reference_autograd():
+    """The cosine activation under autograd on the device (adaDecoder.py:20-34) runs the linear form
+    (A V = (q^ (K^ V) + sum v) / l, no N_c x N_s matrix): block output and parameter gradients
+    against fp64 autograd of the reference expression on the CPU."""
+    import network
+    torch.manual_seed(3)
+    blk = network.AdaAttnMultiHead(qkv_dim=128, num_heads=2, activation="cosine")
+    fc, fs, fcs = (torch.randn(2, 128, 12, 10), torch.randn(2, 128, 8, 14), torch.randn(2, 128, 12, 10))
+    ref = network.AdaAttnMultiHead(qkv_dim=128, num_heads=2, activation="cosine").double()
+    ref.load_state_dict(blk.state_dict())
+    out_ref = ref(fc.double(), fs.double(), fcs.double())
+    out_ref.square().sum().backward()
+    g = blk.to(DEV)
+    out = g(fc.to(DEV), fs.to(DEV), fcs.to(DEV))
+    out.square().sum().backward()
+    assert rel(out, out_ref) < 1e-5
+    for (n, p), (_, pr) in zip(g.named_parameters(), ref.named_parameters()):
+        assert rel(p.grad, pr.grad) < 1e-4, n
