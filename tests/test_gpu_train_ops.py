@@ -537,6 +537,6 @@ def test_cosine_block_training_linear_form_matches_reference_autograd():
     g = blk.to(DEV)
     out = g(fc.to(DEV), fs.to(DEV), fcs.to(DEV))
     out.square().sum().backward()
-    assert rel(out, out_ref) < 1e-5
+    assert rel(out.cpu(), out_ref) < 1e-5
     for (n, p), (_, pr) in zip(g.named_parameters(), ref.named_parameters()):
-        assert rel(p.grad, pr.grad) < 1e-4, n
+        assert rel(p.grad.cpu(), pr.grad) < 1e-4, n
