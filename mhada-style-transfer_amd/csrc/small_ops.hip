@@ -84,7 +84,9 @@ __global__ void __launch_bounds__(256) vit_batch_attn_kernel(const T* __restrict
 // consecutive features (one 16-B bf16 / two 16-B fp32 loads per q/k/v row instead of 2-4-byte
 // per-lane loads); the L x L dot products are 8-lane shuffle reductions, the softmax and PV
 // are lane-local.
-template <typename T>
+// LMAX (4 | 8) sizes the per-lane q / k / v rows: at L <= 4 (1024^2 batch 4) the kernel keeps
+// 96 instead of 192 of them live, so twice the waves hide the loads.
+template <typename T, int LMAX>
 __global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                                  int L, int ntok, int heads) {
   constexpr int D = 64, E = 8;
@@ -110,9 +112,9 @@ __global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __rest
       }
     }
   };
-  float q[8][E], k[8][E], v[8][E];
+  float q[LMAX][E], k[LMAX][E], v[LMAX][E];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < LMAX; ++i) {
     if (i < L) {
       load8(base + i * row_stride, q[i]);
       load8(base + i * row_stride + C, k[i]);
@@ -120,12 +122,12 @@ __global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __rest
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < LMAX; ++i) {
     if (i >= L) break;
-    float sc[8];
+    float sc[LMAX];
     float m = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < LMAX; ++j) {
       if (j < L) {
         float d = 0.f;
 #pragma unroll
@@ -140,7 +142,7 @@ __global__ void __launch_bounds__(256) vit_batch_attn_vec_kernel(const T* __rest
 #pragma unroll
     for (int e = 0; e < E; ++e) o8[e] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < LMAX; ++j) {
       if (j < L) {
         const float p = __expf(sc[j] - m);
         l += p;
@@ -760,8 +762,12 @@ extern "C" int mhada_vit_batch_attn(const void* qkv, void* out, int dtype, int L
     // 54.8 vs 51.4 us at 512^2 B8. tuning vit_attn_vec = 0 selects the per-lane form (A/B).
     if (dtype != MHADA_F32 && tuning().vit_attn_vec && aligned16(qkv) && aligned16(out)) {
       const dim3 g32((unsigned)((pairs + 31) / 32));
-      hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
-                         ntok, heads);
+      if (L <= 4)
+        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16, 4>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
+                           ntok, heads);
+      else
+        hipLaunchKernelGGL((vit_batch_attn_vec_kernel<bf16, 8>), g32, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, L,
+                           ntok, heads);
       return check_launch("mhada_vit_batch_attn");
     }
     if (dtype == MHADA_F32)

@@ -257,7 +257,7 @@ def test_layernorm(dt):
 
 
 @pytest.mark.parametrize("dt,vec", [(torch.float32, "1"), (torch.bfloat16, "1"), (torch.bfloat16, "0")])
-@pytest.mark.parametrize("L", [1, 2, 3, 8, 11])
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 8, 11])
 def test_vit_batch_attention_matches_nn_mha(dt, vec, L):
     N, C, heads = 300, 512, 8
     mha = torch.nn.MultiheadAttention(C, heads).to(DEV).double()
