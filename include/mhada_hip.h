@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 8 (mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 9 (3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -353,6 +353,27 @@ int mhada_conv3x3_wgrad_wino(const float* x, const float* g, float* dw, float* d
 int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
                        int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
                        mhada_stream_t stream);
+
+/* The 3-channel ends of the training conv stacks (rgb_ops.hip), fp32:
+ * VGG19's first layer (vgg19.py:10-11,25-26: normalise -> Conv2d(3, 64, 3, padding=1) -> ReLU),
+ * input gradient w.r.t. the RGB image in one pass (replaces mhada_relu_bwd + a 64 -> 32-channel
+ * zero-padded transposed conv on mhada_gemm + mhada_vgg_input_bwd):
+ *   dimg [B][3][H][W] = adjoint of normalise( sum_{tap,co} g[p + d_tap][co] wd[tap][co][c] ),
+ *   g = dy * (y > 0); dy, y NHWC [B][H][W][64]; wd [9][64][3] = W[co][c][8 - tap] (flipped). */
+int mhada_vgg_stem_dgrad(const float* dy, const float* y, const float* wd, float* dimg, int B, int H, int W,
+                         mhada_stream_t stream);
+/* The decoder's last layer (conv.py:39-45,94: ReflectionPad2d(1) -> Conv2d(64, 3, 3) -> ReLU; its
+ * forward is mhada_conv3x3_out3): input gradient dx NHWC [B][H][W][64] with the reflection-pad
+ * adjoint folded in, from dy and the layer output y (NCHW [B][3][H][W]) and wd [9][3][64] =
+ * W[co][ci][tap] (replaces relu_bwd + channel padding + a pad-2 transposed conv + mhada_reflect_fold). */
+int mhada_out3_dgrad(const float* dy, const float* y, const float* wd, float* dx, int B, int H, int W,
+                     mhada_stream_t stream);
+/* Its weight gradient dw [3][64][3][3] and bias gradient db [3] (null: skipped) from the layer
+ * input x NHWC [B][H][W][64], dy and y as above; per-workgroup partials in work (>= mhada_out3_wgrad_work
+ * floats) summed in a fixed order (replaces the M <= 4 mhada_gemm_tn + colsum). */
+long long mhada_out3_wgrad_work(int B, int H, int W);
+int mhada_out3_wgrad(const float* x, const float* dy, const float* y, float* dw, float* db, float* work,
+                     long long work_floats, int B, int H, int W, mhada_stream_t stream);
 
 #ifdef __cplusplus
 }

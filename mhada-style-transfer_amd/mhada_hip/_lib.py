@@ -99,6 +99,10 @@ SIGNATURES = {
     "mhada_conv3x3_wgrad_wino_splits": (_I, [_I, _I, _I, _I, _I]),
     "mhada_conv3x3_wgrad_wino": (_I, [_vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _I, _I, _I, _c_ll, _I, _vp]),
     "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp]),
+    "mhada_vgg_stem_dgrad": (_I, [_vp] * 4 + [_I] * 3 + [_vp]),
+    "mhada_out3_dgrad": (_I, [_vp] * 4 + [_I] * 3 + [_vp]),
+    "mhada_out3_wgrad_work": (_c_ll, [_I, _I, _I]),
+    "mhada_out3_wgrad": (_I, [_vp] * 6 + [_c_ll, _I, _I, _I, _vp]),
 }
 
 _lib = None
@@ -128,7 +132,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 def get_tuning(name: str) -> int:

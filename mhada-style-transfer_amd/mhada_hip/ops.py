@@ -694,6 +694,58 @@ def vgg_input_bwd(dout: torch.Tensor) -> torch.Tensor:
     return dimg
 
 
+def _f32_contig(*ts: torch.Tensor, what: str) -> None:
+    for t in ts:
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"{what}: contiguous fp32 tensors expected")
+
+
+def vgg_stem_dgrad(dy: torch.Tensor, y: torch.Tensor, wd: torch.Tensor) -> torch.Tensor:
+    """``mhada_vgg_stem_dgrad``: image gradient [B][3][H][W] of normalise -> conv3x3(3 -> 64, zero
+    pad) -> ReLU from dy, y NHWC [B][H][W][64] and the flipped weights wd [9][64][3]."""
+    _need_gpu(dy, y, wd)
+    _f32_contig(dy, y, wd, what="vgg_stem_dgrad")
+    B, H, W, C = y.shape
+    if C != 64 or dy.shape != y.shape or wd.shape != (9, 64, 3):
+        raise ValueError("vgg_stem_dgrad: dy, y [B][H][W][64], wd [9][64][3]")
+    dimg = torch.empty(B, 3, H, W, device=y.device, dtype=torch.float32)
+    _call("mhada_vgg_stem_dgrad", y, dy.data_ptr(), y.data_ptr(), wd.data_ptr(), dimg.data_ptr(), B, H, W)
+    return dimg
+
+
+def out3_dgrad(dy: torch.Tensor, y: torch.Tensor, wd: torch.Tensor) -> torch.Tensor:
+    """``mhada_out3_dgrad``: input gradient NHWC [B][H][W][64] of ReflectionPad2d(1) -> conv3x3(64 -> 3)
+    -> ReLU from dy and the output y (NCHW [B][3][H][W]) and wd [9][3][64] (W[co][ci][tap])."""
+    _need_gpu(dy, y, wd)
+    _f32_contig(dy, y, wd, what="out3_dgrad")
+    B, C, H, W = y.shape
+    if C != 3 or dy.shape != y.shape or wd.shape != (9, 3, 64):
+        raise ValueError("out3_dgrad: dy, y [B][3][H][W], wd [9][3][64]")
+    dx = torch.empty(B, H, W, 64, device=y.device, dtype=torch.float32)
+    _call("mhada_out3_dgrad", y, dy.data_ptr(), y.data_ptr(), wd.data_ptr(), dx.data_ptr(), B, H, W)
+    return dx
+
+
+def out3_wgrad(x: torch.Tensor, dy: torch.Tensor, y: torch.Tensor, bias: bool = True):
+    """``mhada_out3_wgrad``: (dw [3][64][3][3], db [3] or None) of the same layer from its input x
+    NHWC [B][H][W][64], dy and y NCHW [B][3][H][W]."""
+    _need_gpu(x, dy, y)
+    _f32_contig(x, dy, y, what="out3_wgrad")
+    B, H, W, C = x.shape
+    if C != 64 or y.shape != (B, 3, H, W) or dy.shape != y.shape:
+        raise ValueError("out3_wgrad: x [B][H][W][64], dy, y [B][3][H][W]")
+    lib = _lib.load()
+    n = lib.mhada_out3_wgrad_work(B, H, W)
+    if n <= 0:
+        raise ValueError("out3_wgrad: bad shape")
+    work = torch.empty(n, device=x.device, dtype=torch.float32)
+    dw = torch.empty(3, 64, 3, 3, device=x.device, dtype=torch.float32)
+    db = torch.empty(3, device=x.device, dtype=torch.float32) if bias else None
+    _call("mhada_out3_wgrad", x, x.data_ptr(), dy.data_ptr(), y.data_ptr(), dw.data_ptr(), _ptr(db),
+          work.data_ptr(), n, B, H, W)
+    return dw, db
+
+
 def rows_normalize(x: torch.Tensor, mu: torch.Tensor, rs: torch.Tensor, unit: bool = False) -> torch.Tensor:
     """``mhada_rows_normalize``: (x - mu) * rs on token rows [B][N][C] (and / |row| if unit)."""
     _need_gpu(x, mu, rs)

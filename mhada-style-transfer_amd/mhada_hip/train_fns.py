@@ -465,6 +465,86 @@ def feature_loss_terms(x, ref_mean=None, ref_std=None, t=None):
     return FeatureLossFn.apply(x, ref_mean, ref_std, t)
 
 
+def _cached_build(weight: torch.Tensor, key: tuple, build) -> torch.Tensor:
+    """A derived layout of a frozen weight, cached like _cached; built per call when trainable."""
+    if weight.requires_grad:
+        return build()
+    cache = _pack_slot(weight)
+    hit = cache.get(key)
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    w = build()
+    cache[key] = (weight._version, w)
+    return w
+
+
+class Out3Fn(torch.autograd.Function):
+    """The decoder's last layer (conv.py:94, ConvReLU(64, 3): ReflectionPad2d(1) -> Conv2d(64, 3, 3)
+    -> ReLU) from NHWC x [B][H][W][64] straight to the NCHW image [B][3][H][W]: forward on
+    mhada_conv3x3_out3 (the inference kernel), backward on mhada_out3_dgrad (ReLU, transposed conv
+    and reflection-pad adjoints in one pass) and mhada_out3_wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        wf = weight.detach().permute(2, 3, 1, 0).float().contiguous()  # [tap][ci][co]
+        y = ops.conv3x3_out3(x, wf, bias.detach().float().contiguous())
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            wd = weight.detach().permute(2, 3, 0, 1).reshape(9, 3, 64).float().contiguous()  # [tap][co][ci]
+            gx = ops.out3_dgrad(gy, y, wd)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dw, db = ops.out3_wgrad(x, gy, y, bias=ctx.needs_input_grad[2])
+            gw = dw if ctx.needs_input_grad[1] else None
+            gb = db
+        return gx, gw, gb
+
+
+def _out3_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dtype == F32 and x.dim() == 4 and x.shape[-1] == 64 and x.shape[1] >= 2
+            and x.shape[2] >= 2 and x.is_contiguous() and tuple(conv.weight.shape) == (3, 64, 3, 3)
+            and conv.bias is not None)
+
+
+class VggStemFn(torch.autograd.Function):
+    """VGG19's input normalisation and first layer (vgg19.py:10-11,25-26: imageNet1k_normalize ->
+    Conv2d(3, 64, 3, padding=1) -> ReLU) with frozen weights: the forward is VggInputFn + the
+    zero-padded conv; the backward is ONE mhada_vgg_stem_dgrad pass (ReLU adjoint, the 64 -> 3
+    transposed conv, the normalisation adjoint) in place of relu_bwd, a 64 -> 32-channel GEMM conv
+    and vgg_input_bwd."""
+
+    @staticmethod
+    def forward(ctx, img, weight, bias):
+        x = ops.vgg_input(img.float().contiguous(), 32)
+        B, H, W, cx = x.shape
+        y = torch.empty(B, H, W, 64, device=x.device, dtype=F32)
+        wf = _cached(weight, "f", cx)
+        ops.conv3x3(x, wf, bias.detach().float().contiguous(), F32, upsample=False, relu=True, pad_mode="zero",
+                    pad=1, out=y, wino_u=_wino(weight, "f", wf, cx))
+        ctx.save_for_backward(weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        weight, y = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        wd = _cached_build(weight, ("stem_d",), lambda: weight.detach()[:, :3].flip(2, 3).permute(2, 3, 0, 1)
+                           .reshape(9, 64, 3).float().contiguous())
+        return ops.vgg_stem_dgrad(gy.contiguous(), y, wd), None, None
+
+
+def _stem_eligible(img: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    return (img.is_cuda and img.dim() == 4 and img.shape[1] == 3 and tuple(conv.weight.shape) == (64, 3, 3, 3)
+            and conv.bias is not None and not conv.weight.requires_grad and not conv.bias.requires_grad)
+
+
 def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True):
     return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu)
 
@@ -482,8 +562,11 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
     """Decoder.forward (conv.py:96-100) on the HIP training kernels; ``order`` lists
     (sequence name, index, upsample-after) as autograd_path.DECODER_ORDER."""
     x = nchw_to_nhwc(x_nchw.float())
-    for seq, idx, up in order:
-        x = conv3x3(x, getattr(dec, seq)[idx].conv.conv, "reflect", relu=True)
+    for i, (seq, idx, up) in enumerate(order):
+        conv = getattr(dec, seq)[idx].conv.conv
+        if i == len(order) - 1 and not up and _out3_eligible(x, conv):
+            return Out3Fn.apply(x, conv.weight, conv.bias)  # conv3.1: 64 -> 3, NCHW out
+        x = conv3x3(x, conv, "reflect", relu=True)
         if up:
             x = Upsample2xFn.apply(x)
     return x.permute(0, 3, 1, 2).contiguous()
@@ -492,13 +575,19 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
 def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, torch.Tensor]:
     """VGG19.forward (vgg19.py:42-70) on the HIP kernels: relu1_1 .. relu5_1 as NCHW views of
     NHWC storage."""
-    x = VggInputFn.apply(img)
+    x = None
     feats = {}
     for s, (a, b) in enumerate(slices, start=1):
         seq = getattr(vgg, f"slice{s}")
         for i in range(a, b):
             if i in convs:
-                x = conv3x3(x, getattr(seq, str(i)), "zero", relu=True)
+                conv = getattr(seq, str(i))
+                if x is None:
+                    if _stem_eligible(img, conv):
+                        x = VggStemFn.apply(img, conv.weight, conv.bias)
+                        continue
+                    x = VggInputFn.apply(img)
+                x = conv3x3(x, conv, "zero", relu=True)
             elif i in pools:
                 x = MaxPool2Fn.apply(x)
             # ReLU modules are fused into the conv epilogue

@@ -85,7 +85,7 @@ def test_compute_dtype_resolution():
 def _header_symbols():
     with open(os.path.join(REPO, "include", "mhada_hip.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mhada_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long long|const char\*)\s+(mhada_\w+)\s*\(", src, re.M)))
 
 
 def test_library_loads_and_exports_every_header_symbol():

@@ -540,3 +540,54 @@ def test_cosine_block_training_linear_form_matches_reference_autograd():
     assert rel(out.cpu(), out_ref) < 1e-5
     for (n, p), (_, pr) in zip(g.named_parameters(), ref.named_parameters()):
         assert rel(p.grad.cpu(), pr.grad) < 1e-4, n
+
+
+# ---- the 3-channel ends of the conv stacks (csrc/rgb_ops.hip) -------------------------------------
+@pytest.mark.parametrize("B,H,W", [(2, 2, 2), (1, 3, 5), (2, 37, 70), (1, 64, 130), (3, 9, 64)])
+def test_out3_fn_vs_fp64(B, H, W):
+    """train_fns.Out3Fn (the decoder's ConvReLU(64, 3), conv.py:94) against aten fp64 autograd:
+    the NCHW output, the input gradient (ReLU, transposed conv and ReflectionPad2d adjoints,
+    including the mirrored border taps at H, W = 2 and 3) and the weight / bias gradients, whose
+    fixed-order reduction gives the same bits on a second call."""
+    x = rnd(B, H, W, 64, seed=21)
+    w = rnd(3, 64, 3, 3, seed=22, scale=24 ** -1)
+    b = rnd(3, seed=23, scale=0.2)
+    gy = rnd(B, 3, H, W, seed=24)
+    xg = x.clone().requires_grad_(True)
+    wg = w.clone().requires_grad_(True)
+    bg = b.clone().requires_grad_(True)
+    y = train_fns.Out3Fn.apply(xg, wg, bg)
+    y.backward(gy)
+    x64 = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True)
+    ref = F.relu(F.conv2d(F.pad(x64, (1, 1, 1, 1), mode="reflect"), w64, b64))
+    ref.backward(gy.double())
+    assert rel(y, ref) < 1e-6
+    assert rel(xg.grad, x64.grad.permute(0, 2, 3, 1)) < 1e-5
+    assert rel(wg.grad, w64.grad) < 1e-5
+    assert rel(bg.grad, b64.grad) < 1e-5
+    dw2, db2 = ops.out3_wgrad(x, gy, y.detach())
+    assert torch.equal(dw2, wg.grad) and torch.equal(db2, bg.grad)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 2, 2), (1, 5, 7), (2, 37, 70), (1, 64, 130), (2, 40, 48)])
+def test_vgg_stem_fn_vs_fp64(B, H, W):
+    """train_fns.VggStemFn (imageNet1k_normalize -> Conv2d(3, 64, 3, padding=1) -> ReLU with frozen
+    weights, vgg19.py:10-11,25-26) against aten fp64 autograd: the NHWC output and the image
+    gradient of mhada_vgg_stem_dgrad (ReLU, zero-padded transposed conv and normalisation
+    adjoints in one pass)."""
+    img = (torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(25)) * 255).to(DEV)
+    w = rnd(64, 3, 3, 3, seed=26, scale=0.2)
+    b = rnd(64, seed=27, scale=0.1)
+    gy = rnd(B, H, W, 64, seed=28)
+    ig = img.clone().requires_grad_(True)
+    y = train_fns.VggStemFn.apply(ig, w, b)
+    y.backward(gy)
+    i64 = img.double().requires_grad_(True)
+    mean = i64.new_tensor([0.485, 0.456, 0.406]).view(-1, 1, 1)
+    std = i64.new_tensor([0.229, 0.224, 0.225]).view(-1, 1, 1)
+    ref = F.relu(F.conv2d((i64 / 255.0 - mean) / std, w.double(), b.double(), padding=1))
+    ref.backward(gy.double().permute(0, 3, 1, 2))
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 1e-5
+    assert rel(ig.grad, i64.grad) < 1e-5
