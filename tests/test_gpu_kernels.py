@@ -438,3 +438,30 @@ def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
         y = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
     ref = _attn_ref(q.float(), kv.float(), fcs, mu, rs, vmu)
     assert rel(y.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("nz,M,N,K", [(3, 1000, 64, 4096), (2, 4096, 64, 96), (1, 333, 37, 64), (4, 77, 3, 32),
+                                      (1, 98304, 64, 64)])
+def test_gemm_n64_ring_kernel(nz, M, N, K):
+    """The fp32 N <= 64 LDS-DMA ring GEMM (the attention backward's dQ = dS K, the per-head 1x1
+    convs): batched strided operands, bias, ReLU and residual epilogues against fp64, and against
+    the register-staged tile it replaces (xknob bit 3)."""
+    a = rnd(nz, M, K + 4, seed=11)[..., :K]  # row stride K + 4 (16-B aligned, not dense)
+    w = rnd(nz, N, K, scale=K ** -0.5, seed=12)
+    b = rnd(N, seed=13)
+    ldc = (N + 3) // 4 * 4
+    r = rnd(nz, M, ldc, seed=14)
+    args = dict(a=a, w=w, M=M, N=N, K=K, compute=torch.float32, lda=K + 4, sa=(M * (K + 4), 0), nb=(nz, 1),
+                ldw=K, sw=(N * K, 0), ldc=ldc, sc=(M * ldc, 0))
+    c = torch.zeros(nz, M, ldc, device=DEV)
+    ops.gemm(c=c, bias=b, **args)
+    ref = a.double() @ w.double().transpose(1, 2) + b.double()
+    assert rel(c[..., :N], ref) < TOL[torch.float32]
+    c2 = torch.zeros_like(c)
+    ops.gemm(c=c2, bias=b, r=r, ldr=ldc, sr=(M * ldc, 0), relu=True, **args)
+    assert rel(c2[..., :N], torch.relu(ref) + r[..., :N].double()) < TOL[torch.float32]
+    for xk in (8, 1, 2, 4):  # the register-staged tile; the other tile / ring-depth instantiations
+        with _lib.tuning(xknob=xk):
+            c3 = torch.zeros_like(c)
+            ops.gemm(c=c3, bias=b, **args)
+        assert rel(c3[..., :N], ref) < TOL[torch.float32], xk

@@ -162,6 +162,32 @@ def conv_suite():
                   + "  ".join(f"{k} {v * 1e3:8.1f} us {fl / v / 1e9:7.1f} TF" for k, v in t.items()))
 
 
+def n64_suite():
+    """fp32 N = 64 GEMMs of the training step: the attention backward's dQ = dS K (24 images x 8
+    heads at 64^2 tokens) and the grouped per-head 1x1 convs (K = 64): the LDS-DMA ring kernel vs
+    the register-staged tile (xknob 8) vs torch.bmm."""
+    dev = "cuda"
+    for nz, M, K, lda in ((192, 4096, 4096, 4096), (8, 98304, 64, 512), (8, 98304, 64, 64)):
+        a = torch.randn(nz, M, lda, device=dev) if lda == K else torch.randn(M, lda, device=dev)
+        w = torch.randn(nz, 64, K, device=dev) / K ** 0.5
+        c = torch.empty(nz, M, 64, device=dev)
+        sa = (M * K, 0) if lda == K else (64, 0)
+        args = dict(a=a, w=w, c=c, M=M, N=64, K=K, compute=torch.float32, lda=lda, sa=sa, nb=(nz, 1), ldw=K,
+                    sw=(64 * K, 0), ldc=64, sc=(M * 64, 0))
+        fns = {"ring": lambda: ops.gemm(**args), "tile": lambda: with_env("MHADA_XKNOB", "8", ops.gemm, **args),
+               "r256x3": lambda: with_env("MHADA_XKNOB", "1", ops.gemm, **args),
+               "r128x4": lambda: with_env("MHADA_XKNOB", "2", ops.gemm, **args),
+               "r64x4": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args)}
+        if lda == K:
+            fns["torch"] = lambda: torch.bmm(a, w.transpose(1, 2))
+        t = bench(fns, rounds=5, iters=3)
+        fl = 2 * nz * M * 64 * K
+        by = 4 * nz * M * (K + 64)
+        print(f"n64 fp32 z={nz} M={M} K={K}: " + "  ".join(f"{k} {v * 1e3:8.1f} us {fl / v / 1e9:6.1f} TF "
+                                                        f"{by / v / 1e6:6.0f} GB/s" for k, v in t.items()))
+        del a
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     torch.manual_seed(0)
@@ -169,6 +195,8 @@ if __name__ == "__main__":
         gemm_suite()
     if what in ("gemmk",):
         gemm_k_suite()
+    if what in ("n64",):
+        n64_suite()
     if what in ("conv", "all"):
         conv_suite()
     if what in ("out3", "conv", "all"):
