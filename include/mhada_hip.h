@@ -296,9 +296,10 @@ int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhad
  * input gradient on the padded grid) -> dx [B][H][W][C]. */
 int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t stream);
 /* MaxPool2d(2, 2) on NHWC (vgg19.py slices, torchvision cfg E) and its backward (the gradient
- * goes to the first maximum of each window in row-major order, as ATen keeps it). */
+ * goes to the first maximum of each window in row-major order, as ATen keeps it).  relu_mask = 1:
+ * x is a ReLU output consumed only by this pool, and the ReLU adjoint (x > 0) is applied too. */
 int mhada_maxpool2(const float* x, float* y, int B, int H, int W, int C, mhada_stream_t stream);
-int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C, int relu_mask,
                        mhada_stream_t stream);
 /* Adjoint of the bilinear x2 upsample (conv.py:71): dy [B][2H][2W][C] -> dx [B][H][W][C]. */
 int mhada_upsample2x_bwd(const float* dy, float* dx, int B, int H, int W, int C, mhada_stream_t stream);

@@ -1163,6 +1163,98 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   }
 }
 
+// ------------------------------------------------------------------------------------
+// fp32 GEMM for N <= 64 columns over long K (the attention backward's dQ = dS K: M = Nc, K = Ns,
+// one problem per (batch, head); the grouped per-head 1x1 convs).  Streaming A is the whole
+// cost: at the fp32 MFMA rate a 128x64 tile consumes 8 B/clk/CU of A, ~5 TB/s chip-wide, so the
+// operands go through a 3-deep LDS-DMA ring (global_load_lds, 16 B per lane; K-tile kt + 2 in
+// flight while kt is multiplied) with ONE barrier per K-tile: the barrier that publishes K-tile
+// kt also proves every wave has left K-tile kt - 1, whose slot the next DMA then refills.
+// 4 waves, wave w owns rows 32w..32w+31 x the 64 columns (2 accumulators); two workgroups per
+// CU (72 KiB each).  Rows are 128 B (32 floats), chunk c of row r at slot c ^ ((r >> 1) & 7)
+// (applied on the source address, as gemm_ppp_kernel: conflict-free ds_read_b128).
+// ------------------------------------------------------------------------------------
+template <int BM, int NS, int BK>
+__global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
+  constexpr int NWV = BM / 32, CH = BK / 4, RPI = 64 / CH;  // 16-B chunks per row, rows per DMA instruction
+  constexpr int AH = BM * BK, WH = 64 * BK, STAGE = AH + WH;
+  constexpr int API = 32 / RPI, WPI = 64 / RPI / NWV;  // A / W staging instructions per wave and K-tile
+  static_assert(WPI >= 1 && (CH == 8 || CH == 16), "tile config");
+  __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, z1 = z / p.nb2, z2 = z - z1 * p.nb2;
+  const int m0 = xcd_remap(blockIdx.x, p.ntiles) * BM;
+  const float* ab = reinterpret_cast<const float*>(p.a) + z1 * p.sa1 + z2 * p.sa2;
+  const float* wb = reinterpret_cast<const float*>(p.w) + z1 * p.sw1 + z2 * p.sw2;
+  // chunk c of LDS row r sits at slot c ^ sw(r): conflict-free ds_read_b128 fragment reads
+  auto sw = [](int r) { return CH == 8 ? (r >> 1) & 7 : r & 15; };
+  // staging: one DMA instruction = RPI rows x 128 B (lane -> row lane / CH, slot lane % CH)
+  const float* asrc[API];
+  const float* wsrc[WPI];
+#pragma unroll
+  for (int i = 0; i < API; ++i) {
+    const int r = 32 * wave + RPI * i + lane / CH;
+    const int m = min(m0 + r, p.M - 1);
+    asrc[i] = ab + (long long)m * p.lda + 4 * ((lane % CH) ^ sw(r));
+  }
+#pragma unroll
+  for (int i = 0; i < WPI; ++i) {
+    const int r = RPI * (WPI * wave + i) + lane / CH;
+    const int n = min(r, p.N - 1);
+    wsrc[i] = wb + (long long)n * p.ldw + 4 * ((lane % CH) ^ sw(r));
+  }
+  auto stage = [&](int kt, int slot) {
+    float* dst = smem + slot * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < API; ++i) glds16(asrc[i] + k0, dst + (32 * wave + RPI * i) * BK);
+#pragma unroll
+    for (int i = 0; i < WPI; ++i) glds16(wsrc[i] + k0, dst + AH + RPI * (WPI * wave + i) * BK);
+  };
+  const int h = lane >> 5, r32 = lane & 31;
+  // lane half h supplies k = (BK / 2) h + s at MFMA step s: chunks (CH / 2) h + q of its row
+  int koff[CH / 2];
+#pragma unroll
+  for (int q = 0; q < CH / 2; ++q) koff[q] = 4 * (((CH / 2) * h + q) ^ sw(r32));
+  f32x16 acc[1][2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[0][n][e] = 0.f;
+  const int KT = p.K / BK;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < KT) stage(i, i);
+  for (int kt = 0; kt < KT; ++kt) {
+    // own DMA of K-tile kt done: the K-tiles issued after it (kt + 1 .. kt + NS - 2) may be in flight
+    const int ahead = min(KT - 1 - kt, NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * (API + WPI)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(API + WPI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // a bare s_barrier: __syncthreads() would also drain the DMA of the K-tiles ahead (vmcnt(0))
+    PP_BARRIER();
+    if (kt + NS - 1 < KT) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    const float* sa = smem + (kt % NS) * STAGE + (32 * wave + r32) * BK;
+    const float* swp = smem + (kt % NS) * STAGE + AH + r32 * BK;
+    f32x4 af[CH / 2], wf[2][CH / 2];
+#pragma unroll
+    for (int q = 0; q < CH / 2; ++q) af[q] = *reinterpret_cast<const f32x4*>(sa + koff[q]);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int q = 0; q < CH / 2; ++q) wf[n][q] = *reinterpret_cast<const f32x4*>(swp + n * 32 * BK + koff[q]);
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[0][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[n][s >> 2][s & 3], af[s >> 2][s & 3], acc[0][n], 0, 0, 0);
+  }
+  store_tile<float, 1, 2>(p, acc, z1, z2, m0 + 32 * wave + r32, 0, h);
+}
+
+static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
 static int num_cus() {
   static int n = 0;
   if (!n) {
@@ -1256,6 +1348,32 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (tuning gemm_n64 = 256
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
   if (p.N <= 64) {
+    if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 && AMODE == MHADA_A_ROWS) {
+      // fp32 rows, K % 32: the LDS-DMA ring kernel (xknob bit 3 = the register-staged tile, A/B)
+      if (p.K % 32 == 0 && p.lda % 4 == 0 && p.ldw % 4 == 0 && p.sa1 % 4 == 0 && p.sa2 % 4 == 0 &&
+          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w) && !(tuning().xknob & 8)) {
+        GemmP q = p;
+        q.tiles_n = 1;
+        // long K (the dQ GEMM, K = Ns): 256 x 64 tiles of 256-B K-tiles, two stages (160 KiB);
+        // short K (the grouped 1x1 convs, K = 64): 128 x 64 tiles, 3 stages of 128-B K-tiles
+        // (profiles/r03_opbench_n64.log); xknob 1 / 2 / 4 select the others for A/B runs
+        const int xk = tuning().xknob & 7;
+        if ((xk == 1 || (xk == 0 && p.K >= 1024)) && p.K % 64 == 0) {
+          q.ntiles = (p.M + 255) / 256;
+          hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
+        } else if (xk == 2 && p.K % 64 == 0) {
+          q.ntiles = (p.M + 127) / 128;
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 3, 64>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+        } else if (xk == 4 && p.K % 64 == 0) {
+          q.ntiles = (p.M + 127) / 128;
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 64>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+        } else {
+          q.ntiles = (p.M + 127) / 128;
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 3, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+        }
+        return check_launch("mhada_gemm");
+      }
+    }
     if (tuning().gemm_n64 == 256) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
   }
@@ -1305,7 +1423,6 @@ static int dispatch_mode(int mode, const GemmP& p, int nz, hipStream_t s) {
   return fail("mhada_gemm: bad a_mode");
 }
 
-static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 
 // per-dtype dispatch entry points (gemm_d_*.hip)

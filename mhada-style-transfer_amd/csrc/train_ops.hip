@@ -832,8 +832,11 @@ __global__ void __launch_bounds__(256) maxpool2_kernel(const float* __restrict__
 // one thread per output window x 4 channels: the whole window's dX (4 positions) is written,
 // the gradient to the first maximum in the scan order (0,0), (0,1), (1,0), (1,1); rows / columns
 // beyond 2*Ho, 2*Wo (odd sizes) are zeroed by the caller
+// relu_mask: x is a ReLU output whose only consumer is this pool, so the ReLU adjoint (x > 0)
+// is applied here and the producing conv's backward skips mhada_relu_bwd (one fewer pass)
 __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                           float* __restrict__ dx, int B, int H, int W, int C) {
+                                                           float* __restrict__ dx, int B, int H, int W, int C,
+                                                           int relu_mask) {
   const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
   if (q >= (long long)B * Ho * Wo * C4) return;
@@ -861,7 +864,7 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const float* __restri
         arg = j;
       }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) out[j][e] = j == arg ? g[e] : 0.f;
+    for (int j = 0; j < 4; ++j) out[j][e] = (j == arg && (!relu_mask || v[j][e] > 0.f)) ? g[e] : 0.f;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(dx + offs[j]) = out[j];
@@ -1269,12 +1272,12 @@ extern "C" int mhada_maxpool2(const float* x, float* y, int B, int H, int W, int
 }
 
 extern "C" int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
-                                  mhada_stream_t s_) {
+                                  int relu_mask, mhada_stream_t s_) {
   if (!x || !dy || !dx || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(x) || !al16(dy) || !al16(dx))
     return fail("mhada_maxpool2_bwd: bad args");
   if (H % 2 || W % 2) (void)hipMemsetAsync(dx, 0, (size_t)B * H * W * C * sizeof(float), (hipStream_t)s_);
   hipLaunchKernelGGL(maxpool2_bwd_kernel, grid1((long long)B * (H / 2) * (W / 2) * (C / 4)), dim3(256), 0,
-                     (hipStream_t)s_, x, dy, dx, B, H, W, C);
+                     (hipStream_t)s_, x, dy, dx, B, H, W, C, relu_mask);
   return check_launch("mhada_maxpool2_bwd");
 }
 

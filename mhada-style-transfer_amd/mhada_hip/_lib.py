@@ -91,7 +91,7 @@ SIGNATURES = {
     "mhada_feat_loss_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _F, _vp, _I, _c_ll, _I, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
-    "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_upsample2x_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),

@@ -662,11 +662,12 @@ def maxpool2(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor, relu_mask: bool = False) -> torch.Tensor:
+    """MaxPool2d(2, 2) adjoint; relu_mask also applies the ReLU adjoint (x > 0) of a ReLU output x."""
     _need_gpu(x, dy)
     B, H, W, C = x.shape
     dx = torch.empty_like(x)
-    _call("mhada_maxpool2_bwd", x, x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C)
+    _call("mhada_maxpool2_bwd", x, x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask))
     return dx
 
 

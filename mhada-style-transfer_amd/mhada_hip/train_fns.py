@@ -104,7 +104,8 @@ def _wino(weight: torch.Tensor, kind: str, packed: torch.Tensor, *dims) -> Optio
 
 class Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pad_mode: str, relu: bool):
+    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pad_mode: str, relu: bool,
+                grad_masked: bool = False):
         if x.dtype != F32 or not x.is_contiguous():
             raise ValueError("conv3x3 (training) takes contiguous fp32 NHWC activations")
         B, H, W, cx = x.shape
@@ -117,7 +118,9 @@ class Conv3x3Fn(torch.autograd.Function):
         ops.conv3x3(x, wf, bias.detach().float().contiguous(), F32, upsample=False,
                     relu=relu, pad_mode=pad_mode, pad=1, out=y, wino_u=_wino(weight, "f", wf, cx))
         ctx.save_for_backward(x, weight, y)
-        ctx.pad_mode, ctx.relu = pad_mode, relu
+        # grad_masked: the output's only consumer (MaxPool2Fn(relu_input=True)) hands back the
+        # gradient with the ReLU adjoint already applied
+        ctx.pad_mode, ctx.relu, ctx.grad_masked = pad_mode, relu, grad_masked
         return y if ldc == co else y[..., :co].contiguous()
 
     @staticmethod
@@ -129,7 +132,7 @@ class Conv3x3Fn(torch.autograd.Function):
         gy = gy.contiguous()
         if ldc != co:
             gy = F.pad(gy, (0, ldc - co))
-        g = ops.relu_bwd(gy, y) if ctx.relu else gy
+        g = ops.relu_bwd(gy, y) if ctx.relu and not ctx.grad_masked else gy
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             cg = _ceil(co, 32)
@@ -159,7 +162,7 @@ class Conv3x3Fn(torch.autograd.Function):
                 gb = cs[:co].contiguous()
         elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)[:co].contiguous()
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None
 
 
 class LinearFn(torch.autograd.Function):
@@ -375,15 +378,19 @@ class PatchEmbedFn(torch.autograd.Function):
 
 
 class MaxPool2Fn(torch.autograd.Function):
+    """MaxPool2d(2, 2) on NHWC.  relu_input: x is a ReLU output consumed only by this pool, so the
+    backward also applies the ReLU adjoint and the producing Conv3x3Fn (grad_masked=True) skips it."""
+
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, relu_input: bool = False):
         ctx.save_for_backward(x)
+        ctx.relu_input = relu_input
         return ops.maxpool2(x)
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
-        return ops.maxpool2_bwd(x, gy.contiguous())
+        return ops.maxpool2_bwd(x, gy.contiguous(), ctx.relu_input), None
 
 
 class Upsample2xFn(torch.autograd.Function):
@@ -545,8 +552,8 @@ def _stem_eligible(img: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.bias is not None and not conv.weight.requires_grad and not conv.bias.requires_grad)
 
 
-def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True):
-    return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu)
+def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True, grad_masked: bool = False):
+    return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu, grad_masked)
 
 
 def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
@@ -576,6 +583,7 @@ def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, tor
     """VGG19.forward (vgg19.py:42-70) on the HIP kernels: relu1_1 .. relu5_1 as NCHW views of
     NHWC storage."""
     x = None
+    relu_to_pool = False
     feats = {}
     for s, (a, b) in enumerate(slices, start=1):
         seq = getattr(vgg, f"slice{s}")
@@ -587,9 +595,14 @@ def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, tor
                         x = VggStemFn.apply(img, conv.weight, conv.bias)
                         continue
                     x = VggInputFn.apply(img)
-                x = conv3x3(x, conv, "zero", relu=True)
+                # a conv whose ReLU output feeds only the next pool (vgg19 cfg E: conv1_2, conv2_2,
+                # conv3_4, conv4_4) leaves its ReLU adjoint to the pool's backward
+                pooled = (i + 2) in pools and i + 2 < b
+                x = conv3x3(x, conv, "zero", relu=True, grad_masked=pooled)
+                relu_to_pool = pooled
             elif i in pools:
-                x = MaxPool2Fn.apply(x)
+                x = MaxPool2Fn.apply(x, relu_to_pool)
+                relu_to_pool = False
             # ReLU modules are fused into the conv epilogue
         feats[f"relu{s}_1"] = nhwc_to_nchw(x)
     return feats

@@ -127,6 +127,19 @@ def test_maxpool2_fwd_bwd_with_ties():
     assert torch.equal(xg.grad, xr.grad.permute(0, 2, 3, 1))
 
 
+def test_maxpool2_bwd_with_relu_mask_equals_relu_adjoint_after_pool_adjoint():
+    """MaxPool2Fn(relu_input=True): the pool adjoint with the producing ReLU's adjoint applied
+    (bits of relu_bwd(maxpool2_bwd(g), x)), odd sizes included."""
+    for H, W in ((16, 18), (7, 9)):
+        x = F.relu(rnd(2, H, W, 64, seed=31))
+        gy = rnd(2, H // 2, W // 2, 64, seed=32)
+        ref = ops.relu_bwd(ops.maxpool2_bwd(x, gy), x)
+        assert torch.equal(ops.maxpool2_bwd(x, gy, relu_mask=True), ref)
+        xg = x.clone().requires_grad_(True)
+        train_fns.MaxPool2Fn.apply(xg, True).backward(gy)
+        assert torch.equal(xg.grad, ref)
+
+
 @pytest.mark.parametrize("H,W", [(8, 8), (5, 7), (1, 3), (64, 32)])
 def test_upsample2x_adjoint(H, W):
     x = rnd(2, H, W, 64, seed=7)
