@@ -1090,8 +1090,11 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   // call sites below bind s1 / s2 to `cur` or `nxt` at compile time: selecting the struct by a
   // runtime condition made hipcc copy the whole staging state every iteration (~280 v_mov + 50-100
   // v_readlane per K-tile in the last two K-tiles of each tile).
-  auto ktile = [&](const St& s1, const int k1, const bool w1, const St& s2, const int k2, const bool a2)
-      __attribute__((always_inline)) {
+  // wx: the wait of this K-tile may leave EPI_MIN more operations in flight — the previous tile's
+  // epilogue stores, issued after everything this wait must cover (see the tile boundary below)
+  constexpr int EPI_MIN = (sizeof(TO) == 4 && TN == 2) ? 32 : 16;
+  auto ktile = [&](const St& s1, const int k1, const bool w1, const St& s2, const int k2, const bool a2,
+                   const bool wx) __attribute__((always_inline)) {
     const int cb = sl0;
     if constexpr (TN == 2) {
       // phase 0
@@ -1117,7 +1120,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     }
     if (a2) {
       stage_a(s2, 0, k2, sl2); stage_a(s2, 1, k2, sl2);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (wx) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + EPI_MIN) : "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1129,13 +1133,28 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       sl0 = sl1; sl1 = sl2; sl2 = o;
     }
   };
+  bool pre = false;  // W of this tile's K-tile 1 was staged before the previous tile's epilogue
   while (true) {
-    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, true, cur, kt + 2, true);
-    ktile(cur, KT - 1, true, nxt, 0, has_nxt);  // KT >= 2 (checked on the host)
-    ktile(nxt, 0, has_nxt, nxt, 1, has_nxt);
+    // KT >= 2 (checked on the host); the first K-tile skips the pre-staged W and may leave the
+    // previous epilogue's stores in flight (wx)
+    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, kt > 0 || !pre, cur, kt + 2, true, kt == 0 && pre);
+    ktile(cur, KT - 1, KT > 2 || !pre, nxt, 0, has_nxt, KT == 2 && pre);
+    ktile(nxt, 0, has_nxt, nxt, 1, has_nxt, false);
     // tile boundary: re-align the groups so both store in the same interval (a store between
     // staggered barriers would hold the other group's compute phase), then re-stagger
     if (grp == 0) PP_BARRIER();
+    // Every wave has left the last K-tile, so the ring slot of the next tile's K-tile 1 is free:
+    // stage its W now, BEFORE the epilogue stores.  vmcnt is in order and counts stores, so the
+    // next tile's first wait would otherwise drain this tile's whole C burst (~7 % of an fp32
+    // 512-K GEMM); with everything that wait needs issued before the stores, it may leave them
+    // in flight (at least EPI_MIN per wave in a full tile).  Not with rinit: the next tile's
+    // residual loads follow the stores and its first MFMA needs them.
+    pre = has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
+    if (pre) {
+      stage_w(nxt, 0, 1, sl1);
+      if constexpr (NWH == 2) stage_w(nxt, 1, 1, sl1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (SCR > 0) {
       if (p.lds_epi) {
         float* scr = reinterpret_cast<float*>(smem + NSLOT * TILE) + wave * 1024;

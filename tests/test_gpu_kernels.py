@@ -36,7 +36,10 @@ def test_library_is_the_native_one():
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(100, 96, 64), (1024, 1536, 512), (333, 512, 2048), (4096, 64, 64), (17, 2048, 512),
                                    (32400, 512, 2048), (32400, 512, 512),
-                                   (1000, 384, 576), (8192, 512, 64), (2000, 128, 512), (700, 100, 256)])
+                                   (1000, 384, 576), (8192, 512, 64), (2000, 128, 512), (700, 100, 256),
+                                   # several persistent tiles per CU (the next tile's W staged before the
+                                   # epilogue stores), K = 2 K-tiles included, a partial last row tile
+                                   (70000, 1024, 64), (70000, 1024, 128), (70000, 768, 512)])
 def test_linear(cdt, M, N, K):
     x = rnd(M, K, seed=1, dtype=cdt)
     w = rnd(N, K, scale=K ** -0.5, seed=2, dtype=cdt)
