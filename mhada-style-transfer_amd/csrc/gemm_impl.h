@@ -1137,8 +1137,13 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   while (true) {
     // KT >= 2 (checked on the host); the first K-tile skips the pre-staged W and may leave the
     // previous epilogue's stores in flight (wx)
-    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, kt > 0 || !pre, cur, kt + 2, true, kt == 0 && pre);
-    ktile(cur, KT - 1, KT > 2 || !pre, nxt, 0, has_nxt, KT == 2 && pre);
+    if constexpr (AMODE == MHADA_A_ROWS) {
+      for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, kt > 0 || !pre, cur, kt + 2, true, kt == 0 && pre);
+      ktile(cur, KT - 1, KT > 2 || !pre, nxt, 0, has_nxt, KT == 2 && pre);
+    } else {
+      for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, true, cur, kt + 2, true, false);
+      ktile(cur, KT - 1, true, nxt, 0, has_nxt, false);
+    }
     ktile(nxt, 0, has_nxt, nxt, 1, has_nxt, false);
     // tile boundary: re-align the groups so both store in the same interval (a store between
     // staggered barriers would hold the other group's compute phase), then re-stagger
@@ -1149,7 +1154,9 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     // 512-K GEMM); with everything that wait needs issued before the stores, it may leave them
     // in flight (at least EPI_MIN per wave in a full tile).  Not with rinit: the next tile's
     // residual loads follow the stores and its first MFMA needs them.
-    pre = has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
+    // (ROWS only: in the implicit-GEMM conv instantiations the extra specialisation of the first
+    // K-tile raised register spills and measured slower)
+    pre = AMODE == MHADA_A_ROWS && has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
     if (pre) {
       stage_w(nxt, 0, 1, sl1);
       if constexpr (NWH == 2) stage_w(nxt, 1, 1, sl1);
