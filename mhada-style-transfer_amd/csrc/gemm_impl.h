@@ -1381,21 +1381,25 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
         GemmP q = p;
         q.tiles_n = 1;
         // long K (the dQ GEMM, K = Ns): 256 x 64 tiles of 256-B K-tiles, two stages (160 KiB);
-        // short K (the grouped 1x1 convs, K = 64): 128 x 64 tiles, 3 stages of 128-B K-tiles
-        // (profiles/r03_opbench_n64.log); xknob 1 / 2 / 4 select the others for A/B runs
+        // short K (the grouped 1x1 convs, K = 64): 128 x 64 tiles, 2 stages of 128-B K-tiles (48 KiB,
+        // three workgroups per CU; profiles/r03_opbench_n64*.log); xknob 1 / 2 / 4 select the
+        // 3-stage ring and 64-row tiles (A/B runs)
         const int xk = tuning().xknob & 7;
-        if ((xk == 1 || (xk == 0 && p.K >= 1024)) && p.K % 64 == 0) {
+        if (p.K >= 1024 && p.K % 64 == 0 && xk == 0) {
           q.ntiles = (p.M + 255) / 256;
           hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
-        } else if (xk == 2 && p.K % 64 == 0) {
-          q.ntiles = (p.M + 127) / 128;
-          hipLaunchKernelGGL((gemm_n64_kernel<128, 3, 64>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
-        } else if (xk == 4 && p.K % 64 == 0) {
-          q.ntiles = (p.M + 127) / 128;
-          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 64>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
-        } else {
+        } else if (xk == 1) {
           q.ntiles = (p.M + 127) / 128;
           hipLaunchKernelGGL((gemm_n64_kernel<128, 3, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+        } else if (xk == 2) {
+          q.ntiles = (p.M + 63) / 64;
+          hipLaunchKernelGGL((gemm_n64_kernel<64, 3, 32>), dim3(q.ntiles, nz), dim3(128), 0, s, q);
+        } else if (xk == 4) {
+          q.ntiles = (p.M + 63) / 64;
+          hipLaunchKernelGGL((gemm_n64_kernel<64, 2, 32>), dim3(q.ntiles, nz), dim3(128), 0, s, q);
+        } else {
+          q.ntiles = (p.M + 127) / 128;
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
         }
         return check_launch("mhada_gemm");
       }

@@ -175,9 +175,9 @@ def n64_suite():
         args = dict(a=a, w=w, c=c, M=M, N=64, K=K, compute=torch.float32, lda=lda, sa=sa, nb=(nz, 1), ldw=K,
                     sw=(64 * K, 0), ldc=64, sc=(M * 64, 0))
         fns = {"default": lambda: ops.gemm(**args), "tile": lambda: with_env("MHADA_XKNOB", "8", ops.gemm, **args),
-               "r256x2k64": lambda: with_env("MHADA_XKNOB", "1", ops.gemm, **args),
-               "r128x3k64": lambda: with_env("MHADA_XKNOB", "2", ops.gemm, **args),
-               "r128x2k64": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args)}
+               "r128x3": lambda: with_env("MHADA_XKNOB", "1", ops.gemm, **args),
+               "r64x3": lambda: with_env("MHADA_XKNOB", "2", ops.gemm, **args),
+               "r64x2": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args)}
         if lda == K:
             fns["torch"] = lambda: torch.bmm(a, w.transpose(1, 2))
         t = bench(fns, rounds=5, iters=3)
