@@ -1209,8 +1209,20 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, z1 = z / p.nb2, z2 = z - z1 * p.nb2;
-  const int m0 = xcd_remap(blockIdx.x, p.ntiles) * BM;
+  // Workgroups are dealt to the 8 XCDs round-robin in launch order.  With p.xcd_z (batch count a
+  // multiple of 8) all row tiles of one problem z go to ONE XCD, so its W (the dQ GEMM's K^T,
+  // 1 MiB per (batch, head)) is fetched into one L2 instead of eight.
+  int z, tile;
+  if (p.lds_epi == 4) {
+    const int L = blockIdx.y * gridDim.x + blockIdx.x, nt = gridDim.x;
+    z = L % 8 + 8 * (L / (8 * nt));
+    tile = (L / 8) % nt;
+  } else {
+    z = blockIdx.y;
+    tile = xcd_remap(blockIdx.x, p.ntiles);
+  }
+  const int z1 = z / p.nb2, z2 = z - z1 * p.nb2;
+  const int m0 = tile * BM;
   const float* ab = reinterpret_cast<const float*>(p.a) + z1 * p.sa1 + z2 * p.sa2;
   const float* wb = reinterpret_cast<const float*>(p.w) + z1 * p.sw1 + z2 * p.sw2;
   // chunk c of LDS row r sits at slot c ^ sw(r): conflict-free ds_read_b128 fragment reads
@@ -1380,6 +1392,9 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
           p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w) && !(tuning().xknob & 8)) {
         GemmP q = p;
         q.tiles_n = 1;
+        // lds_epi (unused by this kernel's direct epilogue) = 4 flags the per-XCD grouping of the
+        // problems (xknob 3 = the row-tile remap alone, A/B)
+        q.lds_epi = (nz % 8 == 0 && (tuning().xknob & 7) != 3) ? 4 : 0;
         // long K (the dQ GEMM, K = Ns): 256 x 64 tiles of 256-B K-tiles, two stages (160 KiB);
         // short K (the grouped 1x1 convs, K = 64): 128 x 64 tiles, 2 stages of 128-B K-tiles (48 KiB,
         // three workgroups per CU; profiles/r03_opbench_n64*.log); xknob 1 / 2 / 4 select the

@@ -444,7 +444,7 @@ def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
 
 
 @pytest.mark.parametrize("nz,M,N,K", [(3, 1000, 64, 4096), (2, 4096, 64, 96), (1, 333, 37, 64), (4, 77, 3, 32),
-                                      (1, 98304, 64, 64)])
+                                      (1, 98304, 64, 64), (8, 500, 64, 128), (16, 300, 61, 4096)])
 def test_gemm_n64_ring_kernel(nz, M, N, K):
     """The fp32 N <= 64 LDS-DMA ring GEMM (the attention backward's dQ = dS K, the per-head 1x1
     convs): batched strided operands, bias, ReLU and residual epilogues against fp64, and against
@@ -463,7 +463,7 @@ def test_gemm_n64_ring_kernel(nz, M, N, K):
     c2 = torch.zeros_like(c)
     ops.gemm(c=c2, bias=b, r=r, ldr=ldc, sr=(M * ldc, 0), relu=True, **args)
     assert rel(c2[..., :N], torch.relu(ref) + r[..., :N].double()) < TOL[torch.float32]
-    for xk in (8, 1, 2, 4):  # the register-staged tile; the other tile / ring-depth instantiations
+    for xk in (8, 1, 2, 4, 3):  # the register-staged tile; the other tile / ring instantiations; no XCD grouping
         with _lib.tuning(xknob=xk):
             c3 = torch.zeros_like(c)
             ops.gemm(c=c3, bias=b, **args)

@@ -177,7 +177,8 @@ def n64_suite():
         fns = {"default": lambda: ops.gemm(**args), "tile": lambda: with_env("MHADA_XKNOB", "8", ops.gemm, **args),
                "r128x3": lambda: with_env("MHADA_XKNOB", "1", ops.gemm, **args),
                "r64x3": lambda: with_env("MHADA_XKNOB", "2", ops.gemm, **args),
-               "r64x2": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args)}
+               "r64x2": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args),
+               "no_xcdz": lambda: with_env("MHADA_XKNOB", "3", ops.gemm, **args)}
         if lda == K:
             fns["torch"] = lambda: torch.bmm(a, w.transpose(1, 2))
         t = bench(fns, rounds=5, iters=3)
