@@ -302,7 +302,10 @@ int mhada_maxpool2(const float* x, float* y, int B, int H, int W, int C, mhada_s
 int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C, int relu_mask,
                        mhada_stream_t stream);
 /* Adjoint of the bilinear x2 upsample (conv.py:71): dy [B][2H][2W][C] -> dx [B][H][W][C]. */
-int mhada_upsample2x_bwd(const float* dy, float* dx, int B, int H, int W, int C, mhada_stream_t stream);
+/* relu_x (nullable): the upsample input when it is a ReLU output consumed only by the upsample;
+ * dx is then also multiplied by (x > 0). */
+int mhada_upsample2x_bwd(const float* dy, const float* relu_x, float* dx, int B, int H, int W, int C,
+                         mhada_stream_t stream);
 /* imageNet1k_normalize (vgg19.py:6-12): img [B][3][H][W] fp32 0..255 -> NHWC [B][H][W][Cp]
  * ((x/255 - mean)/std, channels 3..Cp-1 zero), and the adjoint of that map. */
 int mhada_vgg_input(const float* img, float* out, int B, int H, int W, int Cp, mhada_stream_t stream);
@@ -366,9 +369,11 @@ int mhada_vgg_stem_dgrad(const float* dy, const float* y, const float* wd, float
 /* The decoder's last layer (conv.py:39-45,94: ReflectionPad2d(1) -> Conv2d(64, 3, 3) -> ReLU; its
  * forward is mhada_conv3x3_out3): input gradient dx NHWC [B][H][W][64] with the reflection-pad
  * adjoint folded in, from dy and the layer output y (NCHW [B][3][H][W]) and wd [9][3][64] =
- * W[co][ci][tap] (replaces relu_bwd + channel padding + a pad-2 transposed conv + mhada_reflect_fold). */
-int mhada_out3_dgrad(const float* dy, const float* y, const float* wd, float* dx, int B, int H, int W,
-                     mhada_stream_t stream);
+ * W[co][ci][tap] (replaces relu_bwd + channel padding + a pad-2 transposed conv + mhada_reflect_fold).
+ * relu_x (nullable): the layer input x when it is a ReLU output consumed only by this layer — dx is
+ * then also multiplied by (x > 0), the producing layer's ReLU adjoint. */
+int mhada_out3_dgrad(const float* dy, const float* y, const float* wd, const float* relu_x, float* dx, int B, int H,
+                     int W, mhada_stream_t stream);
 /* Its weight gradient dw [3][64][3][3] and bias gradient db [3] (null: skipped) from the layer
  * input x NHWC [B][H][W][64], dy and y as above; per-workgroup partials in work (>= mhada_out3_wgrad_work
  * floats) summed in a fixed order (replaces the M <= 4 mhada_gemm_tn + colsum). */

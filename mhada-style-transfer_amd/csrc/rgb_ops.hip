@@ -119,8 +119,9 @@ __global__ void __launch_bounds__(256) vgg_stem_dgrad_kernel(const float* __rest
 // wave goes out through LDS as whole 1-KiB row slices.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) out3_dgrad_kernel(const float* __restrict__ dy, const float* __restrict__ y,
-                                                         const float* __restrict__ wd, float* __restrict__ dx, int H,
-                                                         int W, int tiles_x, int tiles_y) {
+                                                         const float* __restrict__ wd, const float* __restrict__ relu_x,
+                                                         float* __restrict__ dx, int H, int W, int tiles_x,
+                                                         int tiles_y) {
   constexpr int C = 64, TR = 4, TC = 64, HR = TR + 2, HC = TC + 2, OS = C + 4;
   __shared__ __attribute__((aligned(16))) f32x4 halo[HR * HC];
   __shared__ __attribute__((aligned(16))) float sout[TR][TC * OS];
@@ -188,12 +189,20 @@ __global__ void __launch_bounds__(256) out3_dgrad_kernel(const float* __restrict
     *reinterpret_cast<f32x4*>(so + lane * OS + c) = f32x4{acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
   __syncthreads();
   if (py < H) {
-    float* dst = dx + (((long long)b * H + py) * W + x0) * C;
+    const long long row = (((long long)b * H + py) * W + x0) * C;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int ch = lane + 64 * j, pix = ch >> 4, c4 = ch & 15;
-      if (x0 + pix < W)
-        *reinterpret_cast<f32x4*>(dst + (long long)pix * C + 4 * c4) = *reinterpret_cast<const f32x4*>(so + pix * OS + 4 * c4);
+      if (x0 + pix < W) {
+        const long long o = row + (long long)pix * C + 4 * c4;
+        f32x4 v = *reinterpret_cast<const f32x4*>(so + pix * OS + 4 * c4);
+        if (relu_x) {  // the ReLU adjoint of the layer that produced x (its only consumer is this one)
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(relu_x + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = xv[e] > 0.f ? v[e] : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(dx + o) = v;
+      }
     }
   }
 }
@@ -350,15 +359,15 @@ extern "C" int mhada_vgg_stem_dgrad(const float* dy, const float* y, const float
   return check_launch("mhada_vgg_stem_dgrad");
 }
 
-extern "C" int mhada_out3_dgrad(const float* dy, const float* y, const float* wd, float* dx, int B, int H, int W,
-                                mhada_stream_t s_) {
+extern "C" int mhada_out3_dgrad(const float* dy, const float* y, const float* wd, const float* relu_x, float* dx, int B,
+                                int H, int W, mhada_stream_t s_) {
   if (!dy || !y || !wd || !dx || B <= 0 || H < 2 || W < 2) return fail("mhada_out3_dgrad: bad args (H, W >= 2)");
-  if (!al16(dx)) return fail("mhada_out3_dgrad: dx must be 16-byte aligned");
+  if (!al16(dx) || !al16(relu_x)) return fail("mhada_out3_dgrad: dx / relu_x must be 16-byte aligned");
   const int tiles_x = (W + 63) / 64, tiles_y = (H + 3) / 4;
   const long long nb = (long long)B * tiles_x * tiles_y;
   if (nb >= (1LL << 31)) return fail("mhada_out3_dgrad: grid too large");
-  hipLaunchKernelGGL(out3_dgrad_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)s_, dy, y, wd, dx, H, W, tiles_x,
-                     tiles_y);
+  hipLaunchKernelGGL(out3_dgrad_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)s_, dy, y, wd, relu_x, dx, H, W,
+                     tiles_x, tiles_y);
   return check_launch("mhada_out3_dgrad");
 }
 

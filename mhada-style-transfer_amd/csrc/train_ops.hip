@@ -880,8 +880,10 @@ MHADA_DEV float up2_weight(int o, int i, int n) {
   return (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
 }
 
-__global__ void __launch_bounds__(256) upsample2x_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, int B,
-                                                             int H, int W, int C) {
+// relu_x (nullable): the upsample input when it is a ReLU output consumed only by the upsample —
+// its ReLU adjoint (x > 0) is applied to dx here and the producing conv skips mhada_relu_bwd
+__global__ void __launch_bounds__(256) upsample2x_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ relu_x,
+                                                             float* __restrict__ dx, int B, int H, int W, int C) {
   const int C4 = C / 4;
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
   if (q >= (long long)B * H * W * C4) return;
@@ -903,7 +905,13 @@ __global__ void __launch_bounds__(256) upsample2x_bwd_kernel(const float* __rest
       acc += (wy * wx) * g;
     }
   }
-  *reinterpret_cast<f32x4*>(dx + (((long long)b * H + y) * W + x) * C + 4 * c4) = acc;
+  const long long o = (((long long)b * H + y) * W + x) * C + 4 * c4;
+  if (relu_x) {
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(relu_x + o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = xv[e] > 0.f ? acc[e] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(dx + o) = acc;
 }
 
 __constant__ float c_in_mean[3] = {0.485f, 0.456f, 0.406f};
@@ -1281,11 +1289,12 @@ extern "C" int mhada_maxpool2_bwd(const float* x, const float* dy, float* dx, in
   return check_launch("mhada_maxpool2_bwd");
 }
 
-extern "C" int mhada_upsample2x_bwd(const float* dy, float* dx, int B, int H, int W, int C, mhada_stream_t s_) {
-  if (!dy || !dx || B <= 0 || H <= 0 || W <= 0 || C % 4 || !al16(dy) || !al16(dx))
+extern "C" int mhada_upsample2x_bwd(const float* dy, const float* relu_x, float* dx, int B, int H, int W, int C,
+                                    mhada_stream_t s_) {
+  if (!dy || !dx || B <= 0 || H <= 0 || W <= 0 || C % 4 || !al16(dy) || !al16(dx) || !al16(relu_x))
     return fail("mhada_upsample2x_bwd: bad args");
-  hipLaunchKernelGGL(upsample2x_bwd_kernel, grid1((long long)B * H * W * (C / 4)), dim3(256), 0, (hipStream_t)s_, dy, dx,
-                     B, H, W, C);
+  hipLaunchKernelGGL(upsample2x_bwd_kernel, grid1((long long)B * H * W * (C / 4)), dim3(256), 0, (hipStream_t)s_, dy,
+                     relu_x, dx, B, H, W, C);
   return check_launch("mhada_upsample2x_bwd");
 }
 

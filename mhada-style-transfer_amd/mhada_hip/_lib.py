@@ -92,7 +92,7 @@ SIGNATURES = {
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
-    "mhada_upsample2x_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_upsample2x_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_vgg_input_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_wino_weights": (_I, [_vp, _vp, _I, _I, _vp]),
@@ -100,7 +100,7 @@ SIGNATURES = {
     "mhada_conv3x3_wgrad_wino": (_I, [_vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _I, _I, _I, _c_ll, _I, _vp]),
     "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp]),
     "mhada_vgg_stem_dgrad": (_I, [_vp] * 4 + [_I] * 3 + [_vp]),
-    "mhada_out3_dgrad": (_I, [_vp] * 4 + [_I] * 3 + [_vp]),
+    "mhada_out3_dgrad": (_I, [_vp] * 5 + [_I] * 3 + [_vp]),
     "mhada_out3_wgrad_work": (_c_ll, [_I, _I, _I]),
     "mhada_out3_wgrad": (_I, [_vp] * 6 + [_c_ll, _I, _I, _I, _vp]),
 }

@@ -671,11 +671,15 @@ def maxpool2_bwd(x: torch.Tensor, dy: torch.Tensor, relu_mask: bool = False) -> 
     return dx
 
 
-def upsample2x_bwd(dy: torch.Tensor) -> torch.Tensor:
-    _need_gpu(dy)
+def upsample2x_bwd(dy: torch.Tensor, relu_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Adjoint of the NHWC bilinear x2; with relu_x (the upsample input, a ReLU output) also the
+    producing ReLU's adjoint."""
+    _need_gpu(dy, relu_x)
     B, Ho, Wo, C = dy.shape
     dx = torch.empty(B, Ho // 2, Wo // 2, C, device=dy.device, dtype=torch.float32)
-    _call("mhada_upsample2x_bwd", dy, dy.data_ptr(), dx.data_ptr(), B, Ho // 2, Wo // 2, C)
+    if relu_x is not None and (relu_x.shape != dx.shape or relu_x.dtype != torch.float32 or not relu_x.is_contiguous()):
+        raise ValueError("upsample2x_bwd: relu_x must be the contiguous fp32 upsample input")
+    _call("mhada_upsample2x_bwd", dy, dy.data_ptr(), _ptr(relu_x), dx.data_ptr(), B, Ho // 2, Wo // 2, C)
     return dx
 
 
@@ -714,16 +718,19 @@ def vgg_stem_dgrad(dy: torch.Tensor, y: torch.Tensor, wd: torch.Tensor) -> torch
     return dimg
 
 
-def out3_dgrad(dy: torch.Tensor, y: torch.Tensor, wd: torch.Tensor) -> torch.Tensor:
+def out3_dgrad(dy: torch.Tensor, y: torch.Tensor, wd: torch.Tensor, relu_x: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``mhada_out3_dgrad``: input gradient NHWC [B][H][W][64] of ReflectionPad2d(1) -> conv3x3(64 -> 3)
-    -> ReLU from dy and the output y (NCHW [B][3][H][W]) and wd [9][3][64] (W[co][ci][tap])."""
-    _need_gpu(dy, y, wd)
-    _f32_contig(dy, y, wd, what="out3_dgrad")
+    -> ReLU from dy and the output y (NCHW [B][3][H][W]) and wd [9][3][64] (W[co][ci][tap]); with
+    relu_x (the layer input, a ReLU output) also the producing ReLU's adjoint."""
+    _need_gpu(dy, y, wd, relu_x)
+    _f32_contig(dy, y, wd, *(() if relu_x is None else (relu_x,)), what="out3_dgrad")
     B, C, H, W = y.shape
     if C != 3 or dy.shape != y.shape or wd.shape != (9, 3, 64):
         raise ValueError("out3_dgrad: dy, y [B][3][H][W], wd [9][3][64]")
     dx = torch.empty(B, H, W, 64, device=y.device, dtype=torch.float32)
-    _call("mhada_out3_dgrad", y, dy.data_ptr(), y.data_ptr(), wd.data_ptr(), dx.data_ptr(), B, H, W)
+    if relu_x is not None and relu_x.shape != dx.shape:
+        raise ValueError("out3_dgrad: relu_x must be the [B][H][W][64] layer input")
+    _call("mhada_out3_dgrad", y, dy.data_ptr(), y.data_ptr(), wd.data_ptr(), _ptr(relu_x), dx.data_ptr(), B, H, W)
     return dx
 
 

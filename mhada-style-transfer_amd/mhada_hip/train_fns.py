@@ -394,13 +394,20 @@ class MaxPool2Fn(torch.autograd.Function):
 
 
 class Upsample2xFn(torch.autograd.Function):
+    """Bilinear x2 on NHWC.  relu_input: x is the ReLU output of a Conv3x3Fn(grad_masked=True)
+    consumed only here, and the backward applies that ReLU's adjoint too."""
+
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, relu_input: bool = False):
+        ctx.relu_input = relu_input
+        if relu_input:
+            ctx.save_for_backward(x)
         return ops.upsample2x(x)
 
     @staticmethod
     def backward(ctx, gy):
-        return ops.upsample2x_bwd(gy.contiguous())
+        relu_x = ctx.saved_tensors[0] if ctx.relu_input else None
+        return ops.upsample2x_bwd(gy.contiguous(), relu_x), None
 
 
 class VggInputFn(torch.autograd.Function):
@@ -492,10 +499,13 @@ class Out3Fn(torch.autograd.Function):
     and reflection-pad adjoints in one pass) and mhada_out3_wgrad."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, relu_input: bool = False):
+        # relu_input: x is the ReLU output of a Conv3x3Fn(grad_masked=True) whose only consumer is
+        # this layer, and the input gradient carries that ReLU's adjoint too
         wf = weight.detach().permute(2, 3, 1, 0).float().contiguous()  # [tap][ci][co]
         y = ops.conv3x3_out3(x, wf, bias.detach().float().contiguous())
         ctx.save_for_backward(x, weight, y)
+        ctx.relu_input = relu_input
         return y
 
     @staticmethod
@@ -505,12 +515,12 @@ class Out3Fn(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             wd = weight.detach().permute(2, 3, 0, 1).reshape(9, 3, 64).float().contiguous()  # [tap][co][ci]
-            gx = ops.out3_dgrad(gy, y, wd)
+            gx = ops.out3_dgrad(gy, y, wd, x if ctx.relu_input else None)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             dw, db = ops.out3_wgrad(x, gy, y, bias=ctx.needs_input_grad[2])
             gw = dw if ctx.needs_input_grad[1] else None
             gb = db
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 def _out3_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -569,13 +579,23 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
     """Decoder.forward (conv.py:96-100) on the HIP training kernels; ``order`` lists
     (sequence name, index, upsample-after) as autograd_path.DECODER_ORDER."""
     x = nchw_to_nhwc(x_nchw.float())
+    last = getattr(dec, order[-1][0])[order[-1][1]].conv.conv
+    masked = False
     for i, (seq, idx, up) in enumerate(order):
         conv = getattr(dec, seq)[idx].conv.conv
-        if i == len(order) - 1 and not up and _out3_eligible(x, conv):
-            return Out3Fn.apply(x, conv.weight, conv.bias)  # conv3.1: 64 -> 3, NCHW out
-        x = conv3x3(x, conv, "reflect", relu=True)
+        if i == len(order) - 1 and not up and (masked or _out3_eligible(x, conv)):
+            return Out3Fn.apply(x, conv.weight, conv.bias, masked)  # conv3.1: 64 -> 3, NCHW out
+        if i == len(order) - 1 and masked:
+            raise RuntimeError("decoder_forward: the masked layer's consumer must be Out3Fn")
+        # the layer feeding conv3.1 directly (conv3.0) leaves its ReLU adjoint to Out3Fn's dgrad;
+        # its output (NHWC, 64 channels, same H x W) then meets every _out3_eligible condition
+        masked = (i == len(order) - 2 and not up and not order[-1][2] and conv.weight.shape[0] == 64
+                  and x.is_cuda and x.dtype == F32 and x.shape[1] >= 2 and x.shape[2] >= 2
+                  and tuple(last.weight.shape) == (3, 64, 3, 3) and last.bias is not None)
+        # a layer followed by the bilinear x2 leaves its ReLU adjoint to the upsample's backward
+        x = conv3x3(x, conv, "reflect", relu=True, grad_masked=masked or (up and x.is_cuda))
         if up:
-            x = Upsample2xFn.apply(x)
+            x = Upsample2xFn.apply(x, x.is_cuda)
     return x.permute(0, 3, 1, 2).contiguous()
 
 

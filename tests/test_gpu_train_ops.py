@@ -152,6 +152,10 @@ def test_upsample2x_adjoint(H, W):
     r.backward(gy.double().permute(0, 3, 1, 2))
     assert rel(y, r.permute(0, 2, 3, 1)) < 1e-6
     assert rel(xg.grad, x64.grad.permute(0, 2, 3, 1)) < 1e-6
+    xr = F.relu(x)  # relu_input: the producing ReLU's adjoint folded in, bits of relu_bwd after it
+    xrg = xr.clone().requires_grad_(True)
+    train_fns.Upsample2xFn.apply(xrg, True).backward(gy)
+    assert torch.equal(xrg.grad, ops.relu_bwd(ops.upsample2x_bwd(gy), xr))
 
 
 def test_vgg_input_and_adjoint():
@@ -582,6 +586,10 @@ def test_out3_fn_vs_fp64(B, H, W):
     assert rel(bg.grad, b64.grad) < 1e-5
     dw2, db2 = ops.out3_wgrad(x, gy, y.detach())
     assert torch.equal(dw2, wg.grad) and torch.equal(db2, bg.grad)
+    # relu_input: the producing layer's ReLU adjoint folded into the input gradient
+    wd = w.permute(2, 3, 0, 1).reshape(9, 3, 64).contiguous()
+    xr = F.relu(x)
+    assert torch.equal(ops.out3_dgrad(gy, y.detach(), wd, xr), ops.relu_bwd(ops.out3_dgrad(gy, y.detach(), wd), xr))
 
 
 @pytest.mark.parametrize("B,H,W", [(2, 2, 2), (1, 5, 7), (2, 37, 70), (1, 64, 130), (2, 40, 48)])
