@@ -10,6 +10,11 @@ stylised against a cached 256^2 style + warping error, fp32 and bf16) under "con
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+--gpus N > 1 without a launcher (WORLD_SIZE unset): bench.py starts the N rank processes itself
+(one child per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous) BEFORE
+this process makes any GPU call, relays their output and exits non-zero if any rank fails.
+Under a launcher WORLD_SIZE must equal --gpus.
+
 Multi-GPU: inference replicas: the ViT's batch-axis attention couples the
 images of one forward call, so a call's batch is never split; each rank runs its own batch,
 no collective on the data path (barrier + max-over-ranks timing only) -> scaling "weak".
@@ -42,7 +47,7 @@ def max_over_ranks(x: float, world: int) -> float:
     """The job's time: max over ranks (RCCL on the GPU; gloo when MHADA_BENCH_BACKEND=gloo)."""
     if world == 1:
         return x
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    dev = bench_device() if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -221,32 +226,34 @@ def run_video(dtype, steps, warmup, rank, world):
                        "batch_per_gpu": 1, "compute_dtype": dts, "parallelism": f"replicas x{world}"}}
 
 
-def run_train(steps, warmup, rank, world):
-    """BASELINE configs[3]: train_image.py step at 512^2, 8 images per GPU, DP over RCCL."""
+def run_train(steps, warmup, rank, world, res=512, batch=8):
+    """BASELINE configs[3]: train_image.py step at 512^2, 8 images per GPU, DP over RCCL.
+    (res / batch are smaller only in the CPU rehearsal of the rank protocol, tests/test_bench_cpu.py.)"""
     import network
     from mhada_hip.recipe import load_recipe, seeded_image
     from mhada_hip.train import Trainer
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = bench_device()
     vc = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c").to(dev).train()
     vs = load_recipe(network.VisionTransformer(pos_embedding=False), "vit_s").to(dev).train()
     ada = load_recipe(network.AdaAttnTransformerMultiHead(), "ada").to(dev).train()
     vgg = load_recipe(network.VGG19(), "vgg").to(dev)
     tr = Trainer(vc, vs, ada, vgg)
-    batch = 8
     for i in range(warmup):
-        tr.step(seeded_image(batch, 512, 512, 100 + rank * 1000 + i).to(dev),
-                seeded_image(batch, 512, 512, 500 + rank * 1000 + i).to(dev))
-    data = [(seeded_image(batch, 512, 512, 100 + rank * 1000 + warmup + i).to(dev),
-             seeded_image(batch, 512, 512, 500 + rank * 1000 + warmup + i).to(dev)) for i in range(steps)]
-    torch.cuda.synchronize()
+        tr.step(seeded_image(batch, res, res, 100 + rank * 1000 + i).to(dev),
+                seeded_image(batch, res, res, 500 + rank * 1000 + i).to(dev))
+    data = [(seeded_image(batch, res, res, 100 + rank * 1000 + warmup + i).to(dev),
+             seeded_image(batch, res, res, 500 + rank * 1000 + warmup + i).to(dev)) for i in range(steps)]
+    sync()
     if world > 1:
         dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for c, s in data:
         last = tr.step(c, s)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
+    sync()
     el = time.perf_counter() - t0
     el = max_over_ranks(el, world)
     agree = None
@@ -254,18 +261,19 @@ def run_train(steps, warmup, rank, world):
         agree = rank_agreement([tr.vit_c, tr.vit_s, tr.ada])
         assert agree["identical"], f"DP ranks diverged: {agree}"
     backend = dist.get_backend() if world > 1 else None
-    return {"metric": "train_image.py step throughput at 512x512, 8 images/GPU [configs[3]]",
+    return {"metric": f"train_image.py step throughput at {res}x{res}, {batch} images/GPU [configs[3]]",
             "value": round(batch * steps * world / el, 3), "unit": "images/s", "n_gpus": world, "steps": steps,
             "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic rand*255 images, recipe random-init weights",
             "config": {"workload": "train step (4 ViT + 3 AdaFormer + 5 VGG19 fwd, 4 losses, bwd, Adam)",
-                       "global_batch": batch * world, "resolution": 512,
+                       "global_batch": batch * world, "resolution": res, "device": dev.type,
                        "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} grad all-reduce)"
                                        if world > 1 else "single GPU"),
                        "backend": backend,
-                       "engine": "every conv / linear / attention fwd+bwd on HIP kernels (Winograd fp32 convs, "
-                                 "dS-spill attention backward, TN weight-gradient GEMMs); losses, Adam and glue on "
-                                 "PyTorch-ROCm (DESIGN.md §3b)"},
+                       "engine": ("every conv / linear / attention fwd+bwd on HIP kernels (Winograd fp32 convs, "
+                                  "dS-spill attention backward, TN weight-gradient GEMMs); losses, Adam and glue on "
+                                  "PyTorch-ROCm (DESIGN.md §3b)" if dev.type == "cuda" else
+                                  "CPU rehearsal of the rank protocol: the reference's aten expression")},
             "last_losses": last, "rank_agreement": agree}
 
 
@@ -360,9 +368,68 @@ def cpu_baseline():
                              "note": "oracle/mhada_oracle.py (numpy fp32, same weights), BLAS threads as configured"}}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start ranks 0..n-1 of this same command as child processes (one per GPU) and wait for them.
+    Runs in a parent that has made NO GPU call (so no exec-after-GPU-init anywhere); the children
+    inherit stdout (rank 0 prints the JSON line).  If a rank fails, the others are stopped (by
+    their own PIDs) so a rank blocked in a collective cannot hang the job; returns the first
+    non-zero exit status, else 0."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {r} exited with status {code}; stopping the other ranks", file=sys.stderr)
+                for o in live:
+                    procs[o].terminate()
+                for o in live:
+                    try:
+                        procs[o].wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        procs[o].kill()
+                        procs[o].wait()
+                live.clear()
+        time.sleep(0.2)
+    return rc
+
+
+def bench_device() -> torch.device:
+    """The rank's device: its GPU, or the CPU under --device cpu (the CPU rehearsal of the
+    multi-rank protocol in tests/test_bench_cpu.py; the aten path of the drop-in modules)."""
+    return _DEVICE[0]
+
+
+_DEVICE = [torch.device("cpu")]
+
+
+def sync():
+    if bench_device().type == "cuda":
+        torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without a launcher starts the ranks itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -370,24 +437,41 @@ def main():
     ap.add_argument("--only-secondary", action="store_true", help="run only the 1024^2 bf16 config (profiling)")
     ap.add_argument("--train", action="store_true", help="only BASELINE configs[3]: DP training step at 512^2")
     ap.add_argument("--no-train", action="store_true", help="skip the training config in the default line")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                    help="cpu: rehearse the rank protocol on the CPU (--train only, gloo; tests)")
+    ap.add_argument("--train-res", type=int, default=512, help=argparse.SUPPRESS)
+    ap.add_argument("--train-batch", type=int, default=8, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))  # no GPU call has happened in this process
+    elif args.gpus is not None and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; the modulo only matters when ranks outnumber devices (a 2-rank
-    # rehearsal of the multi-GPU path on a 1-GPU box, with MHADA_BENCH_BACKEND=gloo)
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    backend = os.environ.get("MHADA_BENCH_BACKEND", "nccl" if args.device == "cuda" else "gloo")
+    if args.device == "cpu":
+        if not args.train or backend != "gloo":
+            raise SystemExit("bench.py --device cpu rehearses the DP training protocol only (--train, gloo)")
+    else:
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and world > ndev:
+            raise SystemExit(f"bench.py: {world} RCCL ranks but {ndev} visible GPU(s)")
+        # one process per GPU; the modulo only matters for a gloo rehearsal with more ranks than
+        # devices (MHADA_BENCH_BACKEND=gloo on a 1-GPU box)
+        local = local % max(1, ndev)
+        torch.cuda.set_device(local)
+        _DEVICE[0] = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("MHADA_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
 
     if args.train:
-        r = run_train(args.steps, args.warmup, rank, world)
+        r = run_train(args.steps, args.warmup, rank, world, args.train_res, args.train_batch)
         if rank == 0:
             print(json.dumps(r), flush=True)
         if world > 1:
@@ -404,7 +488,8 @@ def main():
     videos = {} if args.no_secondary else {
         f"video_1080p_s256_{'f32' if dt == torch.float32 else 'bf16'}": run_video(dt, args.steps, args.warmup, rank, world)
         for dt in (torch.float32, torch.bfloat16)}
-    train = None if (args.no_secondary or args.no_train) else run_train(args.steps, args.warmup, rank, world)
+    train = None if (args.no_secondary or args.no_train) else run_train(args.steps, args.warmup, rank, world,
+                                                                         args.train_res, args.train_batch)
 
     if rank == 0:
         line = {

@@ -22,7 +22,7 @@ def global_style_loss(fcs, fs, loss_fn):
     loss = 0
     for i in (1, 2, 3, 4, 5):
         a, b = fcs[f"relu{i}_1"], fs[f"relu{i}_1"]
-        loss = loss + loss_fn(a.mean(dim=(2, 3)), b.mean(dim=(2, 3))) + loss_fn(a.std(dim=(2, 3)), b.std(dim=(2, 3)))
+        loss = loss + (loss_fn(a.mean(dim=(2, 3)), b.mean(dim=(2, 3))) + loss_fn(a.std(dim=(2, 3)), b.std(dim=(2, 3))))
     return loss
 
 

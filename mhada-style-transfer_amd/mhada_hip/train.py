@@ -114,7 +114,7 @@ class Trainer:
             if i >= 3:  # lossfn.py:26-34: the AdaAttN target of the content / style features
                 t = self.no_learn[i - 3](fc[k], fs[k], L.feature_down_sample(fc, i), L.feature_down_sample(fs, i))
             lm, ls, lmse = feature_loss_terms(fcs[k], fs[k].mean(dim=(2, 3)), fs[k].std(dim=(2, 3)), t)
-            gs = gs + lm + ls
+            gs = gs + (lm + ls)  # lossfn.py:21: loss += mean_dist + std_dist
             if t is not None:
                 lf = lf + lmse
             a = feature_loss_terms(fcc[k], t=fc[k])[2]
