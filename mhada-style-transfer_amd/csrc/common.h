@@ -45,7 +45,7 @@ struct Tuning {
   int attn_sched = 3;        // bf16 fixed-shift attention (Ns % 128 == 0): 3 LDS-DMA staging, 5 half-tile
                              // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
-  int xknob = 0;             // scratch knob for A/B experiments (no effect unless a kernel reads it)
+  int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };
 const Tuning& tuning();
 

@@ -360,10 +360,7 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[e] += q[e];
             }
-            if (p.lds_epi == 3)  // A/B: non-temporal stores (xknob bit 2)
-              __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4*>(crow + n));
-            else
-              *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+            *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
             if (p.c2)
               *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 +
                                          (long long)m * p.ldc2 + n) = bf16x4{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
@@ -528,10 +525,7 @@ MHADA_DEV void store_tile_lds_bf16(const GemmP& p, const f32x16 (&acc)[TM][2], i
       if (m >= p.M) continue;
       bf16* crow = cbase + (long long)m * p.ldc;
       if (n + 7 < p.N && ((p.ldc & 7) == 0)) {
-        if (p.lds_epi == 3)  // A/B: non-temporal stores (xknob bit 2)
-          __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&v[i]), reinterpret_cast<f32x4*>(crow + n));
-        else
-          *reinterpret_cast<bf16x8*>(crow + n) = v[i];
+        *reinterpret_cast<bf16x8*>(crow + n) = v[i];
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -1166,10 +1160,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
       if (p.lds_epi) {
         float* scr = reinterpret_cast<float*>(smem + NSLOT * TILE) + wave * 1024;
         if constexpr (sizeof(TO) == 2 && TN == 2) {
-          if (p.lds_epi != 2)
-            store_tile_lds_bf16<4>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
-          else
-            store_tile_lds<TO, 4, TN>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
+          store_tile_lds_bf16<4>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
         } else {
           store_tile_lds<TO, 4, TN>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
         }
@@ -1311,9 +1302,8 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
-  // 1: LDS-staged epilogue (bf16 output: 16-B stores), 2: LDS-staged with the 8-B bf16 stores (A/B
-  // through xknob bit 0), 0: direct stores
-  p.lds_epi = tuning().gemm_ldsepi ? ((tuning().xknob & 1) ? 2 : ((tuning().xknob & 4) ? 3 : 1)) : 0;
+  // 1: LDS-staged epilogue (bf16 output: 16-B stores), 0: direct stores (tuning gemm_ldsepi = 0)
+  p.lds_epi = tuning().gemm_ldsepi ? 1 : 0;
   // residual rows preloaded into the accumulators: fp32 output with a residual, no ReLU (the
   // reference adds the residual after the activation), 16-B aligned rows
   p.rinit = (sizeof(TO) == 4 && p.r && !p.relu && tuning().gemm_rinit && ((uintptr_t)p.r & 15) == 0 &&
@@ -1339,8 +1329,8 @@ template <typename TC, typename TA, typename TO, int AMODE, int BM, int BN, int 
 static int launch_gemm(const GemmP& p0, int nz, hipStream_t stream) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
-  // LDS-staged epilogue (xknob bit 1 = direct stores, A/B); the scratch needs 4 KiB per wave
-  p.lds_epi = (tuning().gemm_ldsepi && !(tuning().xknob & 2) &&
+  // LDS-staged epilogue (tuning gemm_ldsepi = 0: direct stores); the scratch needs 4 KiB per wave
+  p.lds_epi = (tuning().gemm_ldsepi &&
                (size_t)2 * (BM + BN) * Cfg<TC>::LS * sizeof(TC) >= (size_t)WM * WN * 4096) ? 1 : 0;
   const int tiles_m = (p.M + BM - 1) / BM;
   p.ntiles = tiles_m * p.tiles_n;
@@ -1387,31 +1377,21 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
   if (p.N <= 64) {
     if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 && AMODE == MHADA_A_ROWS) {
-      // fp32 rows, K % 32: the LDS-DMA ring kernel (xknob bit 3 = the register-staged tile, A/B)
+      // fp32 rows, K % 32: the LDS-DMA ring kernel
       if (p.K % 32 == 0 && p.lda % 4 == 0 && p.ldw % 4 == 0 && p.sa1 % 4 == 0 && p.sa2 % 4 == 0 &&
-          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w) && !(tuning().xknob & 8)) {
+          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w)) {
         GemmP q = p;
         q.tiles_n = 1;
         // lds_epi (unused by this kernel's direct epilogue) = 4 flags the per-XCD grouping of the
-        // problems (xknob 3 = the row-tile remap alone, A/B)
-        q.lds_epi = (nz % 8 == 0 && (tuning().xknob & 7) != 3) ? 4 : 0;
+        // problems
+        q.lds_epi = nz % 8 == 0 ? 4 : 0;
         // long K (the dQ GEMM, K = Ns): 256 x 64 tiles of 256-B K-tiles, two stages (160 KiB);
         // short K (the grouped 1x1 convs, K = 64): 128 x 64 tiles, 2 stages of 128-B K-tiles (48 KiB,
-        // three workgroups per CU; profiles/r03_opbench_n64*.log); xknob 1 / 2 / 4 select the
-        // 3-stage ring and 64-row tiles (A/B runs)
-        const int xk = tuning().xknob & 7;
-        if (p.K >= 1024 && p.K % 64 == 0 && xk == 0) {
+        // three workgroups per CU; profiles/r03_opbench_n64*.log; 3-stage rings and 64-row tiles
+        // measured no faster)
+        if (p.K >= 1024 && p.K % 64 == 0) {
           q.ntiles = (p.M + 255) / 256;
           hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
-        } else if (xk == 1) {
-          q.ntiles = (p.M + 127) / 128;
-          hipLaunchKernelGGL((gemm_n64_kernel<128, 3, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
-        } else if (xk == 2) {
-          q.ntiles = (p.M + 63) / 64;
-          hipLaunchKernelGGL((gemm_n64_kernel<64, 3, 32>), dim3(q.ntiles, nz), dim3(128), 0, s, q);
-        } else if (xk == 4) {
-          q.ntiles = (p.M + 63) / 64;
-          hipLaunchKernelGGL((gemm_n64_kernel<64, 2, 32>), dim3(q.ntiles, nz), dim3(128), 0, s, q);
         } else {
           q.ntiles = (p.M + 127) / 128;
           hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);

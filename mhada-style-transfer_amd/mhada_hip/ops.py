@@ -451,25 +451,28 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     return out, mo, lse
 
 
-# Largest dS spill (BH * Nc * Ns fp32) the training backward takes (512^2 batch 8: 4.3 GB, reused
-# across the step's attention calls by the caching allocator); larger problems, or spill=False,
-# recompute S and dA in the query-stationary dQ kernel instead.
+# Largest dS spill (BH * Nc * Ns fp32) the training backward takes (512^2 batch 8, the three
+# AdaFormer calls batched: 12.9 GB, reused across the step's attention calls by the caching
+# allocator); larger problems, or spill=False, recompute S and dA in the query-stationary dQ
+# kernel instead.  The choice depends on the shapes and this budget only — never on the device's
+# free memory — so a step's dQ bits are reproducible run to run (the two paths sum dQ in different
+# fp32 orders).  A spill that does not fit raises the allocator's OOM instead of switching paths.
 DS_SPILL_BYTES = 16 << 30
 # Per-(b, h) slice bound of the kernel's 32-bit dS buffer offsets ((Nc + 32) * Ns, attn_train.hip)
 DS_SPILL_MAX_ROWS = 0x7fff0000 // 4
+# Which backward each attn_train_bwd call took ("spill" / "recompute"): tests and tools read it.
+BWD_PATH_COUNTS = {"spill": 0, "recompute": 0}
 
 
-def _device_headroom(dev: torch.device) -> int:
-    """Bytes a new allocation can take without an OOM: free device memory plus what the caching
-    allocator holds reserved but unused (the dS buffer of the previous block is reused from there)."""
-    free, _ = torch.cuda.mem_get_info(dev)
-    return free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+def ds_spill_eligible(BH: int, Nc: int, Ns: int) -> bool:
+    """The shape rule of attn_train_bwd's default path (see DS_SPILL_BYTES)."""
+    return Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS
 
 
 def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
     """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64).  With the dS spill
-    (default when it fits DS_SPILL_BYTES and Ns % 4 == 0): ``mhada_attn_train_dkv`` writes dS and
-    dQ = dS K runs as one batched GEMM (896 instead of 1280 FLOP per query-key-head pair)."""
+    (default when ``ds_spill_eligible``): ``mhada_attn_train_dkv`` writes dS and dQ = dS K runs as
+    one batched GEMM (896 instead of 1280 FLOP per query-key-head pair)."""
     _rows64(q, k, v, lse, dmo, dd)
     BH, Nc, _ = q.shape
     Ns = k.shape[1]
@@ -477,9 +480,8 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
             or v.shape != k.shape:
         raise ValueError("attn_train_bwd: bad shapes")
     if spill is None:
-        need = 4 * BH * Nc * Ns
-        spill = Ns % 4 == 0 and need <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS \
-            and need <= _device_headroom(q.device)
+        spill = ds_spill_eligible(BH, Nc, Ns)
+    BWD_PATH_COUNTS["spill" if spill else "recompute"] += 1
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)

@@ -141,3 +141,16 @@ def test_wino_eligible_respects_32bit_offsets():
     w = torch.empty(64, 9 * 64, dtype=torch.float32, device="meta")
     assert ops.wino_eligible(torch.empty(8, 512, 512, 64, device="meta"), w, False)
     assert not ops.wino_eligible(torch.empty(8, 2048, 2048, 64, device="meta"), w, False)
+
+
+def test_ds_spill_rule_is_shape_only(monkeypatch):
+    """the attention backward's spill / recompute choice never looks at free device
+    memory (that made dQ's bits depend on allocator state)."""
+    from mhada_hip import ops
+
+    def boom(*a, **k):
+        raise AssertionError("the path rule must not query device memory")
+    monkeypatch.setattr(torch.cuda, "mem_get_info", boom)
+    assert ops.ds_spill_eligible(3 * 8 * 8, 4096, 4096)  # 512^2 B8, three AdaFormer calls batched
+    assert not ops.ds_spill_eligible(4, 4096, 4094)       # Ns % 4 != 0
+    assert not ops.ds_spill_eligible(1024, 8192, 8192)    # past DS_SPILL_BYTES

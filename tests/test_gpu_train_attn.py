@@ -95,6 +95,29 @@ def test_attn_train_bwd_ds_spill_matches_recompute(BH, Nc, Ns):
     assert _rel(a[0].double(), b[0].double()) < 1e-5
 
 
+def test_attn_train_bwd_default_path_is_shape_determined(monkeypatch):
+    """the spill / recompute choice depends on shapes and ops.DS_SPILL_BYTES only (not
+    on free memory), is recorded in ops.BWD_PATH_COUNTS, and repeated calls give the same bits."""
+    g = torch.Generator().manual_seed(9)
+    BH, Nc, Ns = 2, 96, 64
+    q, k, v = (torch.randn(BH, n, 64, generator=g).cuda() * 0.5 for n in (Nc, Ns, Ns))
+    v = (v - v.mean(dim=1, keepdim=True)).contiguous()
+    out, mo, lse = ops.attn_train_fwd(q, k, v, torch.randn(BH, Nc, 64, generator=g).cuda())
+    dmo = torch.randn(BH, Nc, 128, generator=g).cuda()
+    dd = (dmo * mo).sum(-1).contiguous()
+    res = {}
+    for budget, path in ((ops.DS_SPILL_BYTES, "spill"), (4 * BH * Nc * Ns - 1, "recompute")):
+        monkeypatch.setattr(ops, "DS_SPILL_BYTES", budget)
+        assert ops.ds_spill_eligible(BH, Nc, Ns) == (path == "spill")
+        before = dict(ops.BWD_PATH_COUNTS)
+        a = ops.attn_train_bwd(q, k, v, lse, dmo, dd)
+        b = ops.attn_train_bwd(q, k, v, lse, dmo, dd)
+        assert ops.BWD_PATH_COUNTS[path] == before[path] + 2
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+        res[path] = a
+    assert torch.equal(res["spill"][1], res["recompute"][1]) and torch.equal(res["spill"][2], res["recompute"][2])
+
+
 def test_attn_train_lse_and_stats():
     g = torch.Generator().manual_seed(5)
     q, x = torch.randn(2, 96, 64, generator=g), torch.randn(2, 96, 64, generator=g)
