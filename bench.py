@@ -4,8 +4,9 @@ A "step" is one full style-transfer forward — vit_c(content), vit_s(style),
 adaFormer(fc, fs) (infer_image.py:83-85 / infer_time.py:74-77) — over one synthetic batch
 already resident in HBM.  Headline workload = BASELINE configs[1]: 512x512, batch 8, fp32.
 The line also carries configs[2] (1024x1024, batch 4, bf16 MFMA path), configs[3] (the
-train_image.py step at 512x512, 8 images per GPU) and configs[4] (1080p u8 video frames ingested,
-stylised against a cached 256^2 style + warping error, fp32 and bf16) under "configs".
+train_image.py step at 512x512, 8 images per GPU), configs[4] (1080p u8 video frames ingested,
+stylised against a cached 256^2 style + warping error, fp32 and bf16) and the reference's own
+latency probe (infer_time.py: B=1 512^2, eager and hipGraph-replayed) under "configs".
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -224,6 +225,53 @@ def run_video(dtype, steps, warmup, rank, world):
             "config": {"workload": "infer_video.py: 1080x1920 u8 BGR frames -> ingest (cv2_to_tensor) -> stylise "
                                    "against a cached 256x256 style, + warping error",
                        "batch_per_gpu": 1, "compute_dtype": dts, "parallelism": f"replicas x{world}"}}
+
+
+def run_infer_time(dtype, warmup, runs=100):
+    """The reference's own latency probe, infer_time.py:64-87: B=1, 512^2 content + style,
+    ``vit_c -> vit_s -> adaFormer -> clamp(0, 255)``, each run bracketed by its own events and a
+    synchronize, averaged over 100 runs (after ``warmup`` untimed runs; the reference times its
+    first run too).  Reported eager (the module calls as the reference makes them) and as one
+    hipGraph replay of the same call (mhada_hip.graphs.GraphedStylizer, bit-identical output);
+    1 - graph / eager = the share of the eager call that is host-side launch overhead / gaps."""
+    from mhada_hip.graphs import GraphedStylizer
+    from mhada_hip.recipe import seeded_image
+    vc, vs, ada = build_models(dtype)
+    dev = bench_device()
+    c = seeded_image(1, 512, 512, 11).to(dev)
+    s = seeded_image(1, 512, 512, 12).to(dev)
+
+    def eager():
+        fc = vc(c)
+        fs = vs(s)
+        _, cs = ada(fc, fs)
+        return cs.clamp(0, 255)
+
+    def probe(fn):
+        with torch.no_grad():
+            for _ in range(warmup):
+                fn()
+            torch.cuda.synchronize()
+            total = 0.0
+            for _ in range(runs):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                out = fn()
+                b.record()
+                torch.cuda.synchronize()
+                total += a.elapsed_time(b)
+        return total / runs, out
+
+    t_eager, ref = probe(eager)
+    ref = ref.clone()
+    g = GraphedStylizer(vc, vs, ada, (1, 3, 512, 512))
+    t_graph, out = probe(lambda: g(c, s))
+    dts = "f32" if dtype == torch.float32 else "bf16"
+    return {"ms_per_frame": round(t_eager, 4), "ms_per_frame_graph": round(t_graph, 4),
+            "launch_gap_share": round(1.0 - t_graph / t_eager, 4), "graph_bit_identical": bool(torch.equal(out, ref)),
+            "runs": runs, "dtype": dts, "unit": "ms/frame",
+            "config": {"workload": "infer_time.py: B=1 512x512 content+style, vit_c -> vit_s -> adaFormer -> clamp, "
+                                   "per-run CUDA-event timing averaged over 100 runs", "batch": 1, "resolution": 512}}
 
 
 def run_train(steps, warmup, rank, world, res=512, batch=8):
@@ -490,6 +538,9 @@ def main():
         for dt in (torch.float32, torch.bfloat16)}
     train = None if (args.no_secondary or args.no_train) else run_train(args.steps, args.warmup, rank, world,
                                                                          args.train_res, args.train_batch)
+    probes = {} if args.no_secondary else {
+        f"infer_time_512_b1_{'f32' if dt == torch.float32 else 'bf16'}": run_infer_time(dt, max(args.warmup, 3))
+        for dt in (torch.float32, torch.bfloat16)}
 
     if rank == 0:
         line = {
@@ -518,6 +569,8 @@ def main():
         if train is not None:
             line.setdefault("configs", {})["train_512_b8_f32"] = {
                 k: train[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "last_losses")}
+        if probes:
+            line.setdefault("configs", {}).update(probes)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

@@ -60,7 +60,7 @@ bool valid(const char* name, int v) {
   if (!strcmp(name, "attn_waves")) return v == 4 || v == 8;
   if (!strcmp(name, "attn_tk")) return v == 64 || v == 128;
   if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
-  if (!strcmp(name, "attn_sched")) return v == 0 || v == 3 || v == 4 || v == 5;
+  if (!strcmp(name, "attn_sched")) return v == 0 || (v >= 3 && v <= 8);
   if (!strcmp(name, "xknob")) return v >= 0 && v < 16;
   return v == 0 || v == 1;
 }

@@ -596,6 +596,28 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 // vmcnt(0) before the one barrier per tile.  Whole key tiles only.  (A second score set for
 // cross-tile pipelining at 128 keys spilled; attn_bf16_fsh_kernel pipelines by half tiles.)
 // --------------------------------------------------------------------------------------
+// In-kernel clock (MI355X_MICROARCH.md, DVFS give-back item 6), diagnostic builds only
+// (-DATTN_CLOCK, tools/attn_clock.py): thread 0 of each workgroup stamps the shader-clock and the
+// 100 MHz real-time counters before and after the key loop into a buffer of their own; no output
+// is computed from them.  In the shipped build ATTN_STAMP expands to nothing.
+#ifdef ATTN_CLOCK
+constexpr int kClockBlocks = 65536;
+__device__ unsigned long long g_attn_clock[4 * kClockBlocks];
+#define ATTN_STAMP(slot)                                                                     \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < kClockBlocks) {                                     \
+      const unsigned long long c_ = __builtin_amdgcn_s_memtime();                           \
+      const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                       \
+      g_attn_clock[4 * blockIdx.x + 2 * (slot)] = c_;                                        \
+      g_attn_clock[4 * blockIdx.x + 2 * (slot) + 1] = r_;                                    \
+    }                                                                                        \
+  } while (0)
+#else
+#define ATTN_STAMP(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 MHADA_DEV void attn_glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -710,6 +732,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
     for (int r = 0; r < 16; ++r) Cm[r] = -m2;
   }
   if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  ATTN_STAMP(0);
   {
     // tile t+1's LDS-DMA into the other slot (last read in iteration t-1, before its barrier)
     // flies during tile t's MFMAs; retired at the end of the iteration
@@ -725,6 +748,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p
       __builtin_amdgcn_s_barrier();
     }
   }
+  ATTN_STAMP(1);
   const float lt = l + __shfl_xor(l, 32, 64);
   if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
@@ -896,11 +920,521 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p
   attn_epilogue<bf16>(p, O, l, b, hh, q, h);
 }
 
+// --------------------------------------------------------------------------------------
+// Fixed-shift LDS-DMA kernel on v_mfma_f32_16x16x32_bf16 ("fsq", tuning attn_sched = 6 / 7): the
+// fsg kernel's loop (same LDS-DMA ring, same fixed shift, same FLOPs and LDS bytes per FLOP) with
+// the 16 x 16 output shape, which the chip runs at a higher sustained clock under load than the
+// 32 x 32 shape at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).
+// Orientation as before (swapped products, the query on the MFMA column):
+//   S^T (16 keys x 16 queries) = K (16 x 32 d) . Q^T (32 d x 16 queries): lane = query r16 of a
+//       16-query group qg, rows 4g..4g+3 (g = lane >> 4); a wave owns 32 queries = 2 groups, and
+//       every K fragment feeds both groups' MFMAs;
+//   O^T (16 dv x 16 queries) += V'^T (16 dv x 32 keys) . P^T (32 keys x 16 queries): B slot 8g+j
+//       is vt position 32kg + 8g + j of the key-permuted vt image = key 32kg + 16(g>>1) +
+//       8(j>>2) + 4(g&1) + (j&3).  The two score tiles t = 0 / 1 of a 32-key group are therefore
+//       computed for keys 32kg + 16(r>>3) + 4((r>>2)&1) + (r&3) + 8t (r = A-operand row): lane
+//       group g then holds exactly its 8 B slots (j < 4 from t = 0, j >= 4 from t = 1) — the
+//       permutation costs only the K row address, no lane movement, no second vt layout.
+// K image: chunk c of key row k at 16-B slot c ^ (k & 7) (conflict-free for these row sets
+// under the ds_read_b128 lane groups of MI355X_MICROARCH.md's LDS table); V'^T as in fsg.
+// ONES (attn_sched = 7): the row sum l comes out of one extra MFMA per (32 keys, 16 queries)
+// with an all-ones A operand (D rows = sum_k P[k][q]), removing the 64 v_add_f32 per tile and
+// lane from the VALU stream at +8 MFMAs (72 instead of 64 PV MFMAs per tile and wave); l is then
+// the sum of the bf16-rounded P that the PV products use.
+// --------------------------------------------------------------------------------------
+MHADA_DEV int fsq_key(int r, int t) { return 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3) + 8 * t; }
+
+// Exact two-pass recompute of one wave's 2 x 16 queries (16x16x32 layout; the rare path when a row
+// sum trips kShiftSumThr): true row max over all keys, then the full pass, operands from L2.
+MHADA_DEV void attn_exact_q(const AttnP& p, const bf16* kvb, const bf16* vtb, const bf16x8 (&qf)[2][2],
+                            f32x4 (&O)[2][8], float (&lt)[2], int g, int r16) {
+  const int Ns = p.Ns;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto scores = [&](int k0, f32x4 (&S)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16* kr = kvb + (long long)(k0 + fsq_key(r16, t)) * 128 + 8 * g;
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) S[qg][t] = z4;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + 32 * dh);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) S[qg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][dh], S[qg][t], 0, 0, 0);
+      }
+    }
+  };
+  float m2[2] = {-INFINITY, -INFINITY};
+  for (int k0 = 0; k0 < Ns; k0 += 32) {
+    f32x4 S[2][2];
+    scores(k0, S);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m2[qg] = fmaxf(m2[qg], S[qg][t][j]);
+  }
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    m2[qg] = fmaxf(m2[qg], __shfl_xor(m2[qg], 16, 64));
+    m2[qg] = fmaxf(m2[qg], __shfl_xor(m2[qg], 32, 64));
+    lt[qg] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) O[qg][i] = z4;
+  }
+  for (int k0 = 0; k0 < Ns; k0 += 32) {
+    f32x4 S[2][2];
+    scores(k0, S);
+    bf16x8 pf[2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = fast_exp2(S[qg][j >> 2][j & 3] - m2[qg]);
+        lt[qg] += e;
+        pf[qg][j] = (bf16)e;
+      }
+#pragma unroll
+    for (int dvb = 0; dvb < 8; ++dvb) {
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vtb + (long long)(16 * dvb + r16) * p.ldt + k0 + 8 * g);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg], O[qg][dvb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    lt[qg] += __shfl_xor(lt[qg], 16, 64);
+    lt[qg] += __shfl_xor(lt[qg], 32, 64);
+  }
+}
+
+// Epilogue of the 16x16x32 layout: O[qg][dvb] holds O^T[dv][q] for q = q0 + 16 qg + r16,
+// dv = 16 dvb + 4g + e (dvb 0-3: sum p v', 4-7: sum p v'^2); lt = the full row sums.
+template <typename T>
+MHADA_DEV void attn_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], const float (&lt)[2], int b, int hh, int q0,
+                               int g, int r16) {
+  const int C = p.H * 64;
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q0 + 16 * qg + r16;
+    if (q >= p.Nc) continue;
+    const float inv = 1.0f / lt[qg];
+    const float* fr = p.fcs + ((long long)b * p.Nc + q) * C + hh * 64;
+    const float* mu = p.fcs_mu + (long long)b * C + hh * 64;
+    const float* rs = p.fcs_rstd + (long long)b * C + hh * 64;
+    const float* vm = p.v_mu + (long long)b * C + hh * 64;
+    T* orow = reinterpret_cast<T*>(p.out) + ((long long)b * p.Nc + q) * C + hh * 64;
+#pragma unroll
+    for (int dvb = 0; dvb < 4; ++dvb) {
+      const int dv0 = 16 * dvb + 4 * g;
+      const f32x4 f = *reinterpret_cast<const f32x4*>(fr + dv0);
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(mu + dv0);
+      const f32x4 r4 = *reinterpret_cast<const f32x4*>(rs + dv0);
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(vm + dv0);
+      float res[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[qg][dvb][e] * inv;
+        const float e2 = O[qg][dvb + 4][e] * inv;
+        const float sd = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f));
+        res[e] = sd * ((f[e] - m4[e]) * r4[e]) + (m1 + v4[e]);
+      }
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(orow + dv0) = f32x4{res[0], res[1], res[2], res[3]};
+      } else {
+        *reinterpret_cast<bf16x4*>(orow + dv0) = bf16x4{(bf16)res[0], (bf16)res[1], (bf16)res[2], (bf16)res[3]};
+      }
+    }
+  }
+}
+
+template <int NW, bool ONES>
+__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p) {
+  constexpr int TK = 128, NSL = 2;
+  constexpr int KSZ = TK * 64, VSZ = 128 * TK;  // bf16 elements per slot: K [128][64], V'^T [128][128]
+  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;  // 1-KiB pieces per wave
+  static_assert(KPW >= 1 && VPW >= 1, "tile config");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 96 KiB
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q0 = qb * (32 * NW) + wave * 32;
+  const long long bh = (long long)b * p.H + hh;
+  const int Ns = p.Ns;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 qf[2][2];  // Q^T fragments: query q0 + 16 qg + r16, d = 32 dh + 8 g .. + 8
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q0 + 16 * qg + r16;
+    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * g;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      qf[qg][dh] = *reinterpret_cast<const bf16x8*>(qp + 32 * dh);
+      if (q >= p.Nc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[qg][dh][e] = (bf16)0.0f;
+      }
+    }
+  }
+  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
+  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
+  int ksrc[KPW], vsrc[VPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
+    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
+    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
+  }
+  auto stage = [&](int key0, int sl) {
+    bf16* kd = smem + sl * (KSZ + VSZ);
+    bf16* vd = kd + KSZ;
+    const bf16* ks = kvb + (long long)key0 * 128;
+    const bf16* vs = vtb + key0;
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
+  };
+  // per-lane K row offsets (elements) of the two score tiles of a 32-key group
+  int krow[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) krow[t] = fsq_key(r16, t) * 64;
+  auto qk = [&](int sl, f32x4 (&S)[2][4][2], const f32x4 (&init)[2]) {
+    const bf16* ck = smem + sl * (KSZ + VSZ);
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16* kr = ck + kg * 32 * 64 + krow[t];
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          // key & 7 == r16 & 3 | 4 ((r16 >> 2) & 1) == r16 & 7 (fsq_key keeps the low 3 bits)
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + 8 * ((4 * dh + g) ^ (r16 & 7)));
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg)
+            S[qg][kg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][dh], dh == 0 ? init[qg] : S[qg][kg][t],
+                                                                   0, 0, 0);
+        }
+      }
+  };
+  f32x4 O[2][8], L[2];
+  float part[2][4];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    L[qg] = z4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) O[qg][i] = z4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[qg][j] = 0.f;
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  auto finish = [&](int sl, const f32x4 (&S)[2][4][2]) {
+    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = fast_exp2(S[qg][kg][j >> 2][j & 3]);
+          if constexpr (!ONES) part[qg][j & 3] += e;
+          pf[qg][j] = (bf16)e;
+        }
+      if constexpr (ONES) {
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qg], L[qg], 0, 0, 0);
+      }
+      const int ch = (4 * kg + g) ^ r16;  // row 16 dvb + r16: row & 15 == r16
+#pragma unroll
+      for (int dvb = 0; dvb < 8; ++dvb) {
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (16 * dvb + r16) * TK + 8 * ch);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg], O[qg][dvb], 0, 0, 0);
+      }
+    }
+  };
+
+  const int NTILE = Ns / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 Sa[2][4][2], Cm[2];
+  {  // tile 0: unshifted scores, m2 = their max, then shift
+    const f32x4 zi[2] = {z4, z4};
+    qk(0, Sa, zi);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m = fmaxf(m, Sa[qg][kg][t][j]);
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+#pragma unroll
+      for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Sa[qg][kg][t][j] -= m;
+      Cm[qg] = f32x4{-m, -m, -m, -m};
+    }
+  }
+  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  ATTN_STAMP(0);
+  if (NTILE > 1) stage(TK, 1);
+  finish(0, Sa);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 1; t < NTILE; ++t) {
+    if (t + 1 < NTILE) stage((t + 1) * TK, (t + 1) & 1);
+    qk(t & 1, Sa, Cm);
+    finish(t & 1, Sa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  ATTN_STAMP(1);
+  float lt[2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    if constexpr (ONES) {
+      lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
+    } else {
+      float l = (part[qg][0] + part[qg][1]) + (part[qg][2] + part[qg][3]);
+      l += __shfl_xor(l, 16, 64);
+      lt[qg] = l + __shfl_xor(l, 32, 64);
+    }
+  }
+  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q(p, kvb, vtb, qf, O, lt, g, r16);
+  attn_epilogue_q<bf16>(p, O, lt, b, hh, q0, g, r16);
+}
+
+// --------------------------------------------------------------------------------------
+// Persistent form of the fsq kernel with the all-ones row sum ("fsp", tuning attn_sched = 8):
+// one workgroup per CU walks the (b, h, query-block) blocks w, w + G, w + 2G, ... (the hardware
+// block ids a one-shot launch would use, so xcd_remap keeps the 32 workgroups of an XCD on 32
+// query blocks of one (b, h): K / V' shared in its L2), and the K / V'^T tile stream is continuous
+// across blocks: the 2-slot ring's next-tile DMA in the last tile of a block already fetches the
+// NEXT block's tile 0, and that block's Q rows are loaded in the same iteration, so a block
+// starts with its operands resident instead of paying the HBM latency of its prologue (the
+// one-shot kernel spends ~5 % of its time outside the key loop, tools/attn_clock.py).
+// --------------------------------------------------------------------------------------
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsp_kernel(const AttnP p) {
+  constexpr int TK = 128, NSL = 2;
+  constexpr int KSZ = TK * 64, VSZ = 128 * TK;
+  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;
+  static_assert(KPW >= 1 && VPW >= 1, "tile config");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 96 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int Ns = p.Ns, NTILE = Ns / TK, G = gridDim.x;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  struct Blk {
+    int b, hh, q0;
+    const bf16* kvb;
+    const bf16* vtb;
+  };
+  auto decode = [&](int hw, Blk& k) {
+    const int t = xcd_remap(hw, p.nblk);
+    const int qb = t % p.nqb, bh = t / p.nqb;
+    k.b = bh / p.H;
+    k.hh = bh - k.b * p.H;
+    k.q0 = qb * (32 * NW) + wave * 32;
+    k.kvb = reinterpret_cast<const bf16*>(p.kv) + (long long)bh * Ns * 128;
+    k.vtb = reinterpret_cast<const bf16*>(p.vt) + (long long)bh * 128 * p.ldt;
+  };
+  auto load_q = [&](const Blk& k, bf16x8 (&qf)[2][2]) {
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      const int q = k.q0 + 16 * qg + r16;
+      const bf16* qp = reinterpret_cast<const bf16*>(p.q) +
+                       (((long long)k.b * p.H + k.hh) * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * g;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) qf[qg][dh] = *reinterpret_cast<const bf16x8*>(qp + 32 * dh);
+    }
+  };
+  auto mask_q = [&](const Blk& k, bf16x8 (&qf)[2][2]) {
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+      if (k.q0 + 16 * qg + r16 >= p.Nc) {
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qf[qg][dh][e] = (bf16)0.0f;
+      }
+  };
+  int ksrc[KPW], vsrc[VPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
+    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
+    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
+  }
+  auto stage = [&](const Blk& k, int key0, int sl) {
+    bf16* kd = smem + sl * (KSZ + VSZ);
+    bf16* vd = kd + KSZ;
+    const bf16* ks = k.kvb + (long long)key0 * 128;
+    const bf16* vs = k.vtb + key0;
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
+  };
+  int krow[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) krow[t] = fsq_key(r16, t) * 64;
+  bf16x8 qf[2][2], qn[2][2];
+  auto qk = [&](int sl, f32x4 (&S)[2][4][2], const f32x4 (&init)[2]) {
+    const bf16* ck = smem + sl * (KSZ + VSZ);
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16* kr = ck + kg * 32 * 64 + krow[t];
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + 8 * ((4 * dh + g) ^ (r16 & 7)));
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg)
+            S[qg][kg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][dh], dh == 0 ? init[qg] : S[qg][kg][t],
+                                                                   0, 0, 0);
+        }
+      }
+  };
+  f32x4 O[2][8], L[2];
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  auto finish = [&](int sl, const f32x4 (&S)[2][4][2]) {
+    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[qg][j] = (bf16)fast_exp2(S[qg][kg][j >> 2][j & 3]);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qg], L[qg], 0, 0, 0);
+      const int ch = (4 * kg + g) ^ r16;
+#pragma unroll
+      for (int dvb = 0; dvb < 8; ++dvb) {
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (16 * dvb + r16) * TK + 8 * ch);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg], O[qg][dvb], 0, 0, 0);
+      }
+    }
+  };
+
+  int hw = blockIdx.x;
+  if (hw >= p.nblk) return;
+  Blk cur, nxt;
+  decode(hw, cur);
+  load_q(cur, qf);
+  int sl = 0;
+  stage(cur, 0, sl);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  while (true) {
+    const bool more = hw + G < p.nblk;
+    if (more) decode(hw + G, nxt);
+    mask_q(cur, qf);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      L[qg] = z4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) O[qg][i] = z4;
+    }
+    ATTN_STAMP(0);
+    f32x4 Sa[2][4][2], Cm[2];
+    {  // tile 0: unshifted scores, m2 = their max, then shift
+      const f32x4 zi[2] = {z4, z4};
+      qk(sl, Sa, zi);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m = fmaxf(m, Sa[qg][kg][t][j]);
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Sa[qg][kg][t][j] -= m;
+        Cm[qg] = f32x4{-m, -m, -m, -m};
+      }
+    }
+    // tiles 0 .. NTILE-1: the DMA of the stream's next tile (this block's t+1, or the next block's
+    // tile 0 in the last iteration, with the next block's Q rows) flies during tile t
+    for (int t = 0; t < NTILE; ++t) {
+      if (t + 1 < NTILE) {
+        stage(cur, (t + 1) * TK, sl ^ 1);
+      } else if (more) {
+        stage(nxt, 0, sl ^ 1);
+        load_q(nxt, qn);
+      }
+      if (t > 0) qk(sl, Sa, Cm);
+      finish(sl, Sa);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      sl ^= 1;
+    }
+    ATTN_STAMP(1);
+    float lt[2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) lt[qg] = L[qg][0];
+    if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q(p, cur.kvb, cur.vtb, qf, O, lt, g, r16);
+    attn_epilogue_q<bf16>(p, O, lt, cur.b, cur.hh, cur.q0, g, r16);
+    if (!more) break;
+    hw += G;
+    cur = nxt;
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) qf[qg][dh] = qn[qg][dh];
+  }
+}
+
 // Variant selection (Tuning, common.h): the fixed-shift kernel is the bf16 softmax default; the
 // online-max kernel serves the cosine activation and, through attn_fixed_shift = 0, tests / A-B.
 static bool attn_bf16_fixed_shift() { return tuning().attn_fixed_shift != 0; }
 static int attn_waves(int) { return tuning().attn_waves; }
 static int attn_tk() { return tuning().attn_tk; }
+
+static int attn_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
 
 template <int NW>
 static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s) {
@@ -915,6 +1449,16 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
       if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift()) {
         if (tuning().attn_sched == 3 && p.Ns % 128 == 0) {  // LDS-DMA staging, 128-key tiles
           hipLaunchKernelGGL((attn_bf16_fsg_kernel<8>), grid, blk, 0, s, p);
+          return;
+        }
+        if (tuning().attn_sched == 8 && p.Ns % 128 == 0) {  // persistent 16x16x32, continuous tile stream
+          const dim3 pgrid((unsigned)std::min<long long>(p.nblk, attn_num_cus()));
+          hipLaunchKernelGGL((attn_bf16_fsp_kernel<8>), pgrid, blk, 0, s, p);
+          return;
+        }
+        if ((tuning().attn_sched == 6 || tuning().attn_sched == 7) && p.Ns % 128 == 0) {  // 16x16x32 MFMA
+          if (tuning().attn_sched == 7) hipLaunchKernelGGL((attn_bf16_fsq_kernel<8, true>), grid, blk, 0, s, p);
+          else hipLaunchKernelGGL((attn_bf16_fsq_kernel<8, false>), grid, blk, 0, s, p);
           return;
         }
         if (tuning().attn_sched == 5 && p.Ns % 128 == 0) {  // half-tile pipelined, LDS-DMA staging
@@ -970,3 +1514,13 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   }
   return check_launch("mhada_attn");
 }
+
+#ifdef ATTN_CLOCK
+// Diagnostic builds: copy the first n stamps (4 per workgroup) of the last launch to host memory.
+extern "C" int mhada_dbg_attn_clock(unsigned long long* host, int n) {
+  if (!host || n <= 0 || n > 4 * kClockBlocks) return fail("mhada_dbg_attn_clock: bad args");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_clock), sizeof(unsigned long long) * n) != hipSuccess)
+    return fail("mhada_dbg_attn_clock: copy failed");
+  return MHADA_OK;
+}
+#endif

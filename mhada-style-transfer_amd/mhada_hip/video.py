@@ -11,7 +11,7 @@
 
 The inference forms run the HIP kernels (csrc/warp.hip).  When autograd needs a gradient
 through the warp (train_video.py temporal losses) ``warp`` evaluates the same expression with
-differentiable device ops (training v1).
+differentiable device ops (mhada_hip.losses.warp).
 """
 from __future__ import annotations
 
@@ -36,13 +36,10 @@ def cv2_to_tensor(img, resize: Optional[tuple] = None, device: Optional[torch.de
     tensor in [0, 255] on the device (the reference returns it on the CPU and moves it with
     .to(device) at infer_video.py:81).
 
-    Restriction: ``resize`` may only shrink the frame (every reference script downscales, e.g.
-    infer_video.py:80 takes 1080p to 512x256).  cv2.resize(INTER_AREA) also enlarges, with an
-    interpolation this kernel does not implement; a target larger than the frame raises
-    ValueError here instead of silently differing from cv2."""
-    if resize is not None and len(img.shape) == 3 and (int(resize[0]) > img.shape[1] or int(resize[1]) > img.shape[0]):
-        raise ValueError(f"cv2_to_tensor: resize {tuple(resize)} enlarges the {img.shape[1]}x{img.shape[0]} frame; "
-                         "INTER_AREA upscaling is not implemented (downscale only)")
+    Shrinking uses INTER_AREA's box average; enlarging (any axis) OpenCV's area-mode 2-tap
+    interpolation (csrc/ingest.hip), as cv2.resize(INTER_AREA) does — so a low-resolution video
+    resized to a fixed IMAGE_SIZE (exps_video.py:84, infer_video.py:80) works as in the reference.
+    cv2 is not installed here: parity with cv2's bits is unpinned."""
     if not isinstance(img, torch.Tensor):
         t = torch.from_numpy(img)
         if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:

@@ -490,11 +490,53 @@ def resize_area(img: np.ndarray, out_w: int, out_h: int, dtype=np.float64) -> np
     return np.tensordot(t, wx, axes=([1], [1])).transpose(0, 2, 1).astype(dtype)  # (out_h, out_w, C)
 
 
+def _area_up_taps(n_out: int, n_in: int):
+    """Per-output (s0, s1, w0, w1, one_tap) of OpenCV's generic resize with INTER_AREA
+    coefficients (cv::resize, resize.cpp: the `area_mode` branch of the coefficient tables):
+    s = floor(d*scale), f = (float)((d+1) - (s+1)*inv), f = f <= 0 ? 0 : f - floor(f), clamped at
+    the last pixel, weights saturate_cast<short>(w * 2048) (round half to even)."""
+    inv = n_out / n_in
+    scale = 1.0 / inv
+    taps = []
+    for d in range(n_out):
+        s = int(np.floor(d * scale))
+        one = s + 1 >= n_in
+        f = np.float32((d + 1) - (s + 1) * inv)
+        f = np.float32(0) if f <= 0 else np.float32(f - np.floor(f))
+        if s >= n_in - 1:
+            s, f = n_in - 1, np.float32(0)
+        w0 = int(np.rint(np.float32(np.float32(1) - f) * np.float32(2048)))
+        w1 = int(np.rint(f * np.float32(2048)))
+        taps.append((s, min(s + 1, n_in - 1), w0, w1, one))
+    return taps
+
+
+def resize_area_up(img: np.ndarray, out_w: int, out_h: int) -> np.ndarray:
+    """cv2.resize(img, (out_w, out_h), interpolation=cv2.INTER_AREA) when either axis is ENLARGED
+    (u8): OpenCV then runs its generic separable 2-tap resize with area-mode coefficients
+    (_area_up_taps): horizontal int pass S = w0*p[s0] + w1*p[s1] (p[s0]*2048 where s0 + 1 runs
+    off the frame), vertical pass as the vectorised 32s->8u kernel ((S0>>4)*b0 >> 16) +
+    ((S1>>4)*b1 >> 16), (v + 2) >> 2 saturated.  Restated from OpenCV's published source; cv2
+    is not installed here: PARITY UNPINNED (cv2's scalar row tail rounds differently)."""
+    H, W = img.shape[:2]
+    tx, ty = _area_up_taps(out_w, W), _area_up_taps(out_h, H)
+    x = img.astype(np.int64)
+    s0 = np.array([t[0] for t in tx]); s1 = np.array([t[1] for t in tx])
+    w0 = np.array([t[2] for t in tx]); w1 = np.array([t[3] for t in tx]); one = np.array([t[4] for t in tx])
+    hs = np.where(one[None, :, None], x[:, s0] * 2048, x[:, s0] * w0[None, :, None] + x[:, s1] * w1[None, :, None])
+    r0 = np.array([t[0] for t in ty]); r1 = np.array([t[1] for t in ty])
+    b0 = np.array([t[2] for t in ty])[:, None, None]; b1 = np.array([t[3] for t in ty])[:, None, None]
+    v = (((hs[r0] >> 4) * b0) >> 16) + (((hs[r1] >> 4) * b1) >> 16)
+    return np.clip((v + 2) >> 2, 0, 255).astype(np.uint8)
+
+
 def cv2_to_tensor(img_bgr: np.ndarray, resize=None) -> np.ndarray:
     """utilities.cv2_to_tensor (utilities.py:43-52): BGR->RGB, optional INTER_AREA resize
     (resize = (width, height)), toTensor255 -> (3, h, w) float32 in [0, 255]."""
     rgb = img_bgr[..., ::-1]
-    if resize is not None:
+    if resize is not None and (int(resize[0]) > rgb.shape[1] or int(resize[1]) > rgb.shape[0]):
+        rgb = resize_area_up(rgb, int(resize[0]), int(resize[1]))
+    elif resize is not None:
         rgb = np.clip(np.rint(resize_area(rgb, int(resize[0]), int(resize[1]))), 0, 255).astype(np.uint8)
     t = rgb.transpose(2, 0, 1).astype(np.float32)
     return (t / np.float32(255)) * np.float32(255)  # ToTensor, then .mul(255)

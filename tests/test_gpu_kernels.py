@@ -389,11 +389,15 @@ def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
     return out * f + mm + v_mu.double()[:, None]
 
 
-# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsg" (LDS-DMA; the default
+# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsq" / "fsq1" (LDS-DMA on
+# 16x16x32 MFMAs; fsq1 takes the row sum from an all-ones MFMA; fsp = fsq1 persistent with a
+# continuous tile stream across query blocks), "fsg" (LDS-DMA; the default
 # when Ns % 128 == 0), "fsh" (half-tile pipelined, LDS-DMA), "fsE" (register staging, early loads),
 # "fs" (register staging; the default for ragged Ns) — and the online-max kernel "w8".
 # Variants that need whole 128-key tiles fall back to "fs" on ragged Ns.
-ATTN_VARIANTS = {"fsh": dict(attn_fixed_shift=1, attn_sched=5), "fsg": dict(attn_fixed_shift=1, attn_sched=3),
+ATTN_VARIANTS = {"fsq": dict(attn_fixed_shift=1, attn_sched=6), "fsq1": dict(attn_fixed_shift=1, attn_sched=7),
+                 "fsp": dict(attn_fixed_shift=1, attn_sched=8),
+                 "fsh": dict(attn_fixed_shift=1, attn_sched=5), "fsg": dict(attn_fixed_shift=1, attn_sched=3),
                  "fsE": dict(attn_fixed_shift=1, attn_sched=4), "fs": dict(attn_fixed_shift=1, attn_sched=0),
                  "w8": dict(attn_fixed_shift=0)}
 
@@ -425,11 +429,13 @@ def test_mhada_attn_late_max_jump(kernel, Nc, Ns):
 
 @pytest.mark.parametrize("kernel", list(ATTN_VARIANTS))
 @pytest.mark.parametrize("B,Nc,Ns", [(1, 256, 64), (2, 300, 100), (1, 513, 128), (1, 97, 1000), (2, 1000, 777),
-                                     (1, 64, 4096), (2, 300, 256), (1, 97, 384), (1, 520, 1024)])
+                                     (1, 64, 4096), (2, 300, 256), (1, 97, 384), (1, 520, 1024),
+                                     (2, 5000, 256), (3, 3000, 128)])
 def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
     """The bf16 softmax kernels (ATTN_VARIANTS) at 1..32 key tiles of 128, ragged and whole (1, 2,
     3 and 8 whole tiles exercise the pipelined kernels' prologue, odd tile counts and the 3-slot
-    ring), and partial query blocks: against fp64 torch on the same bf16 operands (bf16 P: 1e-2)."""
+    ring), partial query blocks, and more query blocks than CUs (the persistent kernel's block
+    seams, with 1 and 2 tiles per block): against fp64 torch on the same bf16 operands (1e-2)."""
     H = 8
     q = (rnd(B, H, Nc, 64, seed=15) * 0.35).bfloat16()
     kv = (rnd(B, H, Ns, 128, seed=16) * 0.35).bfloat16()
@@ -448,7 +454,7 @@ def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
 def test_gemm_n64_ring_kernel(nz, M, N, K):
     """The fp32 N <= 64 LDS-DMA ring GEMM (the attention backward's dQ = dS K, the per-head 1x1
     convs): batched strided operands, bias, ReLU and residual epilogues against fp64, and against
-    the register-staged tile it replaces (xknob bit 3)."""
+    the register-staged tile it replaces (unaligned rows)."""
     a = rnd(nz, M, K + 4, seed=11)[..., :K]  # row stride K + 4 (16-B aligned, not dense)
     w = rnd(nz, N, K, scale=K ** -0.5, seed=12)
     b = rnd(N, seed=13)
@@ -463,8 +469,9 @@ def test_gemm_n64_ring_kernel(nz, M, N, K):
     c2 = torch.zeros_like(c)
     ops.gemm(c=c2, bias=b, r=r, ldr=ldc, sr=(M * ldc, 0), relu=True, **args)
     assert rel(c2[..., :N], torch.relu(ref) + r[..., :N].double()) < TOL[torch.float32]
-    for xk in (8, 1, 2, 4, 3):  # the register-staged tile; the other tile / ring instantiations; no XCD grouping
-        with _lib.tuning(xknob=xk):
-            c3 = torch.zeros_like(c)
-            ops.gemm(c=c3, bias=b, **args)
-        assert rel(c3[..., :N], ref) < TOL[torch.float32], xk
+    # rows that are not 16-B aligned (row stride K + 1) take the register-staged tile it replaces
+    a1 = rnd(nz, M, K + 1, seed=11)[..., :K]
+    a1.copy_(a)
+    c3 = torch.zeros_like(c)
+    ops.gemm(c=c3, bias=b, **dict(args, a=a1, lda=K + 1, sa=(M * (K + 1), 0)))
+    assert rel(c3[..., :N], ref) < TOL[torch.float32]

@@ -175,3 +175,21 @@ def test_full_size_against_torch_fp32(res, B, dtype):
     assert mse01(a, b) < 1e-4
     if dtype == torch.float32:
         assert mse_raw(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graphed_stylizer_matches_eager(dtype):
+    """mhada_hip.graphs.GraphedStylizer (one hipGraph replay of vit_c -> vit_s -> adaFormer ->
+    clamp, infer_time.py:74-77) gives the eager call's bits, for new inputs on every replay."""
+    from mhada_hip.graphs import GraphedStylizer
+    ms = models(dtype=dtype)
+    g = GraphedStylizer(*ms, (2, 3, 64, 96))
+    for seed in (3, 5):
+        c = seeded_image(2, 64, 96, seed).to(DEV)
+        s = seeded_image(2, 64, 96, seed + 1).to(DEV)
+        ref = stylize(ms, c, s)[3].clamp(0, 255)
+        out = g(c, s)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    with pytest.raises(ValueError):
+        g(torch.zeros(1, 3, 64, 96, device=DEV), torch.zeros(1, 3, 64, 96, device=DEV))

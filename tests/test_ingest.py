@@ -34,8 +34,28 @@ def test_oracle_resize_area_definition():
     np.testing.assert_array_equal(t[0], img[..., 2].astype(np.float32))
 
 
+def test_oracle_resize_area_up_definition():
+    """INTER_AREA enlarging (OpenCV's area-mode 2-tap path, oracle.resize_area_up): an integer
+    factor replicates pixels (area-mode weights are 0/1 there), a constant image stays constant,
+    and values stay between the neighbouring source levels."""
+    img = _frame(3, 5, 7)
+    up = O.resize_area_up(img, 14, 10)
+    np.testing.assert_array_equal(up, img.repeat(2, axis=0).repeat(2, axis=1))
+    const = np.full((6, 9, 3), 200, np.uint8)
+    np.testing.assert_array_equal(O.resize_area_up(const, 20, 13), 200)
+    frac = O.resize_area_up(img, 11, 8).astype(int)
+    assert frac.shape == (8, 11, 3) and frac.min() >= int(img.min()) and frac.max() <= int(img.max())
+    mixed = O.resize_area_up(img, 3, 9)  # width shrinks, height grows: same generic path
+    assert mixed.shape == (9, 3, 3)
+    t = O.cv2_to_tensor(img, resize=(14, 10))
+    np.testing.assert_array_equal(t[0], up[..., 2].astype(np.float32))
+
+
 def _check_against_oracle(frame, resize, got):
     rgb = frame[..., ::-1]
+    if resize is not None and (resize[0] > frame.shape[1] or resize[1] > frame.shape[0]):
+        np.testing.assert_array_equal(got, O.cv2_to_tensor(frame, resize))  # integer path: bit-exact
+        return
     if resize is None:
         ref = O.cv2_to_tensor(frame)
         np.testing.assert_array_equal(got, ref)  # exact, bit for bit (both fp32 /255 *255)
@@ -50,7 +70,9 @@ def _check_against_oracle(frame, resize, got):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,resize", [(1080, 1920, None), (1080, 1920, (512, 256)), (1080, 1920, (960, 540)),
-                                        (37, 53, (20, 11)), (64, 64, (64, 64)), (7, 5, (1, 1))])
+                                        (37, 53, (20, 11)), (64, 64, (64, 64)), (7, 5, (1, 1)),
+                                        (240, 320, (512, 256)), (37, 53, (100, 41)), (5, 7, (14, 10)),
+                                        (40, 100, (60, 90))])
 def test_frame_ingest_matches_oracle(H, W, resize):
     from mhada_hip import video
     frame = _frame(H * W, H, W)
@@ -72,7 +94,8 @@ def test_frame_ingest_batched_padded_rows_and_errors():
         _check_against_oracle(frames[i].numpy(), (20, 15), out[i])
     keep = ops.frame_ingest(dev, None, bgr=False).cpu().numpy()  # RGB order kept
     np.testing.assert_array_equal(keep[1, 0], frames[1, :, :, 0].numpy().astype(np.float32))
-    with pytest.raises(ValueError):
-        ops.frame_ingest(dev, (60, 80))  # upscaling is not implemented
+    up = ops.frame_ingest(dev, (60, 80), bgr=True).cpu().numpy()  # enlarging: area-mode 2-tap path
+    for i in range(3):
+        _check_against_oracle(frames[i].numpy(), (80, 60), up[i])
     with pytest.raises(ValueError):
         ops.frame_ingest(dev.float(), None)

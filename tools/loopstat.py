@@ -18,8 +18,8 @@ for i, l in enumerate(body):
         print(f"loop {m.group(1)}: {len(seg)} instrs, mfma {sum(v for k, v in c.items() if 'mfma' in k)}")
         print("   " + ", ".join(f"{k} {v}" for k, v in c.most_common(16)))
         if "--seq" in sys.argv:
-            abbrev = {"v_mfma_f32_32x32x16_bf16": "M", "v_exp_f32_e32": "E", "v_fma_f32": "F", "v_accvgpr_read_b32": "R",
+            abbrev = {"v_mfma_f32_32x32x16_bf16": "M", "v_mfma_f32_16x16x32_bf16": "m", "v_exp_f32_e32": "E", "v_fma_f32": "F", "v_accvgpr_read_b32": "R",
                       "v_accvgpr_write_b32": "w", "v_cvt_pk_bf16_f32": "C", "v_add_f32_e64": "A", "v_add_f32_e32": "A",
-                      "v_pk_add_f32": "P", "ds_read_b128": "D", "ds_write_b128": "X", "v_mov_b32_e32": "m",
+                      "v_pk_add_f32": "P", "ds_read_b128": "D", "ds_write_b128": "X", "v_mov_b32_e32": "v",
                       "s_waitcnt": "W", "global_load_dwordx4": "G", "s_barrier": "|B|", "s_nop": "n"}
             print("   " + " ".join(abbrev.get(x, "." ) for x in seg))
