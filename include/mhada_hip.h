@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 9 (3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 10 (mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -172,6 +172,11 @@ int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
  * Replaces the autograd of adaDecoder.py:186-198 (bmm/softmax/bmm/sqrt); A is never stored. */
 int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const float* x, float* out,
                          float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
+/* The same forward on the inference fp32 attention structure (64-key tiles, lazy rescale, PV
+ * operands from a V'^T | V'^2^T image): vt is caller-provided fp32 workspace [BH][128][ceil64(Ns)]
+ * that this call fills from v.  Same outputs as mhada_attn_train_fwd (ABI 10). */
+int mhada_attn_train_fwd_vt(const float* q, const float* k, const float* v, float* vt, const float* x,
+                            float* out, float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
 int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
                          const float* dmo, const float* dd, float* dq, float* dk, float* dv,
                          int BH, int Nc, int Ns, mhada_stream_t stream);
@@ -293,8 +298,11 @@ int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const f
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */
 int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t stream);
 /* Adjoint of ReflectionPad2d(1) (conv.py:27,31): dxp [B][H+2][W+2][C] (the full-correlation
- * input gradient on the padded grid) -> dx [B][H][W][C]. */
-int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t stream);
+ * input gradient on the padded grid) -> dx [B][H][W][C].  relu_mask (null: none; layout of dx):
+ * dx = 0 where relu_mask <= 0 — the ReLU adjoint of the layer that produced the conv's input,
+ * when this conv is that output's only consumer (replaces a mhada_relu_bwd pass; ABI 10). */
+int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, const float* relu_mask,
+                       mhada_stream_t stream);
 /* MaxPool2d(2, 2) on NHWC (vgg19.py slices, torchvision cfg E) and its backward (the gradient
  * goes to the first maximum of each window in row-major order, as ATen keeps it).  relu_mask = 1:
  * x is a ReLU output consumed only by this pool, and the ReLU adjoint (x > 0) is applied too. */
@@ -354,9 +362,11 @@ int mhada_conv3x3_wgrad_wino_splits(int B, int H, int W, int Cin, int Cout);
 int mhada_conv3x3_wgrad_wino(const float* x, const float* g, float* dw, float* db, float* work, long long work_floats,
                              int B, int H, int W, int Cin, int Cout, long long ldg, int pad_mode,
                              mhada_stream_t stream);
+/* relu_mask (null: none; layout of y): y = 0 where relu_mask <= 0 — a ReLU adjoint folded into a
+ * dgrad's output stage (ABI 10). */
 int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
                        int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
-                       mhada_stream_t stream);
+                       const float* relu_mask, mhada_stream_t stream);
 
 /* The 3-channel ends of the training conv stacks (rgb_ops.hip), fp32:
  * VGG19's first layer (vgg19.py:10-11,25-26: normalise -> Conv2d(3, 64, 3, padding=1) -> ReLU),

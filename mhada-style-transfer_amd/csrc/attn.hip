@@ -126,10 +126,68 @@ MHADA_DEV void scale_acc(f32x16 (&O)[4], float alpha) {
 }
 
 
+// Training epilogue (attn_train.hip's forward contract): out' = sqrt(max(E2' - M'^2, 1e-6)) x + M',
+// mo = [M' | E2'], lse2 = m2 + log2(l) per query row; x = p.fcs [BH][Nc][64].
+MHADA_DEV void attn_train_epilogue(const AttnP& p, const f32x16 (&O)[4], float l, float m2, long long bh, int q,
+                                   int h) {
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q >= p.Nc) return;
+  const float inv = 1.0f / lt;
+  const long long row = bh * p.Nc + q;
+  const float* xr = p.fcs + row * 64;
+  float* orow = reinterpret_cast<float*>(p.out) + row * 64;
+  float* mrow = p.mo + row * 128;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 8 * g + 4 * h + 32 * blk;
+      const f32x4 xx = *reinterpret_cast<const f32x4*>(xr + c0);
+      f32x4 o, mm, ee;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[blk][4 * g + e] * inv;
+        const float e2 = O[blk + 2][4 * g + e] * inv;
+        o[e] = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f)) * xx[e] + m1;
+        mm[e] = m1;
+        ee[e] = e2;
+      }
+      *reinterpret_cast<f32x4*>(orow + c0) = o;
+      *reinterpret_cast<f32x4*>(mrow + c0) = mm;
+      *reinterpret_cast<f32x4*>(mrow + 64 + c0) = ee;
+    }
+  if (h == 0) p.lse[row] = m2 + __log2f(lt);
+}
+
+// fp32 V'^T | V'^2^T image [BH][128][ldt] (natural key order, zero padded) of the training v
+// [BH][Ns][64] rows: the PV operand layout of attn_f32_kernel.
+__global__ void __launch_bounds__(256) train_vt_kernel(const float* __restrict__ v, float* __restrict__ vt, int Ns,
+                                                       int ldt) {
+  __shared__ float tile[64][65];
+  const int bh = blockIdx.y, n0 = blockIdx.x * 64;
+  const float* src = v + (long long)bh * Ns * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int n = i >> 6, o = i & 63;
+    tile[n][o] = (n0 + n < Ns) ? src[(long long)(n0 + n) * 64 + o] : 0.f;
+  }
+  __syncthreads();
+  float* dst = vt + (long long)bh * 128 * ldt + n0;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int o = i >> 6, n = i & 63;
+    const float x = tile[n][o];
+    dst[(long long)o * ldt + n] = x;
+    dst[(long long)(64 + o) * ldt + n] = x * x;
+  }
+}
+
 // ======================================================================================
 // fp32 variant
 // ======================================================================================
-template <int ACT, int NW>
+// TRAIN (mhada_attn_train_fwd_vt): the forward of the training step on the same structure —
+// K rows of p.ldk = 64 floats (the training k), Q scaled by log2 e on load (the training q is in
+// natural units), and the training epilogue (attn_train_epilogue: out', [M' | E2'], lse2 =
+// m2 + log2 l, exact for the lazily rescaled state since l is relative to m2).
+template <int ACT, int NW, bool TRAIN = false>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(const AttnP p) {
   constexpr int NT = 64 * NW;
   constexpr int LK = 68, LV = 68;  // padded rows (272 B): conflict-free 16-B reads down a column
@@ -146,14 +204,16 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
   float qreg[32];
   {
     const float* qp = reinterpret_cast<const float*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 32 * h;
+    const float qs = TRAIN ? 1.4426950408889634f : 1.0f;  // log2 e (inference: folded into K)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const f32x4 t = *reinterpret_cast<const f32x4*>(qp + 4 * i);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) qreg[4 * i + e] = (q < p.Nc) ? t[e] : 0.f;
+      for (int e = 0; e < 4; ++e) qreg[4 * i + e] = (q < p.Nc) ? t[e] * qs : 0.f;
     }
   }
-  const float* kvb = reinterpret_cast<const float*>(p.kv) + bh * p.Ns * 128;
+  const int ldk = TRAIN ? 64 : 128;
+  const float* kvb = reinterpret_cast<const float*>(p.kv) + bh * p.Ns * ldk;
   const float* vtb = reinterpret_cast<const float*>(p.vt) + bh * 128 * (long long)p.ldt;
 
   // K rows from kv, V'^T | V'^2^T columns from the vt image (mhada_transpose_v, zero padded to
@@ -165,7 +225,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
     for (int i = 0; i < KCH; ++i) {
       const int c = tid + NT * i, row = c >> 4, col = (c & 15) * 4;
       const int key = key0 + row;
-      sk[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sk[i] = key < p.Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * ldk + col) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
@@ -270,7 +330,8 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
     if (softmax_tile<ACT, 2>(S, m2, l, alpha)) scale_acc(O, alpha);
     pv(sV[cb], S);
   }
-  attn_epilogue<float>(p, O, l, b, hh, q, h);
+  if constexpr (TRAIN) attn_train_epilogue(p, O, l, m2, bh, q, h);
+  else attn_epilogue<float>(p, O, l, b, hh, q, h);
 }
 
 // ======================================================================================
@@ -1501,6 +1562,7 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   p.q = q; p.kv = kv; p.vt = vt; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
   p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
   p.prio = tuning().attn_prio;
+  p.ldk = 128;
   p.ldt = (Ns + 63) / 64 * 64;
   const int nw = attn_waves(dtype);
   p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
@@ -1524,3 +1586,27 @@ extern "C" int mhada_dbg_attn_clock(unsigned long long* host, int n) {
   return MHADA_OK;
 }
 #endif
+
+// Training forward on the inference fp32 attention structure (64-key tiles, lazy rescale, the PV
+// operands as one 16-B LDS read per 4 MFMAs from the V'^T | V'^2^T image): replaces
+// mhada_attn_train_fwd (attn_train.hip), same outputs.  vt: caller-provided workspace
+// [BH][128][ceil64(Ns)] fp32, filled here from v.
+extern "C" int mhada_attn_train_fwd_vt(const float* q, const float* k, const float* v, float* vt, const float* x,
+                                       float* out, float* mo, float* lse, int BH, int Nc, int Ns,
+                                       mhada_stream_t s_) {
+  if (!q || !k || !v || !vt || !x || !out || !mo || !lse || BH <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_train_fwd_vt: bad args");
+  if (BH > 65535) return fail("mhada_attn_train_fwd_vt: BH > 65535");
+  const hipStream_t s = (hipStream_t)s_;
+  AttnP p = {};
+  p.q = q; p.kv = k; p.vt = vt; p.fcs = x; p.out = out; p.mo = mo; p.lse = lse;
+  p.B = BH; p.H = 1; p.Nc = Nc; p.Ns = Ns; p.ldk = 64;
+  p.ldt = (Ns + 63) / 64 * 64;
+  p.nqb = (Nc + 255) / 256;
+  const long long nblk = (long long)BH * p.nqb;
+  if (nblk > (1LL << 31) - 1) return fail("mhada_attn_train_fwd_vt: grid too large");
+  p.nblk = (int)nblk;
+  hipLaunchKernelGGL(train_vt_kernel, dim3(p.ldt / 64, BH), dim3(256), 0, s, v, vt, Ns, p.ldt);
+  hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX, 8, true>), dim3(p.nblk), dim3(512), 0, s, p);
+  return check_launch("mhada_attn_train_fwd_vt");
+}

@@ -18,6 +18,12 @@ struct AttnP {
   void* out;        // [B][Nc][C]
   int B, H, Nc, Ns, ldt, nqb, nblk;
   int prio;                    // fs kernel: s_setprio(1) for the younger wave half (MHADA_ATTN_PRIO)
+  // training forward (attn_f32_kernel<.., TRAIN = true>, mhada_attn_train_fwd_vt): K rows of ldk
+  // floats (64: the training k [BH][Ns][64]; inference reads K from kv rows of 128), Q unscaled
+  // (log2 e applied on load), x = InstanceNorm(fcs) [BH][Nc][64]; writes out', [M' | E2'], lse2
+  int ldk;
+  float* mo;
+  float* lse;
 };
 
 MHADA_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

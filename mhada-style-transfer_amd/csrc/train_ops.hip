@@ -780,7 +780,7 @@ __global__ void __launch_bounds__(256) feat_loss_bwd_kernel(const float* __restr
 // dX[b][y][x] = sum of dXp[b][py][px] over the padded positions whose reflection is (y, x):
 // py = y + 1, plus py = 0 when y == 1 and py = H + 1 when y == H - 2 (same in x).
 __global__ void __launch_bounds__(256) reflect_fold_kernel(const float* __restrict__ dxp, float* __restrict__ dx, int B,
-                                                           int H, int W, int C) {
+                                                           int H, int W, int C, const float* __restrict__ mask) {
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
   const int C4 = C / 4;
   const long long total = (long long)B * H * W * C4;
@@ -805,7 +805,13 @@ __global__ void __launch_bounds__(256) reflect_fold_kernel(const float* __restri
   for (int i = 0; i < ny; ++i)
     for (int j = 0; j < nx; ++j)
       acc += *reinterpret_cast<const f32x4*>(dxp + (((long long)b * Hp + ys[i]) * Wp + xs[j]) * C + 4 * c4);
-  *reinterpret_cast<f32x4*>(dx + (((long long)b * H + y) * W + x) * C + 4 * c4) = acc;
+  const long long o = (((long long)b * H + y) * W + x) * C + 4 * c4;
+  if (mask) {  // the ReLU adjoint of the layer that produced x (its output's only consumer is this conv)
+    const f32x4 m = *reinterpret_cast<const f32x4*>(mask + o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = m[e] > 0.f ? acc[e] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(dx + o) = acc;
 }
 
 __global__ void __launch_bounds__(256) maxpool2_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H,
@@ -1264,11 +1270,12 @@ extern "C" int mhada_feat_loss_bwd(const float* x, const float* t, const float* 
   return check_launch("mhada_feat_loss_bwd");
 }
 
-extern "C" int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, mhada_stream_t s_) {
-  if (!dxp || !dx || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(dxp) || !al16(dx))
+extern "C" int mhada_reflect_fold(const float* dxp, float* dx, int B, int H, int W, int C, const float* relu_mask,
+                                  mhada_stream_t s_) {
+  if (!dxp || !dx || B <= 0 || H < 2 || W < 2 || C % 4 || !al16(dxp) || !al16(dx) || (relu_mask && !al16(relu_mask)))
     return fail("mhada_reflect_fold: bad args");
   hipLaunchKernelGGL(reflect_fold_kernel, grid1((long long)B * H * W * (C / 4)), dim3(256), 0, (hipStream_t)s_, dxp, dx,
-                     B, H, W, C);
+                     B, H, W, C, relu_mask);
   return check_launch("mhada_reflect_fold");
 }
 

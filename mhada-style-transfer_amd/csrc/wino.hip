@@ -58,6 +58,7 @@ struct WinoP {
   const float* u;     // [Cin/8][16][Cout][8]
   const float* bias;  // [Cout] or null
   float* y;           // NHWC [B][Ho][Wo][ldc]
+  const float* mask;  // null, or [B][Ho][Wo][ldc]: y = 0 where mask <= 0 (a ReLU adjoint folded into a dgrad)
   int B, H, W, Cin, Cout, Ho, Wo, pad, zero, relu;
   long long ldc;
   int nbx, nby, nbn, nblk;
@@ -282,8 +283,14 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
       }
       const int ox = ox0 + q;
       if (ox < p.Wo) {
-        if (oy0 < p.Ho) p.y[((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co] = y0;
-        if (oy0 + 1 < p.Ho) p.y[((long long)(b * p.Ho + oy0 + 1) * p.Wo + ox) * p.ldc + co] = y1;
+        const long long i0 = ((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co;
+        const long long i1 = i0 + (long long)p.Wo * p.ldc;
+        if (p.mask) {
+          if (oy0 < p.Ho && !(p.mask[i0] > 0.f)) y0 = 0.f;
+          if (oy0 + 1 < p.Ho && !(p.mask[i1] > 0.f)) y1 = 0.f;
+        }
+        if (oy0 < p.Ho) p.y[i0] = y0;
+        if (oy0 + 1 < p.Ho) p.y[i1] = y1;
       }
     }
   }
@@ -643,7 +650,7 @@ extern "C" int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, m
 
 extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
                                   int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
-                                  mhada_stream_t s_) {
+                                  const float* relu_mask, mhada_stream_t s_) {
   if (!x || !u || !y || B <= 0 || H < 2 || W < 2 || Cin <= 0 || Cout <= 0)
     return fail("mhada_conv3x3_wino: bad args");
   if (Cin % kCK || Cout % kCO) return fail("mhada_conv3x3_wino: needs Cin % 8 == 0 and Cout % 64 == 0");
@@ -652,7 +659,7 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   if (ldc < Cout) return fail("mhada_conv3x3_wino: ldc < Cout");
   if (((uintptr_t)x | (uintptr_t)u) & 15) return fail("mhada_conv3x3_wino: x and u must be 16-byte aligned");
   WinoP p;
-  p.x = x; p.u = u; p.bias = bias; p.y = y;
+  p.x = x; p.u = u; p.bias = bias; p.y = y; p.mask = relu_mask;
   p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
   p.zero = pad_mode == MHADA_PAD_ZERO;
   p.pad = p.zero ? pad : 1;

@@ -68,6 +68,7 @@ SIGNATURES = {
     "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
+    "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
     "mhada_attn_train_bwd": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_attn_train_dkv": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
@@ -89,7 +90,7 @@ SIGNATURES = {
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
     "mhada_feat_loss_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _F, _vp, _I, _c_ll, _I, _vp]),
-    "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_upsample2x_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
@@ -98,7 +99,7 @@ SIGNATURES = {
     "mhada_wino_weights": (_I, [_vp, _vp, _I, _I, _vp]),
     "mhada_conv3x3_wgrad_wino_splits": (_I, [_I, _I, _I, _I, _I]),
     "mhada_conv3x3_wgrad_wino": (_I, [_vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _I, _I, _I, _c_ll, _I, _vp]),
-    "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp]),
+    "mhada_conv3x3_wino": (_I, [_vp] * 4 + [_I] * 5 + [_c_ll, _I, _I, _I, _vp, _vp]),
     "mhada_vgg_stem_dgrad": (_I, [_vp] * 4 + [_I] * 3 + [_vp]),
     "mhada_out3_dgrad": (_I, [_vp] * 5 + [_I] * 3 + [_vp]),
     "mhada_out3_wgrad_work": (_c_ll, [_I, _I, _I]),
@@ -132,7 +133,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 def get_tuning(name: str) -> int:

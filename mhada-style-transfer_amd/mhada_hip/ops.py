@@ -193,9 +193,11 @@ def wino_weights(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv3x3_wino(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = True,
-                 pad_mode: str = "reflect", pad: int = 1, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``mhada_conv3x3_wino``: fp32 NHWC conv3x3 from the transformed filters ``u``."""
-    _need_gpu(x, u, bias, out)
+                 pad_mode: str = "reflect", pad: int = 1, out: Optional[torch.Tensor] = None,
+                 relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``mhada_conv3x3_wino``: fp32 NHWC conv3x3 from the transformed filters ``u``; ``relu_mask``
+    (the output's layout): zero the outputs where relu_mask <= 0 (a folded ReLU adjoint)."""
+    _need_gpu(x, u, bias, out, relu_mask)
     B, H, W, Ci = x.shape
     Co = u.shape[2]
     if x.dtype != torch.float32 or not x.is_contiguous() or u.shape[0] * 8 != Ci:
@@ -209,25 +211,33 @@ def conv3x3_wino(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
     y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32) if out is None else out
     if y.shape[:3] != (B, Ho, Wo) or y.dtype != torch.float32 or y.shape[-1] < Co or not y.is_contiguous():
         raise ValueError("conv3x3_wino: bad output buffer")
+    if relu_mask is not None and (relu_mask.shape != y.shape or relu_mask.dtype != torch.float32
+                                  or not relu_mask.is_contiguous()):
+        raise ValueError("conv3x3_wino: relu_mask must be a contiguous fp32 tensor shaped like the output")
     _call("mhada_conv3x3_wino", x, x.data_ptr(), u.data_ptr(), _ptr(bias), y.data_ptr(), B, H, W, Ci, Co,
-          y.shape[-1], mode, pad, int(relu))
+          y.shape[-1], mode, pad, int(relu), _ptr(relu_mask))
     return y
 
 
 def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
             upsample: bool, relu: bool = True, pad_mode: str = "reflect", pad: int = 1,
-            out: Optional[torch.Tensor] = None, wino_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, wino_u: Optional[torch.Tensor] = None,
+            relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NHWC x [B][H][W][Cin] -> NHWC [B][H'][W'][Cout]; ReflectionPad2d(1)+conv3x3(+ReLU),
     optionally on bilinear-x2(x), or (pad_mode "zero") a zero-padded conv with padding `pad`
     (1: same size, 2: the full correlation, H' = H + 2).  w packed [Cout][9*Cin] in the compute
     dtype.  ``out`` may be a preallocated [B][H'][W'][ldc >= Cout] buffer (channel padding).
     fp32 runs as Winograd F(2x2,3x3) when the shape allows (``wino_u``: cached transformed
-    filters of ``w``)."""
+    filters of ``w``).  ``relu_mask`` (fp32, shaped like the output): zero the outputs where
+    relu_mask <= 0 — a ReLU adjoint folded into a dgrad (in the Winograd output stage; a separate
+    mhada_relu_bwd pass on the implicit-GEMM path)."""
     B, H, W, Ci = x.shape
     Co = w.shape[0]
     if out_dtype == torch.float32 and wino_eligible(x, w, upsample) and x.is_contiguous():
         u = wino_u if wino_u is not None else wino_weights(w)
-        return conv3x3_wino(x, u, bias, relu, pad_mode, pad, out)
+        return conv3x3_wino(x, u, bias, relu, pad_mode, pad, out, relu_mask)
+    if relu_mask is not None:
+        return relu_bwd(conv3x3(x, w, bias, out_dtype, upsample, relu, pad_mode, pad, out), relu_mask)
     if pad_mode == "zero":
         if upsample:
             raise ValueError("zero-padded conv3x3 has no fused upsample")
@@ -446,9 +456,19 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     out = torch.empty_like(q)
     mo = torch.empty(BH, Nc, 128, device=q.device, dtype=torch.float32)
     lse = torch.empty(BH, Nc, device=q.device, dtype=torch.float32)
-    _call("mhada_attn_train_fwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), x.data_ptr(), out.data_ptr(),
-                                          mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns)
+    if TRAIN_FWD_VT:
+        # the inference fp32 attention structure on a V'^T | V'^2^T image (workspace, freed after)
+        vt = torch.empty(BH, 128, (Ns + 63) // 64 * 64, device=q.device, dtype=torch.float32)
+        _call("mhada_attn_train_fwd_vt", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), vt.data_ptr(), x.data_ptr(),
+              out.data_ptr(), mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns)
+    else:
+        _call("mhada_attn_train_fwd", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), x.data_ptr(), out.data_ptr(),
+              mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns)
     return out, mo, lse
+
+
+# attn_train_fwd: True = mhada_attn_train_fwd_vt (the default), False = the round-1 kernel (A/B, tests)
+TRAIN_FWD_VT = True
 
 
 # Largest dS spill (BH * Nc * Ns fp32) the training backward takes (512^2 batch 8, the three
@@ -648,11 +668,15 @@ def feat_loss_bwd(x: torch.Tensor, mu: Optional[torch.Tensor], alpha: Optional[t
     return g
 
 
-def reflect_fold(dxp: torch.Tensor) -> torch.Tensor:
-    _need_gpu(dxp)
+def reflect_fold(dxp: torch.Tensor, relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``mhada_reflect_fold``; ``relu_mask`` (shaped like the result): zero where relu_mask <= 0."""
+    _need_gpu(dxp, relu_mask)
     B, Hp, Wp, C = dxp.shape
     dx = torch.empty(B, Hp - 2, Wp - 2, C, device=dxp.device, dtype=torch.float32)
-    _call("mhada_reflect_fold", dxp, dxp.data_ptr(), dx.data_ptr(), B, Hp - 2, Wp - 2, C)
+    if relu_mask is not None and (relu_mask.shape != dx.shape or relu_mask.dtype != torch.float32
+                                  or not relu_mask.is_contiguous()):
+        raise ValueError("reflect_fold: relu_mask must be a contiguous fp32 tensor shaped like the result")
+    _call("mhada_reflect_fold", dxp, dxp.data_ptr(), dx.data_ptr(), B, Hp - 2, Wp - 2, C, _ptr(relu_mask))
     return dx
 
 

@@ -105,7 +105,7 @@ def _wino(weight: torch.Tensor, kind: str, packed: torch.Tensor, *dims) -> Optio
 class Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pad_mode: str, relu: bool,
-                grad_masked: bool = False):
+                grad_masked: bool = False, relu_input: bool = False):
         if x.dtype != F32 or not x.is_contiguous():
             raise ValueError("conv3x3 (training) takes contiguous fp32 NHWC activations")
         B, H, W, cx = x.shape
@@ -120,7 +120,10 @@ class Conv3x3Fn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y)
         # grad_masked: the output's only consumer (MaxPool2Fn(relu_input=True)) hands back the
         # gradient with the ReLU adjoint already applied
-        ctx.pad_mode, ctx.relu, ctx.grad_masked = pad_mode, relu, grad_masked
+        # relu_input: x is the ReLU output of a Conv3x3Fn(grad_masked=True) whose only consumer is this
+        # conv: the input gradient leaves with that ReLU's adjoint applied (the Winograd dgrad's output
+        # stage / the reflect fold zero it where x <= 0), so the producer skips its relu_bwd pass
+        ctx.pad_mode, ctx.relu, ctx.grad_masked, ctx.relu_input = pad_mode, relu, grad_masked, relu_input
         return y if ldc == co else y[..., :co].contiguous()
 
     @staticmethod
@@ -139,11 +142,13 @@ class Conv3x3Fn(torch.autograd.Function):
             gk = g if cg == ldc else F.pad(g, (0, cg - ldc))
             wt = _cached(weight, "d", cx, cg)
             ut = _wino(weight, "d", wt, cx, cg)
+            mask = x if ctx.relu_input else None
             if ctx.pad_mode == "zero":
-                gx = ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero", pad=1, wino_u=ut)
+                gx = ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero", pad=1, wino_u=ut,
+                                 relu_mask=mask)
             else:
                 gx = ops.reflect_fold(ops.conv3x3(gk, wt, None, F32, upsample=False, relu=False, pad_mode="zero",
-                                                  pad=2, wino_u=ut))
+                                                  pad=2, wino_u=ut), relu_mask=mask)
         if ctx.needs_input_grad[1] and ops.wgrad_wino_eligible(x, g, co):
             # Winograd F(2x2,3x3) weight gradient (2.25x fewer products than the im2col TN GEMM),
             # bias gradient from its dY transform
@@ -162,7 +167,7 @@ class Conv3x3Fn(torch.autograd.Function):
                 gb = cs[:co].contiguous()
         elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)[:co].contiguous()
-        return gx, gw, gb, None, None, None
+        return gx, gw, gb, None, None, None, None
 
 
 class LinearFn(torch.autograd.Function):
@@ -562,8 +567,9 @@ def _stem_eligible(img: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.bias is not None and not conv.weight.requires_grad and not conv.bias.requires_grad)
 
 
-def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True, grad_masked: bool = False):
-    return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu, grad_masked)
+def conv3x3(x, conv: torch.nn.Conv2d, pad_mode: str, relu: bool = True, grad_masked: bool = False,
+            relu_input: bool = False):
+    return Conv3x3Fn.apply(x, conv.weight, conv.bias, pad_mode, relu, grad_masked, relu_input)
 
 
 def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
@@ -581,6 +587,7 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
     x = nchw_to_nhwc(x_nchw.float())
     last = getattr(dec, order[-1][0])[order[-1][1]].conv.conv
     masked = False
+    relu_in = False  # x is the ReLU output of the previous conv, consumed only by this conv
     for i, (seq, idx, up) in enumerate(order):
         conv = getattr(dec, seq)[idx].conv.conv
         if i == len(order) - 1 and not up and (masked or _out3_eligible(x, conv)):
@@ -592,8 +599,12 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
         masked = (i == len(order) - 2 and not up and not order[-1][2] and conv.weight.shape[0] == 64
                   and x.is_cuda and x.dtype == F32 and x.shape[1] >= 2 and x.shape[2] >= 2
                   and tuple(last.weight.shape) == (3, 64, 3, 3) and last.bias is not None)
-        # a layer followed by the bilinear x2 leaves its ReLU adjoint to the upsample's backward
-        x = conv3x3(x, conv, "reflect", relu=True, grad_masked=masked or (up and x.is_cuda))
+        # a layer followed by the bilinear x2 leaves its ReLU adjoint to the upsample's backward, one
+        # followed by another conv3x3 of this loop to that conv's input gradient (relu_input)
+        nxt_conv = (not up and not masked and x.is_cuda and i + 1 < len(order) - 1)
+        x = conv3x3(x, conv, "reflect", relu=True, grad_masked=masked or (up and x.is_cuda) or nxt_conv,
+                    relu_input=relu_in)
+        relu_in = nxt_conv
         if up:
             x = Upsample2xFn.apply(x, x.is_cuda)
     return x.permute(0, 3, 1, 2).contiguous()
@@ -604,6 +615,7 @@ def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, tor
     NHWC storage."""
     x = None
     relu_to_pool = False
+    relu_in = False
     feats = {}
     for s, (a, b) in enumerate(slices, start=1):
         seq = getattr(vgg, f"slice{s}")
@@ -618,7 +630,11 @@ def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, tor
                 # a conv whose ReLU output feeds only the next pool (vgg19 cfg E: conv1_2, conv2_2,
                 # conv3_4, conv4_4) leaves its ReLU adjoint to the pool's backward
                 pooled = (i + 2) in pools and i + 2 < b
-                x = conv3x3(x, conv, "zero", relu=True, grad_masked=pooled)
+                # a conv whose ReLU output feeds only the next conv of the same slice (conv3_2, 3_3,
+                # 4_2, 4_3: not a slice end, so not a loss feature) leaves it to that conv's dgrad
+                chained = (i + 2) in convs and i + 2 < b and x.is_cuda
+                x = conv3x3(x, conv, "zero", relu=True, grad_masked=pooled or chained, relu_input=relu_in)
+                relu_in = chained
                 relu_to_pool = pooled
             elif i in pools:
                 x = MaxPool2Fn.apply(x, relu_to_pool)

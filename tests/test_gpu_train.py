@@ -104,3 +104,20 @@ def test_rccl_data_parallel_grads_match_single_gpu():
             assert torch.equal(grads[0][n], grads[1][n]), n
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_train_step_512_b1_losses_match_oracle():
+    """BASELINE configs[3]'s resolution (512^2), batch 1: the five loss terms of one
+    train_image.py:103-136 step on the HIP path against the numpy oracle (oracle.train_losses,
+    rtol 2e-4), run here inside the test (about a minute of CPU on the box's 16 threads)."""
+    from oracle import mhada_oracle as O
+    c = seeded_image(1, 512, 512, 61)
+    s = seeded_image(1, 512, 512, 62)
+    ms = build("cpu")
+    p = [O.to_numpy_params(m.state_dict()) for m in ms]
+    ref = np.array(O.train_losses(c.numpy(), s.numpy(), *p))
+    tr = Trainer(*build("cuda"))
+    out = tr.backward(c.cuda(), s.cuda())
+    got = np.array([float(out[k].detach()) for k in ("loss_gs", "loss_lf", "loss_id1", "loss_id2", "loss")])
+    np.testing.assert_allclose(got, ref, rtol=2e-4)

@@ -176,3 +176,29 @@ def test_fused_block_under_autocast_runs_fp32_kernels():
     assert torch.isfinite(ys[1][0]).all() and torch.isfinite(ys[1][1]).all()
     assert _rel(ys[1][0].double(), ys[0][0].double()) < 5e-2
     assert _rel(ys[1][1].double(), ys[0][1].double()) < 5e-2
+
+
+@pytest.mark.parametrize("vt", [True, False])
+@pytest.mark.parametrize("BH,Nc,Ns,scale", [(2, 300, 700, 0.5), (3, 97, 33, 1.0), (1, 512, 4096, 0.35),
+                                            (2, 256, 130, 2.5)])
+def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, vt, BH, Nc, Ns, scale):
+    """Both training forwards — mhada_attn_train_fwd_vt (the inference fp32 structure: 64-key tiles,
+    lazy rescale, V'^T | V'^2^T image; the default) and the round-1 mhada_attn_train_fwd — against
+    fp64: out', [M' | E2'] and lse2 (exact although the running max is rescaled lazily), ragged
+    key tiles, peaky logits (scale 2.5: the max moves late and by a lot)."""
+    monkeypatch.setattr(ops, "TRAIN_FWD_VT", vt)
+    g = torch.Generator().manual_seed(BH * 100 + Ns)
+    q = torch.randn(BH, Nc, 64, generator=g) * scale
+    k = torch.randn(BH, Ns, 64, generator=g) * scale
+    v = torch.randn(BH, Ns, 64, generator=g) * 2
+    v = v - v.mean(dim=1, keepdim=True)
+    x = torch.randn(BH, Nc, 64, generator=g)
+    out, mo, lse = ops.attn_train_fwd(*(t.cuda().contiguous() for t in (q, k, v, x)))
+    qd, kd, vd = q.double(), k.double(), v.double()
+    s = qd @ kd.transpose(1, 2)
+    a = torch.softmax(s, -1)
+    assert torch.allclose(lse.double().cpu(), torch.logsumexp(s, -1) / torch.log(torch.tensor(2.0, dtype=torch.float64)),
+                          atol=2e-4, rtol=1e-5)
+    assert _rel(mo[..., :64].double().cpu(), a @ vd) < 2e-5
+    assert _rel(mo[..., 64:].double().cpu(), a @ vd ** 2) < 2e-5
+    assert _rel(out.double().cpu(), _ref(qd, kd, vd, x.double())) < 2e-4

@@ -112,6 +112,34 @@ def test_conv3x3_fwd_bwd(pad_mode, B, H, W, Ci, Co, cx):
     assert rel(conv.bias.grad, b64.grad) < 1e-5
 
 
+@pytest.mark.parametrize("pad_mode", ["reflect", "zero"])
+@pytest.mark.parametrize("B,H,W,C", [(2, 12, 10, 64), (1, 7, 9, 128)])
+def test_conv_chain_relu_adjoint_folded_into_dgrad(pad_mode, B, H, W, C):
+    """conv a -> ReLU -> conv b with a's ReLU adjoint folded into b's input gradient (Conv3x3Fn
+    grad_masked on a, relu_input on b: the Winograd dgrad's output stage / the reflect fold zero
+    it where a's output is <= 0) gives the bits of the unfolded chain (relu_bwd pass in a)."""
+    x = rnd(B, H, W, C, seed=41)
+    convs = []
+    for i in range(2):
+        conv = torch.nn.Conv2d(C, C, 3).to(DEV)
+        with torch.no_grad():
+            conv.weight.copy_(rnd(C, C, 3, 3, seed=42 + i, scale=(9 * C) ** -0.5))
+            conv.bias.copy_(rnd(C, seed=44 + i, scale=0.1))
+        convs.append(conv)
+    gy = rnd(B, H, W, C, seed=46)
+    grads = []
+    for fold in (False, True):
+        xg = x.clone().requires_grad_(True)
+        h = train_fns.conv3x3(xg, convs[0], pad_mode, relu=True, grad_masked=fold)
+        y = train_fns.conv3x3(h, convs[1], pad_mode, relu=True, relu_input=fold)
+        for c in convs:
+            c.weight.grad = c.bias.grad = None
+        y.backward(gy)
+        grads.append([xg.grad] + [t.grad.clone() for c in convs for t in (c.weight, c.bias)])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 def test_maxpool2_fwd_bwd_with_ties():
     # post-ReLU activations: many zeros, so the first-maximum rule decides most windows
     x = F.relu(rnd(2, 16, 18, 64, seed=5))

@@ -19,7 +19,7 @@ for v in bits:
         [ctypes.c_int] * 3 + [ctypes.c_void_p]
     lib.mhada_wino_weights.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     assert lib.mhada_wino_weights(w.data_ptr(), u.data_ptr(), Co, Ci, st) == 0
-    f = lambda: lib.mhada_conv3x3_wino(x.data_ptr(), u.data_ptr(), None, y.data_ptr(), B, H, H, Ci, Co, Co, 0, 1, 1, st)  # noqa
+    f = lambda: lib.mhada_conv3x3_wino(x.data_ptr(), u.data_ptr(), None, y.data_ptr(), B, H, H, Ci, Co, Co, 0, 1, 1, None, st)  # noqa
     f(); torch.cuda.synchronize()
     ts = []
     for _ in range(15):

@@ -30,7 +30,7 @@ for (B, H, Ci, Co, pm) in [(8, 128, 256, 256, 0), (8, 512, 64, 64, 0), (8, 256, 
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(5):
-                lib.mhada_conv3x3_wino(x.data_ptr(), u.data_ptr(), None, ys[v].data_ptr(), B, H, H, Ci, Co, Co, pm, 1, 1, st)
+                lib.mhada_conv3x3_wino(x.data_ptr(), u.data_ptr(), None, ys[v].data_ptr(), B, H, H, Ci, Co, Co, pm, 1, 1, None, st)
             e.record()
             torch.cuda.synchronize()
             if r:
