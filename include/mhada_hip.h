@@ -86,6 +86,9 @@ typedef struct mhada_gemm_args {
   const float* bias; long long sb1, sb2;
   const void* r; int r_dtype; long long ldr, sr1, sr2;
   void* c; int c_dtype; long long ldc, sc1, sc2;
+  /* 1: ReLU after the bias (before a residual).  2 (ABI 10): ReLU-adjoint mask — r is not added
+   * but read as a mask of C's layout: C = 0 where r <= 0 (a gradient GEMM whose input was a ReLU
+   * output consumed only by the forward of this layer; fp32 C and r, ROWS mode). */
   int relu;
   int pad;      /* CONV3X3_ZERO only: 1 or 2 (0 = 1) */
   /* Optional second output (NULL = none): a bf16 copy of C (row stride ldc2, z-strides

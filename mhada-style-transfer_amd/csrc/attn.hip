@@ -126,6 +126,28 @@ MHADA_DEV void scale_acc(f32x16 (&O)[4], float alpha) {
 }
 
 
+// In-kernel clock (MI355X_MICROARCH.md, DVFS give-back item 6), diagnostic builds only
+// (-DATTN_CLOCK, tools/attn_clock.py): thread 0 of each workgroup stamps the shader-clock and the
+// 100 MHz real-time counters before and after the key loop into a buffer of their own; no output
+// is computed from them.  In the shipped build ATTN_STAMP expands to nothing.
+#ifdef ATTN_CLOCK
+constexpr int kClockBlocks = 65536;
+__device__ unsigned long long g_attn_clock[4 * kClockBlocks];
+#define ATTN_STAMP(slot)                                                                     \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < kClockBlocks) {                                     \
+      const unsigned long long c_ = __builtin_amdgcn_s_memtime();                           \
+      const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                       \
+      g_attn_clock[4 * blockIdx.x + 2 * (slot)] = c_;                                        \
+      g_attn_clock[4 * blockIdx.x + 2 * (slot) + 1] = r_;                                    \
+    }                                                                                        \
+  } while (0)
+#else
+#define ATTN_STAMP(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 // Training epilogue (attn_train.hip's forward contract): out' = sqrt(max(E2' - M'^2, 1e-6)) x + M',
 // mo = [M' | E2'], lse2 = m2 + log2(l) per query row; x = p.fcs [BH][Nc][64].
 MHADA_DEV void attn_train_epilogue(const AttnP& p, const f32x16 (&O)[4], float l, float m2, long long bh, int q,
@@ -296,6 +318,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
   issue(0);
   commit(0);
   __syncthreads();
+  ATTN_STAMP(0);
   // Full tiles.  The rescale (P <= 2^kRescaleThr, so after the first tile it is rare) is a
   // wave-uniform branch inside the single loop: one register assignment for the O accumulators
   // (a leave-rescale-reenter loop made the compiler copy all of O between two register sets on
@@ -330,6 +353,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_f32_kernel(cons
     if (softmax_tile<ACT, 2>(S, m2, l, alpha)) scale_acc(O, alpha);
     pv(sV[cb], S);
   }
+  ATTN_STAMP(1);
   if constexpr (TRAIN) attn_train_epilogue(p, O, l, m2, bh, q, h);
   else attn_epilogue<float>(p, O, l, b, hh, q, h);
 }
@@ -644,8 +668,8 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 }
 
 // --------------------------------------------------------------------------------------
-// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3, the bf16 softmax default when
-// Ns % 128 == 0; 4.5 % faster than register staging at 1024^2 B4): attn_bf16_fs_kernel's loop with
+// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3; the bf16 softmax default of round
+// 3, 4.5 % faster than register staging at 1024^2 B4; round 4's default is its 16x16x32 form fsq1): attn_bf16_fs_kernel's loop with
 // the K / V'^T tiles staged by global_load_lds (16 B per lane) instead of through registers: no
 // staging registers, no LDS write pass, the next tile's DMA in flight for the whole iteration
 // (hipcc sinks the register-staged kernel's global loads next to their LDS writes).  LDS images
@@ -657,28 +681,6 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 // vmcnt(0) before the one barrier per tile.  Whole key tiles only.  (A second score set for
 // cross-tile pipelining at 128 keys spilled; attn_bf16_fsh_kernel pipelines by half tiles.)
 // --------------------------------------------------------------------------------------
-// In-kernel clock (MI355X_MICROARCH.md, DVFS give-back item 6), diagnostic builds only
-// (-DATTN_CLOCK, tools/attn_clock.py): thread 0 of each workgroup stamps the shader-clock and the
-// 100 MHz real-time counters before and after the key loop into a buffer of their own; no output
-// is computed from them.  In the shipped build ATTN_STAMP expands to nothing.
-#ifdef ATTN_CLOCK
-constexpr int kClockBlocks = 65536;
-__device__ unsigned long long g_attn_clock[4 * kClockBlocks];
-#define ATTN_STAMP(slot)                                                                     \
-  do {                                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < kClockBlocks) {                                     \
-      const unsigned long long c_ = __builtin_amdgcn_s_memtime();                           \
-      const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                       \
-      g_attn_clock[4 * blockIdx.x + 2 * (slot)] = c_;                                        \
-      g_attn_clock[4 * blockIdx.x + 2 * (slot) + 1] = r_;                                    \
-    }                                                                                        \
-  } while (0)
-#else
-#define ATTN_STAMP(slot) \
-  do {                   \
-  } while (0)
-#endif
-
 MHADA_DEV void attn_glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -998,7 +1000,12 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p
 //       permutation costs only the K row address, no lane movement, no second vt layout.
 // K image: chunk c of key row k at 16-B slot c ^ (k & 7) (conflict-free for these row sets
 // under the ds_read_b128 lane groups of MI355X_MICROARCH.md's LDS table); V'^T as in fsg.
-// ONES (attn_sched = 7): the row sum l comes out of one extra MFMA per (32 keys, 16 queries)
+// Measured (tools/attn_clock.py, profiles/r04_attn_clock.log, 1024^2 B4): the 32x32x16 kernel (fsg)
+// holds 1.78-1.83 GHz at 0.62-0.63 of the clock-adjusted peak; this shape holds 2.15-2.19 GHz at
+// 0.54-0.55 (the 16-cycle MFMA blocks vector issue for 8 of its 16 cycles, so the softmax VALU
+// competes harder); net fsq 3 %, fsq1 4-6 % faster than fsg.
+// ONES (attn_sched = 7, the bf16 softmax default when Ns % 128 == 0): the row sum l comes out of
+// one extra MFMA per (32 keys, 16 queries)
 // with an all-ones A operand (D rows = sum_k P[k][q]), removing the 64 v_add_f32 per tile and
 // lane from the VALU stream at +8 MFMAs (72 instead of 64 PV MFMAs per tile and wave); l is then
 // the sum of the bf16-rounded P that the PV products use.
@@ -1284,6 +1291,9 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p
 
 // --------------------------------------------------------------------------------------
 // Persistent form of the fsq kernel with the all-ones row sum ("fsp", tuning attn_sched = 8):
+// (Measured SLOWER than fsq1: 2.95 vs 2.65 ms at 1024^2 B4 although it holds 2.36 GHz — its
+// loop compiles to 403 instead of 317 instructions (45 waits, 26 register moves for the
+// cur / next block state); kept as an A/B variant.)
 // one workgroup per CU walks the (b, h, query-block) blocks w, w + G, w + 2G, ... (the hardware
 // block ids a one-shot launch would use, so xcd_remap keeps the 32 workgroups of an XCD on 32
 // query blocks of one (b, h): K / V' shared in its L2), and the K / V'^T tile stream is continuous

@@ -42,7 +42,9 @@ struct Tuning {
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
-  int attn_sched = 3;        // bf16 fixed-shift attention (Ns % 128 == 0): 3 LDS-DMA staging, 5 half-tile
+  int attn_sched = 7;        // bf16 fixed-shift attention (Ns % 128 == 0): 7 LDS-DMA staging on 16x16x32
+                             // MFMAs with the all-ones row sum (fsq1, round 4), 6 the same with VALU row
+                             // sums, 8 its persistent form, 3 LDS-DMA on 32x32x16 (fsg), 5 half-tile
                              // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it

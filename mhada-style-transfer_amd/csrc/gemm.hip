@@ -42,6 +42,10 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   p.bias = a->bias; p.sb1 = a->sb1; p.sb2 = a->sb2;
   p.r = a->r; p.ldr = a->ldr; p.sr1 = a->sr1; p.sr2 = a->sr2;
   p.c = a->c; p.ldc = a->ldc; p.sc1 = a->sc1; p.sc2 = a->sc2;
+  if (a->relu < 0 || a->relu > 2) return fail("mhada_gemm: relu must be 0, 1 or 2");
+  if (a->relu == 2 && (!a->r || a->r_dtype != MHADA_F32 || a->c_dtype != MHADA_F32 || a->c2 || a->vt ||
+                       a->a_mode != MHADA_A_ROWS))
+    return fail("mhada_gemm: relu = 2 (ReLU-adjoint mask) needs fp32 C, an fp32 mask in r, ROWS mode, no c2 / vt");
   p.relu = a->relu;
   p.c2 = a->c2; p.ldc2 = a->ldc2; p.sc21 = a->sc21; p.sc22 = a->sc22;
   p.vt = a->vt; p.ldt = a->ldt; p.svt1 = a->svt1; p.svt2 = a->svt2;

@@ -259,7 +259,7 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += bb[e];
           }
-          if (p.relu) {
+          if (p.relu == 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
           }
@@ -267,7 +267,7 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
             if (rrow) {
               const f32x4 rr = *reinterpret_cast<const f32x4*>(rrow + n);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += rr[e];
+              for (int e = 0; e < 4; ++e) v[e] = p.relu == 2 ? (rr[e] > 0.f ? v[e] : 0.f) : v[e] + rr[e];
             }
             *reinterpret_cast<f32x4*>(crow + n) = f32x4{v[0], v[1], v[2], v[3]};
             if (p.c2)
@@ -286,8 +286,8 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
           for (int e = 0; e < 4; ++e) {
             if (n + e < p.N) {
               float x = v[e] + (bbase ? bbase[n + e] : 0.f);
-              if (p.relu) x = fmaxf(x, 0.f);
-              if (rrow) x += to_f32<TO>(rrow[n + e]);
+              if (p.relu == 1) x = fmaxf(x, 0.f);
+              if (rrow) x = p.relu == 2 ? (to_f32<TO>(rrow[n + e]) > 0.f ? x : 0.f) : x + to_f32<TO>(rrow[n + e]);
               crow[n + e] = from_f32<TO>(x);
             }
           }
@@ -349,7 +349,7 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           x[e] = v[i][e] + bb[e];
-          if (p.relu) x[e] = fmaxf(x[e], 0.f);
+          if (p.relu == 1) x[e] = fmaxf(x[e], 0.f);
         }
         TO* crow = cbase + (long long)m * p.ldc;
         const TO* rrow = rbase ? rbase + (long long)m * p.ldr : nullptr;
@@ -358,7 +358,7 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
             if (rrow) {
               const f32x4 q = *reinterpret_cast<const f32x4*>(rrow + n);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) x[e] += q[e];
+              for (int e = 0; e < 4; ++e) x[e] = p.relu == 2 ? (q[e] > 0.f ? x[e] : 0.f) : x[e] + q[e];
             }
             *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
             if (p.c2)
@@ -375,7 +375,11 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if (n + e < p.N) crow[n + e] = from_f32<TO>(x[e] + (rrow ? to_f32<TO>(rrow[n + e]) : 0.f));
+            if (n + e < p.N) {
+              float y = x[e];
+              if (rrow) y = p.relu == 2 ? (to_f32<TO>(rrow[n + e]) > 0.f ? y : 0.f) : y + to_f32<TO>(rrow[n + e]);
+              crow[n + e] = from_f32<TO>(y);
+            }
           }
         }
       }
@@ -505,7 +509,7 @@ MHADA_DEV void store_tile_lds_bf16(const GemmP& p, const f32x16 (&acc)[TM][2], i
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = acc[mi][ni][4 * g + e] + bb[ni][g][e];
-          if (p.relu) x = fmaxf(x, 0.f);
+          if (p.relu == 1) x = fmaxf(x, 0.f);
           o[e] = (bf16)x;
         }
         const int c = 4 * ni + g;

@@ -108,11 +108,20 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
-           residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
-    """x [M][K] @ w[N][K]^T + bias (+relu) (+residual) -> [M][N] of out_dtype."""
+           residual: Optional[torch.Tensor] = None, relu: bool = False,
+           relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [M][K] @ w[N][K]^T + bias (+relu) (+residual) -> [M][N] of out_dtype.  ``relu_mask``
+    (fp32 [M][N], instead of a residual): the result is zeroed where relu_mask <= 0 (a ReLU
+    adjoint folded into a gradient GEMM's epilogue, mhada_gemm relu = 2)."""
     M, K = x.shape
     N = w.shape[0]
     c = torch.empty(M, N, device=x.device, dtype=out_dtype)
+    if relu_mask is not None:
+        if residual is not None or relu or out_dtype != torch.float32 or relu_mask.dtype != torch.float32 \
+                or relu_mask.shape != (M, N) or not relu_mask.is_contiguous():
+            raise ValueError("linear: relu_mask needs fp32 output, a contiguous fp32 [M][N] mask, no residual / relu")
+        return gemm(a=x, w=w, c=c, M=M, N=N, K=K, compute=w.dtype, lda=x.stride(0), ldw=w.stride(0),
+                    bias=bias, r=relu_mask, ldr=N, ldc=N, relu=2)
     return gemm(a=x, w=w, c=c, M=M, N=N, K=K, compute=w.dtype, lda=x.stride(0), ldw=w.stride(0),
                 bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)
 

@@ -174,22 +174,24 @@ class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear layout)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool):
+    def forward(ctx, x, weight, bias, relu: bool, grad_masked: bool = False, relu_input: bool = False):
         x = x.contiguous()
         y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu)
-        ctx.save_for_backward(x, weight, y if relu else None)
-        ctx.relu = relu
+        ctx.save_for_backward(x, weight, y if (relu and not grad_masked) else None)
+        # grad_masked: y's only consumer is a LinearFn(relu_input=True), whose input-gradient GEMM
+        # applies this ReLU's adjoint in its epilogue (mhada_gemm relu = 2): no relu_bwd pass here
+        ctx.relu, ctx.grad_masked, ctx.relu_input = relu, grad_masked, relu_input
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight, y = ctx.saved_tensors
         g = gy.contiguous()
-        if ctx.relu:
+        if ctx.relu and not ctx.grad_masked:
             g = ops.relu_bwd(g, y)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = ops.linear(g, weight.detach().t().contiguous(), None, F32)
+            gx = ops.linear(g, weight.detach().t().contiguous(), None, F32, relu_mask=x if ctx.relu_input else None)
         if ctx.needs_input_grad[1]:
             M, N = g.shape
             gw, cs = ops.gemm_tn(g, x, M=N, N=x.shape[1], K=M, lda=N, ldb=x.shape[1], b_mode=A_ROWS, colsum=True)
@@ -197,11 +199,12 @@ class LinearFn(torch.autograd.Function):
                 gb = cs
         elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None, None
 
 
-def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bool = False) -> torch.Tensor:
-    return LinearFn.apply(x2d, weight, bias, relu)
+def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bool = False,
+           grad_masked: bool = False, relu_input: bool = False) -> torch.Tensor:
+    return LinearFn.apply(x2d, weight, bias, relu, grad_masked, relu_input)
 
 
 class InstanceNormTokensFn(torch.autograd.Function):

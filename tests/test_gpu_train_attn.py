@@ -201,4 +201,8 @@ def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, vt, BH, Nc, Ns, scale):
                           atol=2e-4, rtol=1e-5)
     assert _rel(mo[..., :64].double().cpu(), a @ vd) < 2e-5
     assert _rel(mo[..., 64:].double().cpu(), a @ vd ** 2) < 2e-5
-    assert _rel(out.double().cpu(), _ref(qd, kd, vd, x.double())) < 2e-4
+    # out' = sqrt(E2' - M'^2) x + M' cancels where the variance is small: held to the error of the
+    # reference expression's own fp32 evaluation on the same inputs (x4), with a 2e-4 floor
+    ref = _ref(qd, kd, vd, x.double())
+    err32 = _rel(_ref(q, k, v, x).double(), ref)
+    assert _rel(out.double().cpu(), ref) < max(2e-4, 4 * err32)

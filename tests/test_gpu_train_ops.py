@@ -332,6 +332,25 @@ def test_linear_fn_fwd_bwd(M, K, N, relu):
         assert rel(a, b_) < 1e-5
 
 
+def test_mlp_relu_adjoint_folded_into_dgrad_gemm():
+    """ViT MLP: Linear(ReLU) -> Linear with the first layer's ReLU adjoint applied in the second
+    layer's input-gradient GEMM epilogue (mhada_gemm relu = 2, the mask in r) gives the bits of the
+    unfolded pair (relu_bwd pass), odd N included."""
+    for M, K, N in ((1000, 512, 2048), (77, 64, 70)):
+        x = rnd(M, K, seed=51)
+        w1, b1 = rnd(N, K, seed=52, scale=K ** -0.5), rnd(N, seed=53)
+        w2, b2 = rnd(K, N, seed=54, scale=N ** -0.5), rnd(K, seed=55)
+        gy = rnd(M, K, seed=56)
+        res = []
+        for fold in (False, True):
+            ps = [t.clone().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+            h = train_fns.linear(ps[0], ps[1], ps[2], relu=True, grad_masked=fold)
+            train_fns.linear(h, ps[3], ps[4], relu_input=fold).backward(gy)
+            res.append([t.grad for t in ps])
+        for a, b in zip(*res):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,H,W", [(2, 64, 64), (3, 72, 128)])
 def test_patch_embed_fn_weight_grad(B, H, W):
     img = (torch.rand(B, 3, H, W, generator=torch.Generator().manual_seed(25)) * 255).to(DEV)

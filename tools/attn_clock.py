@@ -7,7 +7,7 @@ back to back for >= 2 s on random data at 1024^2 B4, then reads the last launch'
 clock = d(shader clock) / d(real time) x 100 MHz, median over workgroups.  Also prints the wall
 time per launch (HIP events) and the loop's share of the workgroup lifetime.
 
-    python tools/attn_clock.py [variant ...]        (default: fsg fsq fsq1)
+    python tools/attn_clock.py [variant ...]        (default: fsg fsq1 fsp; "f32": the fp32 kernel at 512^2 B8)
 """
 import ctypes
 import os
@@ -33,9 +33,11 @@ def main():
     lib.mhada_dbg_attn_clock.argtypes = [ctypes.c_void_p, ctypes.c_int]
     names = sys.argv[1:] or ["fsg", "fsq1", "fsp"]
     torch.manual_seed(0)
-    B, H, nc, ns = 4, 8, 16384, 16384
-    q = (torch.randn(B, H, nc, 64, device="cuda") * 0.35).bfloat16()
-    kv = (torch.randn(B, H, ns, 128, device="cuda") * 0.35).bfloat16()
+    f32 = names == ["f32"]  # the fp32 kernel at 512^2 B8 (the headline's attention)
+    B, H, nc, ns = (8, 8, 4096, 4096) if f32 else (4, 8, 16384, 16384)
+    dt = torch.float32 if f32 else torch.bfloat16
+    q = (torch.randn(B, H, nc, 64, device="cuda") * 0.35).to(dt)
+    kv = (torch.randn(B, H, ns, 128, device="cuda") * 0.35).to(dt)
     vt = ops.transpose_v(kv)
     fcs = torch.randn(B, nc, 512, device="cuda")
     mu, rs = ops.instnorm_stats(fcs)
@@ -44,7 +46,7 @@ def main():
     flop = 6.0 * nc * ns * 512 * B
     for rnd in range(2):
         for v in names:
-            with _lib.tuning(**VARIANTS[v]):
+            with _lib.tuning(**VARIANTS.get(v, {})):
                 run = lambda: ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)  # noqa: E731
                 t0 = time.time()
                 n = 0
@@ -72,7 +74,8 @@ def main():
             print(f"round {rnd} {v:5s} {ms:.3f} ms/launch  {flop / ms / 1e9:7.1f} TF/s  in-kernel clock "
                   f"{ghz:.3f} GHz (median of {ok.sum()} workgroups; p10 {np.percentile(dclk[ok] / drt[ok], 10) * 0.1:.3f},"
                   f" p90 {np.percentile(dclk[ok] / drt[ok], 90) * 0.1:.3f})  loop {loop_us:.1f} us/workgroup  "
-                  f"{flop / ms / 1e9 / (ghz * 1024 * 1024 * 1e-3):.3f} of the clock-adjusted bf16 peak", flush=True)
+                  f"{flop / ms / 1e9 / (ghz * 1024 * (64 if f32 else 1024) * 1e-3):.3f} of the clock-adjusted "
+                  f"{'fp32' if f32 else 'bf16'} peak", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,25 @@
+# One gpurun call for a batch of round-4 checks; every GPU step under its own time limit, chained
+# so that a failure (fault, abort, time-out) ends the call.  usage: bash tools/gpu_batch.sh <tag> <step>...
+#   attn       attention variant tests + A/B + in-kernel clocks (bf16 variants and fp32)
+#   c64        decoder conv3.0 fused vs split upsample (tools/c64_ab.py)
+#   newtests   the round-4 GPU tests (ingest, graphs, training forward / folds / 512^2 B1 losses)
+#   gpu        the whole pytest -m gpu suite
+#   bench      the default bench line
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+for s in "$@"; do
+  case $s in
+    attn) bash tools/gpu_attn.sh $TAG tests ab clock || exit 1
+          timeout -k 10 120 python -u tools/attn_clock.py f32 > $OUT/attn_clock_f32.log 2>&1 || exit 1 ;;
+    c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
+    newtests) timeout -k 10 900 $PYT tests/test_ingest.py tests/test_gpu_parity.py tests/test_gpu_train_attn.py tests/test_gpu_train_ops.py tests/test_gpu_train.py tests/test_gpu_kernels.py -k "ingest or graphed or default_path or full_size or fwd_kernels or chain or vgg19_and_decoder or 512_b1 or golden or n64" > $OUT/new_tests.log 2>&1 || exit 3 ;;
+    gpu) timeout -k 10 1000 $PYT tests > $OUT/gpu_tests.log 2>&1 || exit 4 ;;
+    bench) timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1 || exit 5 ;;
+  esac
+done
+echo "gpu_batch $TAG done"
