@@ -295,9 +295,10 @@ int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int 
  * (replaces the ATen backward of lossfn.py:7-23 mean/std distances and lossfn.py:26-34,41-47 MSEs):
  *   g = alpha[b][c] + beta[b][c] * (x - mu[b][c]) + ks * kp[0] * (x - t)
  * alpha / beta / mu [B][C] (all null: no statistics term), t [B][P][C] (null: no MSE term), kp a
- * device scalar (null: 1); C % 4 == 0, 16-byte aligned pointers. */
+ * device scalar (null: 1); C % 4 == 0, 16-byte aligned pointers.  relu = 1 (ABI 10): x is a ReLU
+ * output and g is multiplied by its adjoint (x > 0) (the producing conv then skips mhada_relu_bwd). */
 int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha, const float* beta,
-                        const float* kp, float ks, float* g, int B, long long P, int C, mhada_stream_t stream);
+                        const float* kp, float ks, float* g, int B, long long P, int C, int relu, mhada_stream_t stream);
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */
 int mhada_relu_bwd(const float* dy, const float* y, float* dx, long long n, mhada_stream_t stream);
 /* Adjoint of ReflectionPad2d(1) (conv.py:27,31): dxp [B][H+2][W+2][C] (the full-correlation

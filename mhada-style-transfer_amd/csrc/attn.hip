@@ -1516,6 +1516,13 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
     else
       hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
   } else {
+    if constexpr (NW == 4) {  // small grids (mhada_attn): the 16x16x32 fixed-shift kernel at 4 waves
+      if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift() && tuning().attn_sched == 7 &&
+          p.Ns % 128 == 0) {
+        hipLaunchKernelGGL((attn_bf16_fsq_kernel<4, true>), grid, blk, 0, s, p);
+        return;
+      }
+    }
     if constexpr (NW == 8) {
       if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift()) {
         if (tuning().attn_sched == 3 && p.Ns % 128 == 0) {  // LDS-DMA staging, 128-key tiles
@@ -1574,7 +1581,10 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   p.prio = tuning().attn_prio;
   p.ldk = 128;
   p.ldt = (Ns + 63) / 64 * 64;
-  const int nw = attn_waves(dtype);
+  int nw = attn_waves(dtype);
+  // a grid of 8-wave blocks smaller than the CU count (B = 1 at 512^2: 128 blocks) leaves CUs idle:
+  // 4-wave blocks cover twice as many CUs (one wave per SIMD instead of two)
+  if (nw == 8 && (long long)B * H * ((Nc + 255) / 256) < attn_num_cus()) nw = 4;
   p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
   const long long nblk = (long long)B * H * p.nqb;
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn: grid too large");

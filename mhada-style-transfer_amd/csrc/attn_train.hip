@@ -58,6 +58,27 @@ struct TrainP {
   int Nc, Ns, nb, nblk;  // nb = row blocks per (b, h)
 };
 
+// In-kernel clock of the dK/dV' kernel, diagnostic builds only (-DATTN_CLOCK, tools/attn_clock.py
+// dkv): thread 0 of each workgroup stamps the shader clock and the 100 MHz counter around the
+// query loop into a buffer of its own (MI355X_MICROARCH.md, DVFS give-back item 6).
+#ifdef ATTN_CLOCK
+constexpr int kTrainClockBlocks = 65536;
+__device__ unsigned long long g_train_clock[4 * kTrainClockBlocks];
+#define TRAIN_STAMP(slot)                                                                    \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < kTrainClockBlocks) {                                \
+      const unsigned long long c_ = __builtin_amdgcn_s_memtime();                           \
+      const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                       \
+      g_train_clock[4 * blockIdx.x + 2 * (slot)] = c_;                                       \
+      g_train_clock[4 * blockIdx.x + 2 * (slot) + 1] = r_;                                   \
+    }                                                                                        \
+  } while (0)
+#else
+#define TRAIN_STAMP(slot) \
+  do {                    \
+  } while (0)
+#endif
+
 // Workgroup barrier for the LDS hand-off only: __syncthreads() also acts as a release fence
 // that drains every outstanding global store (vmcnt counts stores on CDNA4), which would
 // serialise the dS spill stores with the next tile.
@@ -382,6 +403,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   load(0);
   store(0);
   __syncthreads();
+  TRAIN_STAMP(0);
   const int nt = (p.Nc + TT - 1) / TT;
   for (int t = 0; t < nt; ++t) {
     const int cb = t & 1;
@@ -431,6 +453,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
     if (nxt) store(cb ^ 1);
     lds_barrier();
   }
+  TRAIN_STAMP(1);
   if (!kv) return;
   const long long row = bh * p.Ns + key;
   const float* vg = p.v + row * 64;
@@ -513,3 +536,13 @@ extern "C" int mhada_attn_train_dkv(const float* q, const float* k, const float*
   hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1, true>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
   return check_launch("mhada_attn_train_dkv");
 }
+
+#ifdef ATTN_CLOCK
+// Diagnostic builds: the first n stamps (4 per workgroup) of the last dK/dV' launch.
+extern "C" int mhada_dbg_train_clock(unsigned long long* host, int n) {
+  if (!host || n <= 0 || n > 4 * kTrainClockBlocks) return fail("mhada_dbg_train_clock: bad args");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_train_clock), sizeof(unsigned long long) * n) != hipSuccess)
+    return fail("mhada_dbg_train_clock: copy failed");
+  return MHADA_OK;
+}
+#endif

@@ -755,7 +755,7 @@ __global__ void __launch_bounds__(256) feat_loss_bwd_kernel(const float* __restr
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ kp, float ks,
                                                             float* __restrict__ g, long long PC4, int C4,
-                                                            long long n4) {
+                                                            long long n4, int relu) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
   const float k = kp ? ks * kp[0] : ks;
@@ -773,6 +773,10 @@ __global__ void __launch_bounds__(256) feat_loss_bwd_kernel(const float* __restr
     const f32x4 w = reinterpret_cast<const f32x4*>(t)[i];
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] += k * (v[e] - w[e]);
+  }
+  if (relu) {  // x is a ReLU output: its adjoint (x > 0) applied here
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v[e] > 0.f ? o[e] : 0.f;
   }
   reinterpret_cast<f32x4*>(g)[i] = o;
 }
@@ -1259,14 +1263,14 @@ extern "C" int mhada_relu_bwd(const float* dy, const float* y, float* dx, long l
 
 extern "C" int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha,
                                    const float* beta, const float* kp, float ks, float* g, int B, long long P,
-                                   int C, mhada_stream_t s_) {
+                                   int C, int relu, mhada_stream_t s_) {
   if (!x || !g || B <= 0 || P <= 0 || C <= 0 || C % 4 || !al16(x) || !al16(g) || (t && !al16(t)))
     return fail("mhada_feat_loss_bwd: bad args (C % 4 == 0, 16-byte aligned)");
   if (alpha && (!beta || !mu || !al16(alpha) || !al16(beta) || !al16(mu)))
     return fail("mhada_feat_loss_bwd: alpha needs beta and mu (16-byte aligned)");
   const long long n4 = (long long)B * P * (C / 4);
   hipLaunchKernelGGL(feat_loss_bwd_kernel, grid1(n4), dim3(256), 0, (hipStream_t)s_, x, t, mu, alpha, beta, kp, ks,
-                     g, P * (C / 4), C / 4, n4);
+                     g, P * (C / 4), C / 4, n4, relu);
   return check_launch("mhada_feat_loss_bwd");
 }
 

@@ -89,7 +89,7 @@ SIGNATURES = {
     "mhada_attn_train_bwd_prep": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
-    "mhada_feat_loss_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _F, _vp, _I, _c_ll, _I, _vp]),
+    "mhada_feat_loss_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _F, _vp, _I, _c_ll, _I, _I, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_maxpool2_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),

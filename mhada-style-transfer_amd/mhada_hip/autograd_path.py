@@ -287,14 +287,15 @@ def imagenet_normalize(x: torch.Tensor) -> torch.Tensor:
     return (x / 255.0 - mean) / std
 
 
-def vgg19_forward(vgg, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+def vgg19_forward(vgg, x: torch.Tensor, masked_features: bool = False) -> Dict[str, torch.Tensor]:
     """VGG19.forward (vgg19.py:42-70): relu1_1 .. relu5_1.  On a ROCm device: the HIP kernels
     (train_fns: zero-padded implicit-GEMM convs with fused ReLU, max-pool, fused normalise;
-    features are NCHW views of NHWC storage); on the CPU: aten."""
+    features are NCHW views of NHWC storage); on the CPU: aten.  masked_features: see
+    train_fns.vgg19_forward (the Trainer's fused feature losses)."""
     if x.is_cuda:
         from network.vgg19 import _CONVS, _POOLS, _SLICES
         from . import train_fns
-        return train_fns.vgg19_forward(vgg, x, {i for i, _, _ in _CONVS}, set(_POOLS), _SLICES)
+        return train_fns.vgg19_forward(vgg, x, {i for i, _, _ in _CONVS}, set(_POOLS), _SLICES, masked_features)
     x = imagenet_normalize(x)
     feats = {}
     for i in range(1, 6):

@@ -655,10 +655,10 @@ def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 
 def feat_loss_bwd(x: torch.Tensor, mu: Optional[torch.Tensor], alpha: Optional[torch.Tensor],
                   beta: Optional[torch.Tensor], t: Optional[torch.Tensor], ks: float,
-                  kp: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  kp: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
     """``mhada_feat_loss_bwd`` on NHWC storage x [B][H][W][C] fp32 (t the same shape, or None;
     mu / alpha / beta [B][C] fp32, or all None; kp a one-element fp32 device tensor or None):
-    alpha + beta (x - mu) + ks * kp (x - t)."""
+    alpha + beta (x - mu) + ks * kp (x - t), times (x > 0) with ``relu`` (x a ReLU output)."""
     _need_gpu(x)
     B, H, W, C = x.shape
     for u in (x, t, mu, alpha, beta, kp):
@@ -673,7 +673,7 @@ def feat_loss_bwd(x: torch.Tensor, mu: Optional[torch.Tensor], alpha: Optional[t
     g = torch.empty_like(x)
     ptr = lambda u: None if u is None else u.data_ptr()  # noqa: E731
     _call("mhada_feat_loss_bwd", x, x.data_ptr(), ptr(t), ptr(mu), ptr(alpha), ptr(beta), ptr(kp), float(ks),
-          g.data_ptr(), B, H * W, C)
+          g.data_ptr(), B, H * W, C, int(relu))
     return g
 
 

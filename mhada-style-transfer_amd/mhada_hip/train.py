@@ -39,6 +39,9 @@ class Trainer:
         self.batch_adaformer = True  # see losses()
         # one backward pass per VGG feature map for the gs / lf / id2 terms (HIP; see _feature_losses)
         self.fused_feature_losses = dev.type == "cuda"
+        # with the fused losses: the ReLU adjoints of the VGG feature maps relu2_1 .. relu5_1 applied by
+        # their consumers (FeatureLossFn / the next conv's dgrad) instead of a relu_bwd pass (bit-identical)
+        self.masked_vgg_features = True
         self.opt_vit_c = torch.optim.Adam(vit_c.parameters(), lr=lr)
         self.opt_vit_s = torch.optim.Adam(vit_s.parameters(), lr=lr)
         self.opt_ada = torch.optim.Adam(ada.parameters(), lr=lr)
@@ -89,9 +92,15 @@ class Trainer:
             _, ss = self.ada(fs_vc, fs_vs)
         vgg_fs = self.vgg(style)
         vgg_fc = self.vgg(content)
-        vgg_fcs = self.vgg(cs)
-        vgg_fcc = self.vgg(cc)
-        vgg_fss = self.vgg(ss)
+        if self.fused_feature_losses and self.masked_vgg_features:
+            # the three feature dicts that take gradients feed only _feature_losses' FeatureLossFn
+            # (relu_input=True): the ReLU adjoints of relu2_1 .. relu5_1 are applied by their consumers
+            from .autograd_path import vgg19_forward
+            vgg_fcs, vgg_fcc, vgg_fss = (vgg19_forward(self.vgg, x, masked_features=True) for x in (cs, cc, ss))
+        else:
+            vgg_fcs = self.vgg(cs)
+            vgg_fcc = self.vgg(cc)
+            vgg_fss = self.vgg(ss)
         if self.fused_feature_losses:
             gs, lf, id2 = self._feature_losses(vgg_fc, vgg_fs, vgg_fcs, vgg_fcc, vgg_fss)
             gs, lf, id2 = gs * LAMBDA_GS, lf * LAMBDA_LF, id2 * LAMBDA_ID2
@@ -113,12 +122,13 @@ class Trainer:
             t = None
             if i >= 3:  # lossfn.py:26-34: the AdaAttN target of the content / style features
                 t = self.no_learn[i - 3](fc[k], fs[k], L.feature_down_sample(fc, i), L.feature_down_sample(fs, i))
-            lm, ls, lmse = feature_loss_terms(fcs[k], fs[k].mean(dim=(2, 3)), fs[k].std(dim=(2, 3)), t)
+            m = i >= 2 and self.masked_vgg_features  # relu2_1 .. relu5_1 from vgg19_forward(masked_features=True)
+            lm, ls, lmse = feature_loss_terms(fcs[k], fs[k].mean(dim=(2, 3)), fs[k].std(dim=(2, 3)), t, relu_input=m)
             gs = gs + (lm + ls)  # lossfn.py:21: loss += mean_dist + std_dist
             if t is not None:
                 lf = lf + lmse
-            a = feature_loss_terms(fcc[k], t=fc[k])[2]
-            b = feature_loss_terms(fss[k], t=fs[k])[2]
+            a = feature_loss_terms(fcc[k], t=fc[k], relu_input=m)[2]
+            b = feature_loss_terms(fss[k], t=fs[k], relu_input=m)[2]
             id2 = id2 + a + b
         return gs, lf, id2
 

@@ -440,9 +440,12 @@ class FeatureLossFn(torch.autograd.Function):
     backward chains and the adds that sum the terms of a feature map."""
 
     @staticmethod
-    def forward(ctx, x, ref_mean, ref_std, t):
-        if any(ctx.needs_input_grad[1:]):
+    def forward(ctx, x, ref_mean, ref_std, t, relu_input: bool = False):
+        if any(ctx.needs_input_grad[1:4]):
             raise ValueError("FeatureLossFn: the reference statistics and the target take no gradient")
+        # relu_input: x is a ReLU output whose producer (a Conv3x3Fn(grad_masked=True), see
+        # vgg19_forward(masked_features=True)) leaves the ReLU adjoint to its consumers
+        ctx.relu_input = relu_input
         ctx.set_materialize_grads(False)
         zero = x.new_zeros(())
         lm = ls = lmse = zero
@@ -476,15 +479,18 @@ class FeatureLossFn(torch.autograd.Function):
             tt = t.permute(0, 2, 3, 1)
             tt = tt if tt.is_contiguous() else tt.contiguous()
         if alpha is None and tt is None:
-            return None, None, None, None
+            if ctx.relu_input:
+                raise RuntimeError("FeatureLossFn(relu_input=True) must return the masked gradient")
+            return None, None, None, None, None
         kp = g_mse.reshape(1).float().contiguous() if tt is not None else None
-        g = ops.feat_loss_bwd(xs, mu.contiguous() if alpha is not None else None, alpha, beta, tt, 2.0 / x.numel(), kp)
-        return g.permute(0, 3, 1, 2), None, None, None
+        g = ops.feat_loss_bwd(xs, mu.contiguous() if alpha is not None else None, alpha, beta, tt, 2.0 / x.numel(), kp,
+                              relu=ctx.relu_input)
+        return g.permute(0, 3, 1, 2), None, None, None, None
 
 
-def feature_loss_terms(x, ref_mean=None, ref_std=None, t=None):
+def feature_loss_terms(x, ref_mean=None, ref_std=None, t=None, relu_input: bool = False):
     """(l_mean, l_std, l_mse) of one feature map (FeatureLossFn)."""
-    return FeatureLossFn.apply(x, ref_mean, ref_std, t)
+    return FeatureLossFn.apply(x, ref_mean, ref_std, t, relu_input)
 
 
 def _cached_build(weight: torch.Tensor, key: tuple, build) -> torch.Tensor:
@@ -613,9 +619,12 @@ def decoder_forward(dec, x_nchw: torch.Tensor, order) -> torch.Tensor:
     return x.permute(0, 3, 1, 2).contiguous()
 
 
-def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, torch.Tensor]:
+def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices, masked_features: bool = False) -> Dict[str, torch.Tensor]:
     """VGG19.forward (vgg19.py:42-70) on the HIP kernels: relu1_1 .. relu5_1 as NCHW views of
-    NHWC storage."""
+    NHWC storage.  masked_features (the Trainer's fused losses only): the caller guarantees that every
+    gradient reaching a feature map relu2_1 .. relu5_1 comes from a FeatureLossFn(relu_input=True),
+    so the convs producing them skip their ReLU adjoint: the loss backward applies it, and the next
+    slice's first conv applies it in its dgrad (relu_input)."""
     x = None
     relu_to_pool = False
     relu_in = False
@@ -636,8 +645,9 @@ def vgg19_forward(vgg, img: torch.Tensor, convs, pools, slices) -> Dict[str, tor
                 # a conv whose ReLU output feeds only the next conv of the same slice (conv3_2, 3_3,
                 # 4_2, 4_3: not a slice end, so not a loss feature) leaves it to that conv's dgrad
                 chained = (i + 2) in convs and i + 2 < b and x.is_cuda
-                x = conv3x3(x, conv, "zero", relu=True, grad_masked=pooled or chained, relu_input=relu_in)
-                relu_in = chained
+                feature = masked_features and s >= 2 and i + 2 == b and x.is_cuda  # relu2_1 .. relu5_1
+                x = conv3x3(x, conv, "zero", relu=True, grad_masked=pooled or chained or feature, relu_input=relu_in)
+                relu_in = chained or feature
                 relu_to_pool = pooled
             elif i in pools:
                 x = MaxPool2Fn.apply(x, relu_to_pool)

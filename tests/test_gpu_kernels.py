@@ -454,7 +454,7 @@ def test_mhada_attn_bf16_tile_counts(kernel, B, Nc, Ns):
 def test_gemm_n64_ring_kernel(nz, M, N, K):
     """The fp32 N <= 64 LDS-DMA ring GEMM (the attention backward's dQ = dS K, the per-head 1x1
     convs): batched strided operands, bias, ReLU and residual epilogues against fp64, and against
-    the register-staged tile it replaces (unaligned rows)."""
+    the register-staged tile it replaces (K % 32 != 0)."""
     a = rnd(nz, M, K + 4, seed=11)[..., :K]  # row stride K + 4 (16-B aligned, not dense)
     w = rnd(nz, N, K, scale=K ** -0.5, seed=12)
     b = rnd(N, seed=13)
@@ -469,9 +469,11 @@ def test_gemm_n64_ring_kernel(nz, M, N, K):
     c2 = torch.zeros_like(c)
     ops.gemm(c=c2, bias=b, r=r, ldr=ldc, sr=(M * ldc, 0), relu=True, **args)
     assert rel(c2[..., :N], torch.relu(ref) + r[..., :N].double()) < TOL[torch.float32]
-    # rows that are not 16-B aligned (row stride K + 1) take the register-staged tile it replaces
-    a1 = rnd(nz, M, K + 1, seed=11)[..., :K]
-    a1.copy_(a)
+    # K % 32 != 0 (here K + 4) takes the register-staged tile the ring kernel replaces
+    a1 = rnd(nz, M, K + 4, seed=11)
+    w1 = rnd(nz, N, K + 4, scale=K ** -0.5, seed=15)
     c3 = torch.zeros_like(c)
-    ops.gemm(c=c3, bias=b, **dict(args, a=a1, lda=K + 1, sa=(M * (K + 1), 0)))
-    assert rel(c3[..., :N], ref) < TOL[torch.float32]
+    ops.gemm(c=c3, bias=b, **dict(args, a=a1, w=w1, K=K + 4, lda=K + 4, sa=(M * (K + 4), 0), ldw=K + 4,
+                                  sw=(N * (K + 4), 0)))
+    ref1 = a1.double() @ w1.double().transpose(1, 2) + b.double()
+    assert rel(c3[..., :N], ref1) < TOL[torch.float32]

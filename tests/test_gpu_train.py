@@ -59,6 +59,23 @@ def test_batched_adaformer_step_matches_per_call_step():
     np.testing.assert_allclose(grads[0], grads[1], rtol=1e-4, atol=1e-6 * grads[1].max())
 
 
+def test_relu_adjoint_folds_are_bit_identical():
+    """The ReLU adjoints folded into consumers (VGG feature maps into the loss backward and the next
+    conv's dgrad: Trainer.masked_vgg_features) give the bits of the relu_bwd passes they replace."""
+    from test_train_cpu import grad_summary
+    c = seeded_image(2, 96, 64, 71).cuda()
+    s = seeded_image(2, 96, 64, 72).cuda()
+    res = []
+    for masked in (False, True):
+        tr = Trainer(*build("cuda"))
+        tr.masked_vgg_features = masked
+        out = tr.backward(c, s)
+        res.append(([float(out[k].detach()) for k in ("loss_gs", "loss_lf", "loss_id1", "loss_id2")],
+                    [p.grad.clone() for m in (tr.vit_c, tr.vit_s, tr.ada) for p in m.parameters()]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
 def test_train_step_full_size_runs():
     tr = Trainer(*build("cuda"))
     c = seeded_image(8, 512, 512, 100).cuda()

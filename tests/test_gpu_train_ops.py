@@ -565,6 +565,15 @@ def test_feature_loss_fn_matches_aten_autograd(stats, target, B, C, H, W):
     for got, want in refs:
         assert abs(got.item() - want.item()) <= 1e-5 * abs(want.item())
     assert rel(x.grad, xd.grad) < 1e-5
+    # relu_input: x a ReLU output, the gradient leaves masked by (x > 0) — the bits of relu_bwd after it
+    xr = F.relu(x.detach()).requires_grad_(True)
+    lm, ls, lmse = train_fns.feature_loss_terms(xr, rm, rsd, t)
+    (w[0] * lm + w[1] * ls + w[2] * lmse).backward()
+    xm = xr.detach().clone().requires_grad_(True)
+    lm, ls, lmse = train_fns.feature_loss_terms(xm, rm, rsd, t, relu_input=True)
+    (w[0] * lm + w[1] * ls + w[2] * lmse).backward()
+    ref = ops.relu_bwd(xr.grad.permute(0, 2, 3, 1).contiguous(), xr.detach().permute(0, 2, 3, 1).contiguous())
+    assert torch.equal(xm.grad.permute(0, 2, 3, 1), ref)
 
 
 @pytest.mark.parametrize("pad_mode", ["reflect", "zero"])

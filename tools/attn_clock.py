@@ -27,11 +27,54 @@ VARIANTS = {"fsg": {"attn_fixed_shift": 1, "attn_sched": 3}, "fsh": {"attn_fixed
             "fsp": {"attn_fixed_shift": 1, "attn_sched": 8}}
 
 
+def train_dkv(lib):
+    """The training dK/dV' kernel at the 512^2 B8 step's shape (the three AdaFormer calls batched:
+    BH = 192, Nc = Ns = 4096), with its dS spill."""
+    lib.mhada_dbg_train_clock.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    torch.manual_seed(0)
+    BH, n = 192, 4096
+    q, k, v, x = (torch.randn(BH, n, 64, device="cuda") * 0.4 for _ in range(4))
+    v = (v - v.mean(dim=1, keepdim=True)).contiguous()
+    out, mo, lse = ops.attn_train_fwd(q, k, v, x)
+    dmo = torch.randn(BH, n, 128, device="cuda")
+    dd = (dmo * mo).sum(-1).contiguous()
+    ds = torch.empty(BH, n, n, device="cuda")
+    dk, dv = torch.empty_like(k), torch.empty_like(v)
+    st = torch.cuda.current_stream().cuda_stream
+    run = lambda: lib.mhada_attn_train_dkv(q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(),  # noqa: E731
+                                           dmo.data_ptr(), dd.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                                           ds.data_ptr(), BH, n, n, st)
+    flop = 768.0 * BH * n * n
+    nblk = BH * (n // 128)
+    for rnd in range(2):
+        t0, cnt = time.time(), 0
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        while time.time() - t0 < 2.0:
+            run()
+            cnt += 1
+            torch.cuda.synchronize()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / cnt
+        buf = np.zeros(4 * nblk, dtype=np.uint64)
+        assert lib.mhada_dbg_train_clock(buf.ctypes.data, 4 * nblk) == 0, lib.mhada_last_error()
+        st4 = buf.reshape(nblk, 4).astype(np.float64)
+        dclk, drt = st4[:, 2] - st4[:, 0], st4[:, 3] - st4[:, 1]
+        ok = drt > 0
+        ghz = np.median(dclk[ok] / drt[ok]) * 0.1
+        print(f"round {rnd} dkv   {ms:.3f} ms/launch  {flop / ms / 1e9:7.1f} TF/s  in-kernel clock {ghz:.3f} GHz "
+              f"(median of {ok.sum()} workgroups)  {flop / ms / 1e9 / (ghz * 1024 * 64 * 1e-3):.3f} of the "
+              f"clock-adjusted fp32 peak ({flop / ms / 1e9 / 157.3:.3f} of the nominal)", flush=True)
+
+
 def main():
     lib = _lib.load(os.path.join(REPO, "mhada-style-transfer_amd", "diag", "libmhada_clock.so"))
     _lib._lib = lib
     lib.mhada_dbg_attn_clock.argtypes = [ctypes.c_void_p, ctypes.c_int]
     names = sys.argv[1:] or ["fsg", "fsq1", "fsp"]
+    if names == ["dkv"]:
+        return train_dkv(lib)
     torch.manual_seed(0)
     f32 = names == ["f32"]  # the fp32 kernel at 512^2 B8 (the headline's attention)
     B, H, nc, ns = (8, 8, 4096, 4096) if f32 else (4, 8, 16384, 16384)

@@ -5,6 +5,8 @@
 #   newtests   the round-4 GPU tests (ingest, graphs, training forward / folds / 512^2 B1 losses)
 #   gpu        the whole pytest -m gpu suite
 #   bench      the default bench line
+#   trainclock in-kernel clock of the training dK/dV' kernel (diagnostic build)
+#   train / trainprof  the training step bench line / its rocprofv3 kernel trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=$1; shift
@@ -17,7 +19,10 @@ for s in "$@"; do
     attn) bash tools/gpu_attn.sh $TAG tests ab clock || exit 1
           timeout -k 10 120 python -u tools/attn_clock.py f32 > $OUT/attn_clock_f32.log 2>&1 || exit 1 ;;
     c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
-    newtests) timeout -k 10 900 $PYT tests/test_ingest.py tests/test_gpu_parity.py tests/test_gpu_train_attn.py tests/test_gpu_train_ops.py tests/test_gpu_train.py tests/test_gpu_kernels.py -k "ingest or graphed or default_path or full_size or fwd_kernels or chain or vgg19_and_decoder or 512_b1 or golden or n64" > $OUT/new_tests.log 2>&1 || exit 3 ;;
+    trainclock) timeout -k 10 180 python -u tools/attn_clock.py dkv > $OUT/train_clock.log 2>&1 || exit 6 ;;
+    train) timeout -k 10 400 python -u bench.py --train --steps 5 --warmup 2 > $OUT/train.log 2>&1 || exit 7 ;;
+    trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trainprof -o run -- python3 bench.py --train --steps 3 --warmup 1 > $OUT/trainprof.log 2>&1 || exit 8 ;;
+    newtests) timeout -k 10 900 $PYT tests/test_ingest.py tests/test_gpu_parity.py tests/test_gpu_train_attn.py tests/test_gpu_train_ops.py tests/test_gpu_train.py tests/test_gpu_kernels.py -k "ingest or graphed or default_path or full_size or fwd_kernels or chain or vgg19_and_decoder or 512_b1 or golden or n64 or bit_identical or feature_loss or mlp_relu or tile_counts or late_max" > $OUT/new_tests.log 2>&1 || exit 3 ;;
     gpu) timeout -k 10 1000 $PYT tests > $OUT/gpu_tests.log 2>&1 || exit 4 ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1 || exit 5 ;;
   esac
