@@ -27,6 +27,7 @@ reference's aten fp32 expression (tests/torch_ref.py, golden-pinned) at B=1 on t
 cores, with the numpy oracle beside it.
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -42,6 +43,22 @@ import torch.distributed as dist
 
 PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense MFMA peaks
 C = 512
+
+
+class _mark:
+    """A roctx range around a timed region ("bench:<config>:<steps>"): under `rocprofv3
+    --marker-trace --kernel-trace` tools/ktrace.py assigns each kernel to the config whose timed
+    region contains it (no profiler attached: a no-op)."""
+
+    def __init__(self, name: str, steps: int):
+        self.label = f"bench:{name}:{steps}"
+
+    def __enter__(self):
+        torch.cuda.nvtx.range_push(self.label)
+
+    def __exit__(self, *exc):
+        torch.cuda.nvtx.range_pop()
+        return False
 
 
 def max_over_ranks(x: float, world: int) -> float:
@@ -131,9 +148,10 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
         log = {}
         engine.record_kernel_events(log)
         t0 = time.perf_counter()
-        for _ in range(steps):
-            out = step()
-        torch.cuda.synchronize()
+        with _mark(f"{res}x{res}_b{batch}_{'f32' if dtype == torch.float32 else 'bf16'}", steps):
+            for _ in range(steps):
+                out = step()
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -206,9 +224,10 @@ def run_video(dtype, steps, warmup, rank, world):
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for t in range(warmup + 1, warmup + 1 + steps):
-            err = step(t)
-        torch.cuda.synchronize()
+        with _mark(f"video_1080p_{'f32' if dtype == torch.float32 else 'bf16'}", steps):
+            for t in range(warmup + 1, warmup + 1 + steps):
+                err = step(t)
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -247,25 +266,26 @@ def run_infer_time(dtype, warmup, runs=100):
         _, cs = ada(fc, fs)
         return cs.clamp(0, 255)
 
-    def probe(fn):
+    def probe(fn, tag):
         with torch.no_grad():
             for _ in range(warmup):
                 fn()
             torch.cuda.synchronize()
             total = 0.0
-            for _ in range(runs):
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                out = fn()
-                b.record()
-                torch.cuda.synchronize()
-                total += a.elapsed_time(b)
+            with _mark(f"infer_time_{'f32' if dtype == torch.float32 else 'bf16'}_{tag}", runs):
+                for _ in range(runs):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    out = fn()
+                    b.record()
+                    torch.cuda.synchronize()
+                    total += a.elapsed_time(b)
         return total / runs, out
 
-    t_eager, ref = probe(eager)
+    t_eager, ref = probe(eager, "eager")
     ref = ref.clone()
     g = GraphedStylizer(vc, vs, ada, (1, 3, 512, 512))
-    t_graph, out = probe(lambda: g(c, s))
+    t_graph, out = probe(lambda: g(c, s), "graph")
     dts = "f32" if dtype == torch.float32 else "bf16"
     return {"ms_per_frame": round(t_eager, 4), "ms_per_frame_graph": round(t_graph, 4),
             "launch_gap_share": round(1.0 - t_graph / t_eager, 4), "graph_bit_identical": bool(torch.equal(out, ref)),
@@ -296,9 +316,10 @@ def run_train(steps, warmup, rank, world, res=512, batch=8):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for c, s in data:
-        last = tr.step(c, s)
-    sync()
+    with _mark(f"train_{res}_b{batch}", steps) if dev.type == "cuda" else contextlib.nullcontext():
+        for c, s in data:
+            last = tr.step(c, s)
+        sync()
     if world > 1:
         dist.barrier()
     sync()
