@@ -476,6 +476,199 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// dK, dV' with the dS spill, LDS-DMA + software-pipelined form (round 4; the training default):
+// the same products in the same order as attn_train_dkv_kernel<.., SPILL> (bit-identical dK / dV'
+// / dS).  That kernel runs one wave per SIMD (288 registers) and measured 0.76 of the
+// clock-adjusted fp32 peak at 2.39 GHz (profiles/r04_train_dkv_clock.log): each tile's MFMA
+// stream stops for its softmax VALU (S -> P, dA -> dS), its dS stores, its staging writes and the
+// barrier.  Here:
+//   * iteration t runs tile t+1's first phase (S, dA = 96 MFMAs) while tile t's softmax VALU and
+//     dS stores fill the MFMA gaps, then tile t's second phase (G1, G2, dK = 96 MFMAs): the matrix
+//     pipe always has independent work (two S / dA register sets, one wave per SIMD);
+//   * the Q / dO / lse / D tiles arrive by LDS-DMA (global_load_lds) into a 3-slot ring — no
+//     staging registers or LDS write pass, one counted vmcnt that never waits on the dS stores;
+//     rows are XOR-swizzled on the source address (16-B chunk c of row r at slot c ^ (r & 15) of
+//     its 256-B bank row): the phase-1 ds_read_b128 (32 rows, one chunk) and the phase-2
+//     ds_read_b32 (one row, 32 consecutive floats) are conflict-free;
+//   * query rows past Nc load clamped rows with lse = +inf, D = 0 (P = 0).
+// 2 waves per SIMD (256 registers) was tried: 40+ spilled registers.
+// ---------------------------------------------------------------------------------------
+MHADA_DEV void train_glds(const float* src, float* lds, int bytes) {
+  if (bytes == 16)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+  else
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+// padding rows of the lse | D tile (query >= Nc): P = exp2(S - inf) = 0, D = 0
+__device__ float g_train_pad[2] = {INFINITY, 0.f};
+
+__global__ void __launch_bounds__(256, 1) attn_train_dkv_dma_kernel(const TrainP p) {
+  constexpr int NW = 4, NS = 3;
+  constexpr int QF = TT * 64, OF = TT * 128, SLOT = QF + OF + 2 * TT;  // floats per ring slot (24.8 KiB)
+  __shared__ __attribute__((aligned(16))) float smem[NS * SLOT];      // 74.5 KiB
+  const int t0 = xcd_remap(blockIdx.x, p.nblk);
+  const long long bh = t0 / p.nb;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int key = (t0 % p.nb) * 32 * NW + wave * 32 + r32;
+  const bool kv = key < p.Ns;
+  float kr[32], vr[32], vr2[32];
+  load_half_row(kr, p.k + bh * p.Ns * 64, key, kv, h, kLog2e);
+  load_half_row(vr, p.v + bh * p.Ns * 64, key, kv, h, 1.0f);
+#pragma unroll
+  for (int s2 = 0; s2 < 32; ++s2) vr2[s2] = vr[s2] * vr[s2];
+  const float* qb = p.q + bh * p.Nc * 64;
+  const float* ob = p.dmo + bh * p.Nc * 128;
+  const float* lb = p.lse + bh * p.Nc;
+  const float* db = p.dd + bh * p.Nc;
+  // DMA pieces (1 KiB = 64 lanes x 16 B) of this wave: Q rows 4 per piece (pieces 2w, 2w+1), dO
+  // rows 2 per piece (pieces 4w .. 4w+3); each lane fetches the global chunk its LDS slot holds
+  auto stage = [&](int q0, int sl) {  // tile q0 .. q0+31 into ring slot sl (rows clamped to Nc - 1)
+    float* d = smem + sl * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 4 * (2 * wave + i) + (lane >> 4);
+      train_glds(qb + (long long)min(q0 + row, p.Nc - 1) * 64 + 4 * ((lane & 15) ^ (row & 15)),
+                 d + (2 * wave + i) * 256, 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 2 * (4 * wave + i) + (lane >> 5);
+      train_glds(ob + (long long)min(q0 + row, p.Nc - 1) * 128 + 4 * (((lane >> 4) & 1) * 16 + ((lane & 15) ^ (row & 15))),
+                 d + QF + (4 * wave + i) * 256, 16);
+    }
+    // lse | D: lanes 0-31 / 32-63; padding queries read +inf / 0 (every wave issues the same
+    // piece, so every wave's wait counts are equal)
+    const int qi = q0 + r32;
+    train_glds(qi < p.Nc ? (h ? db : lb) + qi : g_train_pad + h, d + QF + OF, 4);
+  };
+  // phase-2 reads of row R = rowb(r) + 4h: logical float r32 (chunk r32 / 4) sits at physical
+  // 16-B slot (r32 / 4) ^ (R & 15) = 8 ((r >> 2) & 1) + ((r32 / 4) ^ ((r & 3) | 4h)); float 32 + r32
+  // at slot 8 (1 ^ ((r >> 2) & 1)) + the same low bits.  Per lane only (r & 3) varies: 4 offsets
+  // per operand (O and Q rows differ in length), the rest folds into the ds_read immediate.
+  int xo[4], xq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int lo = 4 * ((r32 >> 2) ^ (j | (4 * h))) + (r32 & 3);
+    xo[j] = 4 * h * 128 + lo;
+    xq[j] = 4 * h * 64 + lo;
+  }
+  const int sw1 = r32 & 15;
+  f32x16 G1[2] = {f32x16{}, f32x16{}}, G2[2] = {f32x16{}, f32x16{}}, dK[2] = {f32x16{}, f32x16{}};
+  const unsigned dkey = kv ? key * 4u : (unsigned)(p.Nc + TT) * p.Ns * 4;
+  const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(p.ds + bh * p.Nc * p.Ns, 0, p.Nc * p.Ns * 4,
+                                                                      0x00020000);
+  // phase 1 of the tile in ring slot sl: S (queries x keys) = Q . K^T, dA = [dM' | dE2'] . [V' | V'^2]^T
+  auto phase1 = [&](int sl, f32x16& S, f32x16& dA) {
+    const float* sQ = smem + sl * SLOT;
+    const float* qrw = sQ + r32 * 64;
+    const float* orw = sQ + QF + r32 * 128;
+    S = f32x16{};
+    dA = f32x16{};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = 4 * ((8 * h + i) ^ sw1);
+      const f32x4 qq = ld4(qrw + c), o1 = ld4(orw + c), o2 = ld4(orw + 64 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int s2 = 4 * i + e;
+        S = mfma(qq[e], kr[s2], S);
+        dA = mfma(o1[e], vr[s2], dA);
+        dA = mfma(o2[e], vr2[s2], dA);
+      }
+    }
+  };
+  // S -> P, dA -> dS in place (tile of ring slot sl, first query q0), and dS's spill stores
+  auto softmax = [&](int sl, int q0, f32x16& S, f32x16& dA) {
+    const float* sLD = smem + sl * SLOT + QF + OF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = acc_row(r, h);
+      S[r] = __builtin_amdgcn_exp2f(S[r] - sLD[qi]);
+      dA[r] = S[r] * (dA[r] - sLD[TT + qi]);
+    }
+    const unsigned base = (unsigned)(q0 + 4 * h) * p.Ns * 4 + dkey;  // dS [q][key]: 32 lanes write 128 B
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dA[r]), dsr,
+                                            (int)(base + ((r & 3) + 8 * (r >> 2)) * p.Ns * 4u), 0, 0);
+  };
+  // phase 2: G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
+  auto phase2 = [&](int sl, const f32x16& P, const f32x16& dS) {
+    const float* sQ = smem + sl * SLOT;
+    const float* sO = sQ + QF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = r & 3, rowb = (r & 3) + 8 * (r >> 2), b3 = (r >> 2) & 1;
+      const float* o = sO + xo[j] + rowb * 128;
+      const float* qq = sQ + xq[j] + rowb * 64;
+      G1[0] = mfma(o[32 * b3], P[r], G1[0]);
+      G1[1] = mfma(o[32 * (1 - b3)], P[r], G1[1]);
+      G2[0] = mfma(o[64 + 32 * b3], P[r], G2[0]);
+      G2[1] = mfma(o[64 + 32 * (1 - b3)], P[r], G2[1]);
+      dK[0] = mfma(qq[32 * b3], dS[r], dK[0]);
+      dK[1] = mfma(qq[32 * (1 - b3)], dS[r], dK[1]);
+    }
+  };
+
+  const int nt = (p.Nc + TT - 1) / TT;
+  stage(0, 0);
+  stage(TT, 1);
+  asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // tile 0 (7 pieces per tile and wave)
+  lds_barrier();
+  TRAIN_STAMP(0);
+  f32x16 Sa, dAa, Sb, dAb;
+  phase1(0, Sa, dAa);
+  int sl = 0;
+  // iteration t: publish tile t + 1; DMA tile t + 2 into the slot tile t - 1 used; tile t + 1's
+  // phase 1 beside tile t's softmax and stores; tile t's phase 2.  Two register sets, A / B,
+  // alternate by unrolling the loop by two.
+  auto step = [&](int t, f32x16& S, f32x16& dA, f32x16& Sn, f32x16& dAn) __attribute__((always_inline)) {
+    // tile t + 1 landed (younger: tile t's dS stores... issued after it in iteration t - 1: 16)
+    if (t == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    lds_barrier();
+    const int sn = sl == 2 ? 0 : sl + 1, s2 = sl == 0 ? 2 : sl - 1;
+    stage((t + 2) * TT, s2);  // past the end: clamped rows, never read
+    softmax(sl, t * TT, S, dA);
+    phase1(sn, Sn, dAn);  // tile t + 1 (past the end: clamped rows, result unused)
+    phase2(sl, S, dA);
+    sl = sn;
+  };
+  int t = 0;
+  for (; t + 1 < nt; t += 2) {
+    step(t, Sa, dAa, Sb, dAb);
+    step(t + 1, Sb, dAb, Sa, dAa);
+  }
+  if (t < nt) step(t, Sa, dAa, Sb, dAb);
+  TRAIN_STAMP(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMA past the end has landed
+  if (!kv) return;
+  const long long row = bh * p.Ns + key;
+  const float* vg = p.v + row * 64;
+  float* dvr = p.dv + row * 64;
+  float* dkr = p.dk + row * 64;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * cb + 8 * g + 4 * h;
+      const f32x4 vv = ld4(vg + c0);
+      f32x4 a, b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = G1[cb][4 * g + e] + 2.0f * vv[e] * G2[cb][4 * g + e];
+        b[e] = dK[cb][4 * g + e];
+      }
+      st4(dvr + c0, a);
+      st4(dkr + c0, b);
+    }
+}
+
 constexpr int kNW = 4;
 // per-(b, h) dS slice addressed by 32-bit buffer offsets, with 0x7ffffff0 free as the drop offset
 constexpr long long kMaxSpillRows = (0x7fff0000LL / 4);
@@ -533,7 +726,10 @@ extern "C" int mhada_attn_train_dkv(const float* q, const float* k, const float*
   p.q = q; p.k = k; p.v = v; p.lse = const_cast<float*>(lse); p.dmo = dmo; p.dd = dd; p.dk = dk; p.dv = dv;
   p.ds = ds; p.Nc = Nc; p.Ns = Ns;
   if (!set_grid(p, BH, Ns)) return fail("mhada_attn_train_dkv: grid too large");
-  hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1, true>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
+  if (tuning().train_dkv_dma)  // LDS-DMA form, two workgroups per CU (round 4)
+    hipLaunchKernelGGL(attn_train_dkv_dma_kernel, dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
+  else
+    hipLaunchKernelGGL((attn_train_dkv_kernel<kNW, 1, true>), dim3(p.nblk), dim3(64 * kNW), 0, (hipStream_t)s_, p);
   return check_launch("mhada_attn_train_dkv");
 }
 

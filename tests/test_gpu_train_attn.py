@@ -95,6 +95,35 @@ def test_attn_train_bwd_ds_spill_matches_recompute(BH, Nc, Ns):
     assert _rel(a[0].double(), b[0].double()) < 1e-5
 
 
+@pytest.mark.parametrize("BH,Nc,Ns", [(2, 128, 64), (1, 37, 300), (3, 500, 256), (2, 33, 4), (1, 64, 128), (2, 161, 96)])
+def test_attn_train_dkv_dma_kernel_matches_register_staged(BH, Nc, Ns):
+    """The LDS-DMA / software-pipelined dK / dV' kernel (tuning train_dkv_dma = 1, the default) against
+    the round-3 register-staged kernel: the same products in the same order, so dK, dV' and the
+    spilled dS are bit-identical (1..16 query tiles, ragged Nc: padded query rows must give P = 0)."""
+    from mhada_hip import _lib
+    g = torch.Generator().manual_seed(BH * 31 + Nc + Ns)
+    q, k, v = (torch.randn(BH, n, 64, generator=g).cuda() * 0.5 for n in (Nc, Ns, Ns))
+    v = (v - v.mean(dim=1, keepdim=True)).contiguous()
+    out, mo, lse = ops.attn_train_fwd(q, k, v, torch.randn(BH, Nc, 64, generator=g).cuda())
+    dmo = torch.randn(BH, Nc, 128, generator=g).cuda()
+    dd = (dmo * mo).sum(-1).contiguous()
+    lib = _lib.load()
+    res = []
+    for dma in (0, 1):
+        dk, dv = torch.empty_like(k), torch.empty_like(v)
+        ds = torch.full((BH, Nc, Ns), float("nan"), device="cuda")
+        with _lib.tuning(train_dkv_dma=dma):
+            rc = lib.mhada_attn_train_dkv(q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
+                                          dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, Nc, Ns,
+                                          torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, lib.mhada_last_error()
+        torch.cuda.synchronize()
+        res.append((dk, dv, ds))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert torch.isfinite(res[1][2]).all()  # every dS element written
+
+
 def test_attn_train_bwd_default_path_is_shape_determined(monkeypatch):
     """the spill / recompute choice depends on shapes and ops.DS_SPILL_BYTES only (not
     on free memory), is recorded in ops.BWD_PATH_COUNTS, and repeated calls give the same bits."""
