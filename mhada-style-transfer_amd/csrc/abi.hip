@@ -40,7 +40,7 @@ const Knob kKnobs[] = {
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
     {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
     {"attn_sched", &Tuning::attn_sched},             {"tn_skinny_lds", &Tuning::tn_skinny_lds},
-    {"train_dkv_dma", &Tuning::train_dkv_dma},
+    {"train_dkv_dma", &Tuning::train_dkv_dma},     {"wino_l2pf", &Tuning::wino_l2pf},
     {"xknob", &Tuning::xknob},
 };
 

@@ -60,6 +60,7 @@ struct WinoP {
   float* y;           // NHWC [B][Ho][Wo][ldc]
   const float* mask;  // null, or [B][Ho][Wo][ldc]: y = 0 where mask <= 0 (a ReLU adjoint folded into a dgrad)
   int B, H, W, Cin, Cout, Ho, Wo, pad, zero, relu;
+  int l2pf;           // tuning wino_l2pf: L2 warm-up of the U chunk two ahead
   long long ldc;
   int nbx, nby, nbn, nblk;
 };
@@ -81,7 +82,8 @@ MHADA_DEV void glds16(const float* src, float* lds) {  // LDS-DMA: lane l -> lds
 }
 
 __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS)];  // 150 KiB
+  // + 64 floats: the landing area of the L2 warm-up loads (wino_l2pf, below), never read
+  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS) + 64];  // 150 KiB
   auto sV = [&](int i) { return lds + i * kVS; };
   auto sU = [&](int i) { return lds + 2 * kVS + i * kUS; };
   auto sR = [&](int i) { return lds + 2 * (kVS + kUS) + i * kRS; };
@@ -142,6 +144,21 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
     for (int t = 0; t < 4; ++t) glds16(uc + uoff[t], su + (4 * wave + t) * 256);
     glds16(p.x + roff[0] + cr * kCK, sr + wave * 256);
     if (wave + 8 < kRDma) glds16(p.x + roff[1] + cr * kCK, sr + (wave + 8) * 256);
+  };
+  // L2 warm-up of U(k + 2) (p.l2pf): every wave issues one 4-byte LDS-DMA per lane, one per 128-B
+  // line of the chunk's 16 x 2-KiB U segments (waves 4-7 repeat waves 0-3), into a landing area
+  // nobody reads.  U(k + 1)'s DMA then finds its lines in L2 instead of paying the HBM latency
+  // inside the chunk (all workgroups of an XCD ask for the same lines at the same moment).  The
+  // warm-up is the wave's youngest memory operation, so publish waits with vmcnt(1).
+  const int pfl = 64 * (wave & 3) + lane;  // line 0..255: segment xi = pfl / 16, 128-B line pfl % 16
+  const int pfoff = ((pfl >> 4) * p.Cout + co0) * kCK + (pfl & 15) * 32;
+  auto l2warm = [&](int cu) {
+#if WINO_DBG & 2
+    return;
+#endif
+    cu = min(cu, nck - 1);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.u + cu * ustride + pfoff),
+                                     (__attribute__((address_space(3))) void*)(lds + 2 * (kVS + kUS + kRS)), 4, 0, 0);
   };
 
   // transform item: channel tc of tile tt; zero-padding positions of its 4x4 patch
@@ -231,10 +248,20 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   for (int k = 0; k < nck; ++k) {
     const int c = k & 1, n = c ^ 1;
     dma(k + 1, sU(n), k + 2, sR(c));
+    if (p.l2pf) l2warm(k + 2);
     mfmas(sV(c), sU(c));
     transform(sR(n), sV(n));
-    publish();
+    if (p.l2pf) {  // this wave's DMA landed (all but its youngest operation, the warm-up), then the barrier
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's V writes
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      publish();
+    }
   }
+  if (p.l2pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last warm-up has landed
 
   // output transform Y = A^T M A (A^T = [[1,1,1,0],[0,1,-1,-1]]): row partials
   // P_i[q] = sum_j M[i][j] A[j][q]; Y[0][q] = P0 + P1 + P2, Y[1][q] = P1 - P2 - P3.  Waves
@@ -667,6 +694,7 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   p.Wo = p.zero ? W + 2 * (pad - 1) : W;
   p.relu = relu;
   p.ldc = ldc;
+  p.l2pf = tuning().wino_l2pf;
   const int TY = (p.Ho + 1) / 2, TX = (p.Wo + 1) / 2;
   p.nby = (TY + kT - 1) / kT;
   p.nbx = (TX + kT - 1) / kT;

@@ -20,6 +20,11 @@ for s in "$@"; do
           timeout -k 10 120 python -u tools/attn_clock.py f32 > $OUT/attn_clock_f32.log 2>&1 || exit 1 ;;
     c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
     trainclock) timeout -k 10 180 python -u tools/attn_clock.py dkv > $OUT/train_clock.log 2>&1 || exit 6 ;;
+    winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py wino_l2pf > $OUT/wino_l2pf_ab.log 2>&1 || exit 9 ;;
+    dkvpmc) for v in 0 1; do
+              timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_LDS --output-format csv -d $OUT/dkvpmc_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc_$v.log 2>&1 || exit 10
+              timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/dkvpmc2_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc2_$v.log 2>&1 || exit 10
+            done ;;
     train) timeout -k 10 400 python -u bench.py --train --steps 5 --warmup 2 > $OUT/train.log 2>&1 || exit 7 ;;
     trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trainprof -o run -- python3 bench.py --train --steps 3 --warmup 1 > $OUT/trainprof.log 2>&1 || exit 8 ;;
     # test FAILURES (pytest rc 1) do not stop the batch; a crash, fault or time-out (any other rc) does
