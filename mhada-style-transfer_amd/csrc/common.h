@@ -47,8 +47,8 @@ struct Tuning {
                              // sums, 8 its persistent form, 3 LDS-DMA on 32x32x16 (fsg), 5 half-tile
                              // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
-  int wino_l2pf = 1;         // fp32 Winograd conv: L2 warm-up of the filter chunk two ahead (0: none)
-  int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, 2 workgroups per CU (0: round 3's)
+  int wino_l2pf = 0;         // fp32 Winograd conv: L2 warm-up of the filter chunk two ahead (0: none; 1 measured 1.3 % slower)
+  int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };
 const Tuning& tuning();
