@@ -41,7 +41,7 @@ const Knob kKnobs[] = {
     {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
     {"attn_sched", &Tuning::attn_sched},             {"tn_skinny_lds", &Tuning::tn_skinny_lds},
     {"train_dkv_dma", &Tuning::train_dkv_dma},     {"wino_l2pf", &Tuning::wino_l2pf},
-    {"xknob", &Tuning::xknob},
+    {"wino_ws", &Tuning::wino_ws},                 {"xknob", &Tuning::xknob},
 };
 
 Tuning g_tuning;
@@ -63,6 +63,7 @@ bool valid(const char* name, int v) {
   if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
   if (!strcmp(name, "attn_sched")) return v == 0 || (v >= 3 && v <= 8);
   if (!strcmp(name, "xknob")) return v >= 0 && v < 16;
+  if (!strcmp(name, "wino_ws")) return v >= 0 && v <= 3;
   return v == 0 || v == 1;
 }
 }  // namespace

@@ -48,6 +48,7 @@ struct Tuning {
                              // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
   int wino_l2pf = 0;         // fp32 Winograd conv: L2 warm-up of the filter chunk two ahead (0: none; 1 measured 1.3 % slower)
+  int wino_ws = 0;           // fp32 Winograd conv: 0 wino_kernel; 1 warp-specialised (measured 7 % slower); 2 persistent 16x16x4 (see wino.hip)
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };

@@ -187,6 +187,74 @@ def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
         assert rel(y[..., :Co], yd) < 2e-6
 
 
+@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
+                                              (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64), (2, 2, 5, 24, 192, 196),
+                                              (1, 40, 36, 96, 64, 64), (2, 64, 48, 16, 64, 64)])
+def test_conv3x3_wino_ws_bit_identical(pad_mode, pad, B, H, W, Ci, Co, ldc):
+    """The warp-specialised Winograd kernel (tuning wino_ws = 1, the default: MFMA waves + transform /
+    DMA waves, 4 x 8-tile workgroups, DMA two chunks ahead) computes the same products in the same
+    order as wino_kernel (wino_ws = 0): bit-identical outputs, bias + ReLU, the folded ReLU mask
+    (relu_mask), padded ldc columns untouched; 1 and 2 chunks (Ci = 8, 16) exercise the prologue."""
+    g = torch.Generator().manual_seed(B * H * W + Ci)
+    x = (torch.rand(B, H, W, Ci, generator=g) - 0.3).to(DEV)
+    wp = (torch.randn(Co, 9 * Ci, generator=g) * (9 * Ci) ** -0.5).to(DEV)
+    bias = torch.randn(Co, generator=g).to(DEV)
+    u = ops.wino_weights(wp)
+    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
+    mask = (torch.rand(B, Ho, Wo, ldc, generator=g) - 0.5).to(DEV)
+    for kw in (dict(bias=bias, relu=True), dict(bias=None, relu=False), dict(bias=bias, relu=False, relu_mask=mask)):
+        outs = []
+        for ws in (0, 1):
+            out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
+            with _lib.tuning(wino_ws=ws):
+                outs.append(ops.conv3x3_wino(x, u, kw["bias"], kw["relu"], pad_mode, pad, out=out,
+                                             relu_mask=kw.get("relu_mask")))
+        assert torch.equal(outs[0], outs[1]), kw.keys()
+        assert bool((outs[1][..., Co:] == 7.0).all())
+
+
+@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
+                                              (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64), (2, 2, 5, 24, 192, 196),
+                                              (4, 128, 128, 16, 128, 128), (8, 64, 64, 8, 64, 64),
+                                              (3, 50, 70, 24, 128, 132), (1, 16, 16, 512, 256, 256)])
+@pytest.mark.parametrize("ws", [2, 3])
+def test_conv3x3_wino_persistent(ws, pad_mode, pad, B, H, W, Ci, Co, ldc):
+    """The persistent 16x16x4 Winograd kernels (tuning wino_ws = 2 LDS-DMA, 3 register-staged: one workgroup per CU walking its
+    items as one chunk stream, MFMA waves holding all 16 positions) against fp64 conv2d and against
+    wino_kernel: bias + ReLU, no bias, the folded ReLU mask (zeros exactly where mask <= 0), padded
+    ldc columns untouched; shapes with 1-64 chunks per item and 1-4 items per workgroup (the stream
+    crossing item boundaries every chunk for Ci = 8)."""
+    g = torch.Generator().manual_seed(B * H * W + Ci + Co)
+    x = (torch.rand(B, H, W, Ci, generator=g) - 0.3).to(DEV)
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) * (9 * Ci) ** -0.5).to(DEV)
+    bias = torch.randn(Co, generator=g).to(DEV)
+    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous()
+    u = ops.wino_weights(wp)
+    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
+    xn = x.permute(0, 3, 1, 2).double()
+    xp = F.pad(xn, (1, 1, 1, 1), mode="reflect") if pad_mode == "reflect" else F.pad(xn, (pad,) * 4)
+    mask = (torch.rand(B, Ho, Wo, ldc, generator=g) - 0.5).to(DEV)
+    for kw in (dict(bias=bias, relu=True), dict(bias=None, relu=False), dict(bias=bias, relu=False, relu_mask=mask)):
+        outs = []
+        for knob in (0, ws):
+            out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
+            with _lib.tuning(wino_ws=knob):
+                outs.append(ops.conv3x3_wino(x, u, kw["bias"], kw["relu"], pad_mode, pad, out=out,
+                                             relu_mask=kw.get("relu_mask")))
+        y = outs[1]
+        assert bool((y[..., Co:] == 7.0).all())
+        ref = F.conv2d(xp, w.double(), None if kw["bias"] is None else bias.double())
+        ref = torch.relu(ref) if kw["relu"] else ref
+        if "relu_mask" in kw:
+            keep = (mask[..., :Co] > 0).permute(0, 3, 1, 2)
+            ref = torch.where(keep, ref, torch.zeros_like(ref))
+            assert bool((y[..., :Co].permute(0, 3, 1, 2)[~keep] == 0).all())
+        assert rel(y[..., :Co].permute(0, 3, 1, 2), ref) < 2e-6, kw.keys()
+        assert rel(y, outs[0]) < 2e-6
+
+
 def test_conv3x3_wino_routing():
     """ops.conv3x3 takes the Winograd kernel for eligible fp32 shapes (same result as the explicit
     call) and the implicit GEMM otherwise (Cout % 64 != 0)."""

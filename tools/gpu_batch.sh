@@ -6,6 +6,7 @@
 #   gpu        the whole pytest -m gpu suite
 #   bench      the default bench line
 #   trainclock in-kernel clock of the training dK/dV' kernel (diagnostic build)
+#   winotests / winoab  the Winograd conv tests / knob A/B (WINO_KNOB, default wino_ws)
 #   train / trainprof  the training step bench line / its rocprofv3 kernel trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -20,7 +21,20 @@ for s in "$@"; do
           timeout -k 10 120 python -u tools/attn_clock.py f32 > $OUT/attn_clock_f32.log 2>&1 || exit 1 ;;
     c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
     trainclock) timeout -k 10 180 python -u tools/attn_clock.py dkv > $OUT/train_clock.log 2>&1 || exit 6 ;;
-    winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py wino_l2pf > $OUT/wino_l2pf_ab.log 2>&1 || exit 9 ;;
+    winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py ${WINO_KNOB:-wino_ws} > $OUT/wino_${WINO_KNOB:-wino_ws}_ab.log 2>&1 || exit 9 ;;
+    winoab3) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0,xknob=0 -c wino_ws=0,xknob=1 -c wino_ws=1 -c wino_ws=2 > $OUT/wino_ab3.log 2>&1 || exit 9 ;;
+    winoab2) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0 -c wino_ws=2 -c wino_ws=3 > $OUT/wino_ab2.log 2>&1 || exit 9 ;;
+    winoab4) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0,xknob=0 -c wino_ws=0,xknob=2 -c wino_ws=0,xknob=3 > $OUT/wino_ab4.log 2>&1 || exit 9 ;;
+    winopk) timeout -k 10 300 $PYT tests/test_gpu_kernels.py -k "wino_persistent" > $OUT/wino_pk_tests.log 2>&1 || exit 14 ;;
+    winotests) timeout -k 10 300 $PYT tests/test_gpu_kernels.py tests/test_gpu_train_ops.py -k "wino or chain" > $OUT/wino_tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 11 ;;
+    winodbg) for shp in ${WINO_DBG_SHAPES:-"8 128 256 256" "8 256 128 128" "8 64 512 512"}; do
+               WINO_KNOB_VALS=${WINO_KNOB_VALS:-0,1} WINO_LIB_DIR=diag/wino_dbg timeout -k 10 120 python -u tools/wino_dbg.py $shp 0 1 2 4 6 >> $OUT/wino_dbg.log 2>&1 || exit 12
+             done ;;
+    winopmc) for v in ${WINO_KNOB_VALS//,/ }; do
+               timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_LDS --output-format csv -d $OUT/winopmc_$v -o run -- python3 tools/wino_only.py $v > $OUT/winopmc_$v.log 2>&1 || exit 13
+               timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/winopmc2_$v -o run -- python3 tools/wino_only.py $v > $OUT/winopmc2_$v.log 2>&1 || exit 13
+               timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum --output-format csv -d $OUT/winopmc3_$v -o run -- python3 tools/wino_only.py $v > $OUT/winopmc3_$v.log 2>&1 || exit 13
+             done ;;
     dkvpmc) for v in 0 1; do
               timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_LDS --output-format csv -d $OUT/dkvpmc_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc_$v.log 2>&1 || exit 10
               timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/dkvpmc2_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc2_$v.log 2>&1 || exit 10
