@@ -91,19 +91,12 @@ MHADA_DEV unsigned lds_byte_off(const float* p) {
 }
 MHADA_DEV void ds_read16(f32x4& r, unsigned byte_off) { asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(byte_off)); }
 template <int N>
-MHADA_DEV void lgkm_wait2(f32x4& a, f32x4& b) {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int N>
 MHADA_DEV void lgkm_wait3(f32x4& a, f32x4& b, f32x4& c) {
   __builtin_amdgcn_sched_barrier(0);  // the MFMAs before stay before, those after stay after
   asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "i"(N));
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool ASMRD, bool STAG>
 __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   // + 64 floats: the landing area of the L2 warm-up loads (wino_l2pf, below), never read
   __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS) + 64];  // 150 KiB
@@ -246,28 +239,6 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
 #if WINO_DBG & 1
     return;
 #endif
-    if constexpr (ASMRD) {  // all 16 operand reads issued up front, position x waits for its own two
-      const unsigned va = lds_byte_off(sv + arow), vb = lds_byte_off(su + brow);
-      f32x4 av[8], bv[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) {
-        ds_read16(av[x], va + x * (kTT * kCK * 4));
-        ds_read16(bv[x], vb + x * (kCO * kCK * 4));
-      }
-      auto mf = [&](int x) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x][s], bv[x][s], acc[x], 0, 0, 0);
-      };
-      lgkm_wait2<14>(av[0], bv[0]); mf(0);
-      lgkm_wait2<12>(av[1], bv[1]); mf(1);
-      lgkm_wait2<10>(av[2], bv[2]); mf(2);
-      lgkm_wait2<8>(av[3], bv[3]); mf(3);
-      lgkm_wait2<6>(av[4], bv[4]); mf(4);
-      lgkm_wait2<4>(av[5], bv[5]); mf(5);
-      lgkm_wait2<2>(av[6], bv[6]); mf(6);
-      lgkm_wait2<0>(av[7], bv[7]); mf(7);
-      return;
-    }
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
       const f32x4 av = *reinterpret_cast<const f32x4*>(sv + x * (kTT * kCK) + arow);
@@ -294,18 +265,8 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
     const int c = k & 1, n = c ^ 1;
     dma(k + 1, sU(n), k + 2, sR(c));
     if (p.l2pf) l2warm(k + 2);
-    if constexpr (STAG) {  // waves 4-7 transform first, beside the MFMAs of waves 0-3 on the same SIMDs
-#pragma unroll 1
-      for (int ph = 0; ph < 2; ++ph) {
-        if (ph == e)
-          mfmas(sV(c), sU(c));
-        else
-          transform(sR(n), sV(n));
-      }
-    } else {
-      mfmas(sV(c), sU(c));
-      transform(sR(n), sV(n));
-    }
+    mfmas(sV(c), sU(c));
+    transform(sR(n), sV(n));
     if (p.l2pf) {  // this wave's DMA landed (all but its youngest operation, the warm-up), then the barrier
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
@@ -393,6 +354,11 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
 // leaves the youngest chunk's 10 pieces per wave in flight), so an L2 / HBM round trip has two
 // chunk times to land instead of one.  The products, their order per accumulator and the output
 // transform's operation order are those of wino_kernel: the result is bit-identical.
+// Measured (profiles/r04_wino_variants.log): 5-13 % SLOWER than wino_kernel on every decoder /
+// VGG19 shape.  Ablation at 256 -> 256 @ 128^2 B8: the MFMA waves alone run within 4 % of
+// wino_kernel's MFMA-only build, but the single transform wave per SIMD (10 LDS-DMA pieces at
+// 60-185 issue cycles each, the transform, the waits) is on the critical path of every chunk, and
+// 32-tile workgroups need twice the U stream per MFMA.  Kept as tuning wino_ws = 1.
 // ------------------------------------------------------------------------------------
 constexpr int kWY = 4, kWX = 8, kWTT = kWY * kWX;      // 32 tiles: 8 x 16 output pixels
 constexpr int kWRX = 2 * kWX + 2, kWRY = 2 * kWY + 2;  // raw patch: 18 x 10 pixels
@@ -659,6 +625,12 @@ __global__ void __launch_bounds__(512, 1) wino_ws_kernel(const WinoP p) {
 // channels as lane group j = lane >> 4 -> channels (2j, 2j+1): one 8-byte read per operand from
 // the same swizzled 32-B rows the DMA and transform produce (swz; conflict-free ds_read_b64).
 // Rings: V 2 x 16 KiB, U 3 x 32 KiB, raw 3 x 8 KiB (the U DMA runs two chunks ahead).
+// Measured (profiles/r04_wino_variants.log): 8-26 % SLOWER than wino_kernel.  Its MFMA waves alone
+// (ablation build, no loads, no transform) are as fast as wino_kernel's MFMA-only build (536 vs
+// 538 us at 256 -> 256 @ 128^2 B8), so the lost time is the transform / DMA waves': 486 us alone
+// for that shape, and the two roles meet at two barriers per chunk; staging the pieces through
+// registers (global_load + ds_write_b128) instead of LDS-DMA was slower still (1.32x).  Kept as
+// tuning wino_ws = 2: the design notes for a faster transform path are in DESIGN.md §3a.
 // ------------------------------------------------------------------------------------
 template <class F, int... I>
 MHADA_DEV void static_for(F&& f, std::integer_sequence<int, I...>) {
@@ -696,7 +668,6 @@ MHADA_DEV PkItem pk_item(const WinoP& p, int j) {  // item j of this workgroup
   return it;
 }
 
-template <bool RS>  // RS: U / raw staged through registers (global_load + ds_write) instead of LDS-DMA
 __global__ void __launch_bounds__(512, 1) wino_pk_kernel(const WinoP p) {
   __shared__ __attribute__((aligned(16))) float lds[2 * kWVS + 3 * kUS + 3 * kWRS];  // 152 KiB
   auto sV = [&](int i) { return lds + i * kWVS; };
@@ -888,33 +859,6 @@ __global__ void __launch_bounds__(512, 1) wino_pk_kernel(const WinoP p) {
       for (int t = 0; t < 2; ++t) glds16(xc + r_off[t], sr + (tw + 4 * t) * 256);
 #endif
     };
-    f32x4 stg[10];  // RS: the staged pieces (8 of U, 2 of the raw patch), lane l -> 16 B at 16 l
-    auto load_u = [&](const Cur& cu) {
-#if !(WINO_DBG & 2)
-      const float* uc = u_src(cu);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) stg[t] = *reinterpret_cast<const f32x4*>(uc + uoff[t]);
-#endif
-    };
-    auto load_r = [&](const Cur& cr) {
-#if !(WINO_DBG & 2)
-      const float* xc = r_src(cr);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) stg[8 + t] = *reinterpret_cast<const f32x4*>(xc + r_off[t]);
-#endif
-    };
-    auto put_u = [&](float* su) {
-#if !(WINO_DBG & 2)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4*>(su + (8 * tw + t) * 256 + 4 * lane) = stg[t];
-#endif
-    };
-    auto put_r = [&](float* sr) {
-#if !(WINO_DBG & 2)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) *reinterpret_cast<f32x4*>(sr + (tw + 4 * t) * 256 + 4 * lane) = stg[8 + t];
-#endif
-    };
     const int ti = tid - 256, tc = ti & 7, tt = ti >> 3;  // item: channel tc of tile tt
     int roffs[16];
 #pragma unroll
@@ -966,22 +910,10 @@ __global__ void __launch_bounds__(512, 1) wino_pk_kernel(const WinoP p) {
 #endif
     };
     // prologue: {U(0), raw(0)}, {U(1), raw(1)}, {raw(2) (+ a duplicate U(1))}; transform raw(0)
-    if constexpr (RS) {  // U(0), raw(0), raw(1) into LDS; U(1), raw(2) left in the staging registers
-      load_u(cur_at(0));
-      load_r(cur_at(0));
-      put_u(sU(0));
-      put_r(sR(0));
-      load_u(cur_at(1));
-      load_r(cur_at(1));
-      put_r(sR(1));
-      load_r(cur_at(2));
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-    } else {
-      dma(cur_at(0), sU(0), cur_at(0), sR(0));
-      dma(cur_at(1), sU(1), cur_at(1), sR(1));
-      dma(cur_at(1), sU(1), cur_at(2), sR(2));
-      asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // U(0), raw(0)
-    }
+    dma(cur_at(0), sU(0), cur_at(0), sR(0));
+    dma(cur_at(1), sU(1), cur_at(1), sR(1));
+    dma(cur_at(1), sU(1), cur_at(2), sR(2));
+    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // U(0), raw(0)
     bare_barrier();
     transform(cur_at(0), sR(0), sV(0));
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // U(1), raw(1)
@@ -994,14 +926,7 @@ __global__ void __launch_bounds__(512, 1) wino_pk_kernel(const WinoP p) {
     int su2 = 2, sr0 = 0;  // (s + 2) % 3, s % 3
     for (int s = 0; s < nst; ++s) {
       const int sr1 = sr0 == 2 ? 0 : sr0 + 1;  // (s + 1) % 3
-      if constexpr (RS) {  // staged U(s+1) -> U[(s+1)%3], raw(s+2) -> R[(s+2)%3]; then load U(s+2), raw(s+3)
-        put_u(sU(sr1));
-        put_r(sR(su2));
-        load_u(cu);
-        load_r(cr);
-      } else {
-        dma(cu, sU(su2), cr, sR(sr0));
-      }
+      dma(cu, sU(su2), cr, sR(sr0));
       transform(ct, sR(sr1), sV((s + 1) & 1));
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -1409,18 +1334,10 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
     return fail("mhada_conv3x3_wino: problem too large for 32-bit indexing");
   p.nblk = (int)nblk;
   if (ws == 2)  // persistent: one workgroup per CU (152 KiB of LDS each)
-    hipLaunchKernelGGL(wino_pk_kernel<false>, dim3(std::min(p.nblk, wino_num_cus())), dim3(512), 0, (hipStream_t)s_, p);
-  else if (ws == 3)
-    hipLaunchKernelGGL(wino_pk_kernel<true>, dim3(std::min(p.nblk, wino_num_cus())), dim3(512), 0, (hipStream_t)s_, p);
+    hipLaunchKernelGGL(wino_pk_kernel, dim3(std::min(p.nblk, wino_num_cus())), dim3(512), 0, (hipStream_t)s_, p);
   else if (ws)
     hipLaunchKernelGGL(wino_ws_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
-  else if (tuning().xknob == 1)
-    hipLaunchKernelGGL((wino_kernel<true, false>), dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
-  else if (tuning().xknob == 2)
-    hipLaunchKernelGGL((wino_kernel<false, true>), dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
-  else if (tuning().xknob == 3)
-    hipLaunchKernelGGL((wino_kernel<true, true>), dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
   else
-    hipLaunchKernelGGL((wino_kernel<false, false>), dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
+    hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
   return check_launch("mhada_conv3x3_wino");
 }

@@ -37,12 +37,13 @@ def needs_grad(module: torch.nn.Module, *xs) -> bool:
     return any(p.requires_grad for p in module.parameters())
 
 
-def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
+def _vit_forward_hip(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor]:
     """VisionTransformer.forward on the HIP training kernels (train_fns): patch embedding and
     every Linear (MHA in/out projections, MLP with fused ReLU) on mhada_gemm forward and
     mhada_gemm / mhada_gemm_tn / mhada_colsum backward; LayerNorm on mhada_layernorm_fwd/_bwd; the
     pos-embed resize on mhada_pos_embed and its gather adjoint; the batch-axis attention core
-    (L = B <= 8 keys per token) on mhada_vit_batch_attn(_bwd)."""
+    (L = B <= 8 keys per token) on mhada_vit_batch_attn(_bwd).  ``groups`` > 1: x holds that many
+    calls' batches back to back, attended separately (vit_forward)."""
     from . import train_fns
     B, _, H, W = x.shape
     p = vit.patch_size
@@ -60,12 +61,14 @@ def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
         d = C // heads
         y = train_fns.layernorm(t.reshape(B * N, C), blk.ln1) if ln_hip else blk.ln1(t).reshape(B * N, C)
         qkv = train_fns.linear(y, att.in_proj_weight, att.in_proj_bias)
-        if d == 64 and B <= 8:  # the batch-axis attention core on HIP (L = B keys per token)
-            o = train_fns.BatchAxisAttnFn.apply(qkv.view(B, N, 3 * C), heads).reshape(B * N, C)
+        if d == 64 and B // groups <= 8:  # the batch-axis attention core on HIP (L = B keys per token)
+            o = train_fns.BatchAxisAttnFn.apply(qkv.view(B, N, 3 * C), heads, groups).reshape(B * N, C)
         else:
-            q, k, v = (z.reshape(B, N, heads, d).permute(1, 2, 0, 3) for z in qkv.split(C, dim=1))  # (N, H, L, d)
+            Lg = B // groups
+            q, k, v = (z.reshape(groups, Lg, N, heads, d).permute(0, 2, 3, 1, 4)  # (G, N, H, L, d)
+                       for z in qkv.split(C, dim=1))
             a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (d ** -0.5), dim=-1)
-            o = torch.matmul(a, v).permute(2, 0, 1, 3).reshape(B * N, C)
+            o = torch.matmul(a, v).permute(0, 3, 1, 2, 4).reshape(B * N, C)
         t = t + train_fns.linear(o, att.out_proj.weight, att.out_proj.bias).view(B, N, C)
         y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2) if ln_hip else blk.ln2(t).reshape(B * N, C)
         # MLP1's ReLU adjoint is applied by MLP2's input-gradient GEMM (its only consumer)
@@ -75,13 +78,20 @@ def _vit_forward_hip(vit, x: torch.Tensor) -> List[torch.Tensor]:
     return outs
 
 
-def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
+def vit_forward(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor]:
     """VisionTransformer.forward (vit.py:148-169); the MHA keeps batch_first=False on a
     (B, N, C) tensor, i.e. attends over the batch axis exactly as the reference.  On a ROCm
-    device the HIP training kernels run it (_vit_forward_hip); the CPU uses aten."""
+    device the HIP training kernels run it (_vit_forward_hip); the CPU uses aten.
+
+    ``groups`` > 1: x is that many calls' batches concatenated (B = groups x L); the batch-axis
+    attention runs over each call's L images separately, everything else is per token, so the
+    outputs are those of the separate calls (Trainer.batch_vit)."""
     if x.is_cuda and vit.patch_size == 8 and not x.requires_grad and \
             isinstance(vit.encoder[0].mlp[1], torch.nn.ReLU) and vit.encoder[0].attention.in_proj_weight is not None:
-        return _vit_forward_hip(vit, x)
+        return _vit_forward_hip(vit, x, groups)
+    if groups > 1:
+        parts = [vit_forward(vit, xg) for xg in x.chunk(groups)]
+        return [torch.cat(o) for o in zip(*parts)]
     B, _, H, W = x.shape
     p = vit.patch_size
     h, w = H // p, W // p

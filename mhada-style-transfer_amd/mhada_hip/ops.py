@@ -290,12 +290,18 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, out_dtype: torc
     return y
 
 
-def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int) -> torch.Tensor:
+def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int, groups: int = 1) -> torch.Tensor:
+    """``mhada_vit_batch_attn`` on qkv [L][ntok][3C]; ``groups`` > 1: the L images are that many
+    independent calls of L / groups images each (consecutive slices), attended separately."""
     _need_gpu(qkv)
     C = qkv.shape[-1] // 3
+    if L % groups:
+        raise ValueError("vit_batch_attn: L must be a multiple of groups")
     out = torch.empty(L, ntok, C, device=qkv.device, dtype=qkv.dtype)
-    _call("mhada_vit_batch_attn", qkv, qkv.data_ptr(), out.data_ptr(), dt_code(qkv.dtype), L, ntok, heads,
-                                          C // heads)
+    Lg, es = L // groups, qkv.element_size()
+    for g in range(groups):
+        _call("mhada_vit_batch_attn", qkv, qkv.data_ptr() + g * Lg * ntok * 3 * C * es,
+              out.data_ptr() + g * Lg * ntok * C * es, dt_code(qkv.dtype), Lg, ntok, heads, C // heads)
     return out
 
 
@@ -821,10 +827,18 @@ def loss_attn(qn: torch.Tensor, kn: torch.Tensor, v: torch.Tensor, x: torch.Tens
     return out
 
 
-def vit_batch_attn_bwd(qkv: torch.Tensor, dout: torch.Tensor, L: int, ntok: int, heads: int) -> torch.Tensor:
-    """``mhada_vit_batch_attn_bwd``: fp32 qkv [L][ntok][3C], dout [L][ntok][C] -> dqkv."""
+def vit_batch_attn_bwd(qkv: torch.Tensor, dout: torch.Tensor, L: int, ntok: int, heads: int,
+                       groups: int = 1) -> torch.Tensor:
+    """``mhada_vit_batch_attn_bwd``: fp32 qkv [L][ntok][3C], dout [L][ntok][C] -> dqkv (``groups``
+    as in vit_batch_attn)."""
     _need_gpu(qkv, dout)
     C = qkv.shape[-1] // 3
+    if L % groups:
+        raise ValueError("vit_batch_attn_bwd: L must be a multiple of groups")
     dqkv = torch.empty_like(qkv)
-    _call("mhada_vit_batch_attn_bwd", qkv, qkv.data_ptr(), dout.data_ptr(), dqkv.data_ptr(), L, ntok, heads, C // heads)
+    Lg = L // groups
+    for g in range(groups):
+        o3, o1 = g * Lg * ntok * 3 * C * 4, g * Lg * ntok * C * 4
+        _call("mhada_vit_batch_attn_bwd", qkv, qkv.data_ptr() + o3, dout.data_ptr() + o1, dqkv.data_ptr() + o3, Lg,
+              ntok, heads, C // heads)
     return dqkv

@@ -37,6 +37,7 @@ class Trainer:
             p.requires_grad_(False)
         self.mse = nn.MSELoss(reduction="mean")
         self.batch_adaformer = True  # see losses()
+        self.batch_vit = True  # see losses()
         # one backward pass per VGG feature map for the gs / lf / id2 terms (HIP; see _feature_losses)
         self.fused_feature_losses = dev.type == "cuda"
         # with the fused losses: the ReLU adjoints of the VGG feature maps relu2_1 .. relu5_1 applied by
@@ -75,12 +76,24 @@ class Trainer:
         convolutions never mix images), so the outputs are the same, while each AdaFormer
         parameter gets one weight-gradient reduction over 3B images instead of three gradients
         summed by autograd (~640 small add launches per step) and every launch is 3x larger.
-        The ViT calls stay separate: their batch-axis attention (vit.py:48) couples the images of
-        one call."""
-        fc_vc = self.vit_c(content)
-        fs_vs = self.vit_s(style)
-        fc_vs = self.vit_s(content)
-        fs_vc = self.vit_c(style)
+        Likewise ``batch_vit`` (the default, on the GPU) runs each ViT's two calls (vit_c on content
+        and style, vit_s on style and content) as one call over the concatenated batch; their
+        batch-axis attention (vit.py:48) couples the images of ONE call, so it runs per call
+        (vit_forward(groups=2)) while every other op (per token) sees the 2B images at once."""
+        if self.batch_vit and content.is_cuda and content.shape == style.shape:
+            # each ViT's two calls as one over the concatenated batch, the batch-axis attention
+            # per call (autograd_path.vit_forward groups): the same outputs, one weight-gradient
+            # GEMM per parameter instead of two partial ones summed by autograd (~150 add launches)
+            from .autograd_path import vit_forward
+            B = content.shape[0]
+            fc_vc, fs_vc = zip(*(o.split(B) for o in vit_forward(self.vit_c, torch.cat([content, style]), groups=2)))
+            fs_vs, fc_vs = zip(*(o.split(B) for o in vit_forward(self.vit_s, torch.cat([style, content]), groups=2)))
+            fc_vc, fs_vc, fs_vs, fc_vs = (list(t) for t in (fc_vc, fs_vc, fs_vs, fc_vs))
+        else:
+            fc_vc = self.vit_c(content)
+            fs_vs = self.vit_s(style)
+            fc_vs = self.vit_s(content)
+            fs_vc = self.vit_c(style)
         if self.batch_adaformer:
             B = content.shape[0]
             _, out = self.ada([torch.cat(t) for t in zip(fc_vc, fc_vc, fs_vc)],

@@ -339,18 +339,18 @@ class BatchAxisAttnFn(torch.autograd.Function):
     mhada_vit_batch_attn_bwd backward."""
 
     @staticmethod
-    def forward(ctx, qkv, heads: int):
+    def forward(ctx, qkv, heads: int, groups: int = 1):
         qkv = qkv.contiguous()
         L, N, _ = qkv.shape
         ctx.save_for_backward(qkv)
-        ctx.heads = heads
-        return ops.vit_batch_attn(qkv, L, N, heads)
+        ctx.heads, ctx.groups = heads, groups
+        return ops.vit_batch_attn(qkv, L, N, heads, groups)
 
     @staticmethod
     def backward(ctx, gout):
         (qkv,) = ctx.saved_tensors
         L, N, _ = qkv.shape
-        return ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads), None
+        return ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads, ctx.groups), None, None
 
 
 class PatchEmbedFn(torch.autograd.Function):

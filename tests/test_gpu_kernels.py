@@ -219,9 +219,9 @@ def test_conv3x3_wino_ws_bit_identical(pad_mode, pad, B, H, W, Ci, Co, ldc):
                                               (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64), (2, 2, 5, 24, 192, 196),
                                               (4, 128, 128, 16, 128, 128), (8, 64, 64, 8, 64, 64),
                                               (3, 50, 70, 24, 128, 132), (1, 16, 16, 512, 256, 256)])
-@pytest.mark.parametrize("ws", [2, 3])
+@pytest.mark.parametrize("ws", [2])
 def test_conv3x3_wino_persistent(ws, pad_mode, pad, B, H, W, Ci, Co, ldc):
-    """The persistent 16x16x4 Winograd kernels (tuning wino_ws = 2 LDS-DMA, 3 register-staged: one workgroup per CU walking its
+    """The persistent 16x16x4 Winograd kernel (tuning wino_ws = 2: one workgroup per CU walking its
     items as one chunk stream, MFMA waves holding all 16 positions) against fp64 conv2d and against
     wino_kernel: bias + ReLU, no bias, the folded ReLU mask (zeros exactly where mask <= 0), padded
     ldc columns untouched; shapes with 1-64 chunks per item and 1-4 items per workgroup (the stream

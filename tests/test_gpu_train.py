@@ -59,6 +59,30 @@ def test_batched_adaformer_step_matches_per_call_step():
     np.testing.assert_allclose(grads[0], grads[1], rtol=1e-4, atol=1e-6 * grads[1].max())
 
 
+def test_batched_vit_step_matches_per_call_step():
+    """Trainer.batch_vit (each ViT's two calls of train_image.py:103-104 as one call over the
+    concatenated batch, the batch-axis attention per call) against the four separate calls: the
+    same ViT features bit for bit, the same losses and gradients up to fp32 summation order."""
+    from test_train_cpu import grad_summary
+    from mhada_hip.autograd_path import vit_forward
+    c = seeded_image(2, 128, 128, 61).cuda()
+    s = seeded_image(2, 128, 128, 62).cuda()
+    tr = Trainer(*build("cuda"))
+    sep = [vit_forward(tr.vit_c, c), vit_forward(tr.vit_c, s)]
+    grp = vit_forward(tr.vit_c, torch.cat([c, s]), groups=2)
+    for o, a, b in zip(grp, *sep):
+        torch.testing.assert_close(o, torch.cat([a, b]), rtol=0, atol=0)
+    outs, grads = [], []
+    for batched in (True, False):
+        tr = Trainer(*build("cuda"))
+        tr.batch_vit = batched
+        out = tr.backward(c, s)
+        outs.append(np.array([float(out[k].detach()) for k in ("loss_gs", "loss_lf", "loss_id1", "loss_id2")]))
+        grads.append(np.concatenate([grad_summary(m) for m in (tr.vit_c, tr.vit_s, tr.ada)]))
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-5)
+    np.testing.assert_allclose(grads[0], grads[1], rtol=1e-4, atol=1e-6 * grads[1].max())
+
+
 def test_relu_adjoint_folds_are_bit_identical():
     """The ReLU adjoints folded into consumers (VGG feature maps into the loss backward and the next
     conv's dgrad: Trainer.masked_vgg_features) give the bits of the relu_bwd passes they replace."""
