@@ -69,11 +69,13 @@ def _vit_forward_hip(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor
                        for z in qkv.split(C, dim=1))
             a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (d ** -0.5), dim=-1)
             o = torch.matmul(a, v).permute(0, 3, 1, 2, 4).reshape(B * N, C)
-        t = t + train_fns.linear(o, att.out_proj.weight, att.out_proj.bias).view(B, N, C)
+        # the residual adds of vit.py:60-61 fused into the out-projection / MLP2 GEMM epilogues
+        t = train_fns.linear(o, att.out_proj.weight, att.out_proj.bias, residual=t.reshape(B * N, C)).view(B, N, C)
         y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2) if ln_hip else blk.ln2(t).reshape(B * N, C)
         # MLP1's ReLU adjoint is applied by MLP2's input-gradient GEMM (its only consumer)
         m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True, grad_masked=True)
-        t = t + train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias, relu_input=True).view(B, N, C)
+        t = train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias, relu_input=True,
+                             residual=t.reshape(B * N, C)).view(B, N, C)
         outs.append(t.permute(0, 2, 1).reshape(B, C, h, w))
     return outs
 

@@ -171,12 +171,18 @@ class Conv3x3Fn(torch.autograd.Function):
 
 
 class LinearFn(torch.autograd.Function):
-    """y = act(x W^T + b) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear layout)."""
+    """y = act(x W^T + b) (+ residual) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear
+    layout).  ``residual`` [M][N] (no ReLU with it): the add of a residual stream fused into the
+    GEMM epilogue (the reference's ``t + f(t)``); its gradient is gy itself."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool, grad_masked: bool = False, relu_input: bool = False):
+    def forward(ctx, x, weight, bias, relu: bool, grad_masked: bool = False, relu_input: bool = False,
+                residual=None):
         x = x.contiguous()
-        y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu)
+        if residual is not None and relu:
+            raise ValueError("LinearFn: a fused residual follows a ReLU-free linear")
+        y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu,
+                       residual=None if residual is None else residual.detach().contiguous())
         ctx.save_for_backward(x, weight, y if (relu and not grad_masked) else None)
         # grad_masked: y's only consumer is a LinearFn(relu_input=True), whose input-gradient GEMM
         # applies this ReLU's adjoint in its epilogue (mhada_gemm relu = 2): no relu_bwd pass here
@@ -199,12 +205,12 @@ class LinearFn(torch.autograd.Function):
                 gb = cs
         elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)
-        return gx, gw, gb, None, None, None
+        return gx, gw, gb, None, None, None, gy if ctx.needs_input_grad[6] else None
 
 
 def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bool = False,
-           grad_masked: bool = False, relu_input: bool = False) -> torch.Tensor:
-    return LinearFn.apply(x2d, weight, bias, relu, grad_masked, relu_input)
+           grad_masked: bool = False, relu_input: bool = False, residual: torch.Tensor = None) -> torch.Tensor:
+    return LinearFn.apply(x2d, weight, bias, relu, grad_masked, relu_input, residual)
 
 
 class InstanceNormTokensFn(torch.autograd.Function):

@@ -332,6 +332,25 @@ def test_linear_fn_fwd_bwd(M, K, N, relu):
         assert rel(a, b_) < 1e-5
 
 
+@pytest.mark.parametrize("M,K,N", [(1000, 512, 512), (300, 2048, 512)])
+def test_linear_fn_fused_residual(M, K, N):
+    """LinearFn(residual=r): y = x W^T + b + r in the GEMM epilogue (the ViT's out-projection and
+    MLP2 residual adds), the residual's gradient passed through: against fp64 autograd."""
+    x = rnd(M, K, seed=25).requires_grad_(True)
+    w = rnd(N, K, seed=26, scale=K ** -0.5).requires_grad_(True)
+    b = rnd(N, seed=27, scale=0.1).requires_grad_(True)
+    r = rnd(M, N, seed=28).requires_grad_(True)
+    gy = rnd(M, N, seed=29)
+    y = train_fns.linear(x, w, b, residual=r)
+    (y * gy).sum().backward()
+    x64, w64, b64, r64 = (t.detach().double().requires_grad_(True) for t in (x, w, b, r))
+    ref = F.linear(x64, w64, b64) + r64
+    (ref * gy.double()).sum().backward()
+    assert rel(y, ref) < 1e-5
+    for a, b_ in ((x.grad, x64.grad), (w.grad, w64.grad), (b.grad, b64.grad), (r.grad, r64.grad)):
+        assert rel(a, b_) < 1e-5
+
+
 def test_mlp_relu_adjoint_folded_into_dgrad_gemm():
     """ViT MLP: Linear(ReLU) -> Linear with the first layer's ReLU adjoint applied in the second
     layer's input-gradient GEMM epilogue (mhada_gemm relu = 2, the mask in r) gives the bits of the
