@@ -23,10 +23,8 @@ for s in "$@"; do
     c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
     trainclock) timeout -k 10 180 python -u tools/attn_clock.py dkv > $OUT/train_clock.log 2>&1 || exit 6 ;;
     winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py ${WINO_KNOB:-wino_ws} > $OUT/wino_${WINO_KNOB:-wino_ws}_ab.log 2>&1 || exit 9 ;;
-    winoab3) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0,xknob=0 -c wino_ws=0,xknob=1 -c wino_ws=1 -c wino_ws=2 > $OUT/wino_ab3.log 2>&1 || exit 9 ;;
     vit) timeout -k 10 600 $PYT tests/test_gpu_train_ops.py tests/test_gpu_train.py -k "linear_fn or vit_training or batch_axis or batched or bit_identical or golden or 256_b2 or rccl" > $OUT/vit_tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 15 ;;
-    winoab2) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0 -c wino_ws=2 -c wino_ws=3 > $OUT/wino_ab2.log 2>&1 || exit 9 ;;
-    winoab4) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0,xknob=0 -c wino_ws=0,xknob=2 -c wino_ws=0,xknob=3 > $OUT/wino_ab4.log 2>&1 || exit 9 ;;
+    winoab2) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0 -c wino_ws=1 -c wino_ws=2 > $OUT/wino_ab2.log 2>&1 || exit 9 ;;
     winopk) timeout -k 10 300 $PYT tests/test_gpu_kernels.py -k "wino_persistent" > $OUT/wino_pk_tests.log 2>&1 || exit 14 ;;
     winotests) timeout -k 10 300 $PYT tests/test_gpu_kernels.py tests/test_gpu_train_ops.py -k "wino or chain" > $OUT/wino_tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 11 ;;
     winodbg) for shp in ${WINO_DBG_SHAPES:-"8 128 256 256" "8 256 128 128" "8 64 512 512"}; do
