@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 10 (mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 11 (mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -180,6 +180,10 @@ int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const f
  * that this call fills from v.  Same outputs as mhada_attn_train_fwd (ABI 10). */
 int mhada_attn_train_fwd_vt(const float* q, const float* k, const float* v, float* vt, const float* x,
                             float* out, float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
+/* dst [BH][64][ldt] = src [BH][N][64] transposed per problem (columns N..ldt-1 zero; ldt % 64 == 0,
+ * ldt >= N): K^T, the W operand of the dQ = dS K GEMM after mhada_attn_train_dkv's dS spill
+ * (replaces the strided aten copy k.transpose(1, 2).contiguous()) (ABI 11). */
+int mhada_transpose64(const float* src, float* dst, int BH, int N, int ldt, mhada_stream_t stream);
 int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
                          const float* dmo, const float* dd, float* dq, float* dk, float* dv,
                          int BH, int Nc, int Ns, mhada_stream_t stream);

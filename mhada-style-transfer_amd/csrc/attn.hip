@@ -182,7 +182,9 @@ MHADA_DEV void attn_train_epilogue(const AttnP& p, const f32x16 (&O)[4], float l
 }
 
 // fp32 V'^T | V'^2^T image [BH][128][ldt] (natural key order, zero padded) of the training v
-// [BH][Ns][64] rows: the PV operand layout of attn_f32_kernel.
+// [BH][Ns][64] rows: the PV operand layout of attn_f32_kernel.  SQ = false: the plain transpose
+// [BH][64][ldt] (mhada_transpose64: K^T, the W operand of the backward's dQ = dS K GEMM).
+template <bool SQ = true>
 __global__ void __launch_bounds__(256) train_vt_kernel(const float* __restrict__ v, float* __restrict__ vt, int Ns,
                                                        int ldt) {
   __shared__ float tile[64][65];
@@ -193,12 +195,12 @@ __global__ void __launch_bounds__(256) train_vt_kernel(const float* __restrict__
     tile[n][o] = (n0 + n < Ns) ? src[(long long)(n0 + n) * 64 + o] : 0.f;
   }
   __syncthreads();
-  float* dst = vt + (long long)bh * 128 * ldt + n0;
+  float* dst = vt + (long long)bh * (SQ ? 128 : 64) * ldt + n0;
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int o = i >> 6, n = i & 63;
     const float x = tile[n][o];
     dst[(long long)o * ldt + n] = x;
-    dst[(long long)(64 + o) * ldt + n] = x * x;
+    if constexpr (SQ) dst[(long long)(64 + o) * ldt + n] = x * x;
   }
 }
 
@@ -1626,7 +1628,16 @@ extern "C" int mhada_attn_train_fwd_vt(const float* q, const float* k, const flo
   const long long nblk = (long long)BH * p.nqb;
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn_train_fwd_vt: grid too large");
   p.nblk = (int)nblk;
-  hipLaunchKernelGGL(train_vt_kernel, dim3(p.ldt / 64, BH), dim3(256), 0, s, v, vt, Ns, p.ldt);
+  hipLaunchKernelGGL(train_vt_kernel<true>, dim3(p.ldt / 64, BH), dim3(256), 0, s, v, vt, Ns, p.ldt);
   hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX, 8, true>), dim3(p.nblk), dim3(512), 0, s, p);
   return check_launch("mhada_attn_train_fwd_vt");
+}
+
+// dst [BH][64][ldt] = src [BH][N][64] transposed per problem, columns N .. ldt - 1 zero: K^T for the
+// training backward's dQ = dS K GEMM (replaces aten's strided k.transpose(1, 2).contiguous()).
+extern "C" int mhada_transpose64(const float* src, float* dst, int BH, int N, int ldt, mhada_stream_t s_) {
+  if (!src || !dst || BH <= 0 || N <= 0 || ldt < N || ldt % 64) return fail("mhada_transpose64: bad args (ldt % 64 == 0, >= N)");
+  if (BH > 65535) return fail("mhada_transpose64: BH > 65535");
+  hipLaunchKernelGGL(train_vt_kernel<false>, dim3(ldt / 64, BH), dim3(256), 0, (hipStream_t)s_, src, dst, N, ldt);
+  return check_launch("mhada_transpose64");
 }

@@ -69,6 +69,7 @@ SIGNATURES = {
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
+    "mhada_transpose64": (_I, [_vp, _vp, _I, _I, _I, _vp]),
     "mhada_attn_train_bwd": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_attn_train_dkv": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
@@ -133,7 +134,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 def get_tuning(name: str) -> int:

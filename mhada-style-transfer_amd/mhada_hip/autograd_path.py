@@ -212,7 +212,12 @@ def block_forward_fused(blk, fc: torch.Tensor, fs: torch.Tensor, fcs: torch.Tens
         k = _head_proj(blk.g_list, F.instance_norm(fs), H).contiguous()
         v = _head_proj(blk.h_list, fs, H)
         x = _heads_rows(F.instance_norm(fcs), H)
-    vmu = v.mean(dim=1, keepdim=True)
+    # V is centred per (head, image, channel) before the moments (E2' - M'^2 without cancellation)
+    # and the mean added back: out = S x + A (v - c) + c = S x + A v for ANY per-row-constant c
+    # (softmax rows sum to 1; the variance is shift-invariant), so d out / d c = 0 and c is
+    # detached — its gradient terms (sum over Nc of dout, minus the mean of dv) are exact zeros the
+    # backward would otherwise spend five kernels per block on
+    vmu = v.detach().mean(dim=1, keepdim=True)
     o = MHAdaAttnFn.apply(q, k, (v - vmu).contiguous(), x) + vmu
     if fc.is_cuda:  # out_conv (1x1) as a token GEMM on the HIP kernels
         from . import train_fns

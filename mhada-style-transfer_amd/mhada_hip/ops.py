@@ -504,6 +504,19 @@ def ds_spill_eligible(BH: int, Nc: int, Ns: int) -> bool:
     return Ns % 4 == 0 and 4 * BH * Nc * Ns <= DS_SPILL_BYTES and (Nc + 32) * Ns <= DS_SPILL_MAX_ROWS
 
 
+def transpose64(x: torch.Tensor) -> torch.Tensor:
+    """``mhada_transpose64``: fp32 [BH][N][64] -> [BH][64][ceil64(N)] (columns >= N zero)."""
+    _need_gpu(x)
+    if x.dtype != torch.float32 or x.dim() != 3 or x.shape[-1] != 64:
+        raise ValueError("transpose64: fp32 [BH][N][64]")
+    x = x.contiguous()
+    BH, N, _ = x.shape
+    ldt = (N + 63) // 64 * 64
+    out = torch.empty(BH, 64, ldt, device=x.device, dtype=torch.float32)
+    _call("mhada_transpose64", x, x.data_ptr(), out.data_ptr(), BH, N, ldt)
+    return out
+
+
 def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
     """``mhada_attn_train_bwd``: returns dq (BH, Nc, 64), dk, dv (BH, Ns, 64).  With the dS spill
     (default when ``ds_spill_eligible``): ``mhada_attn_train_dkv`` writes dS and dQ = dS K runs as
@@ -529,9 +542,10 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
     ds = torch.empty(BH, Nc, Ns, device=q.device, dtype=torch.float32)
     _call("mhada_attn_train_dkv", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
           dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, Nc, Ns)
-    kt = k.transpose(1, 2).contiguous()  # W[n = d][k = key] of the NT GEMM
+    kt = transpose64(k)  # W[n = d][k = key] of the NT GEMM, rows padded to ceil64(Ns)
+    ldt = kt.shape[-1]
     gemm(a=ds, w=kt, c=dq, M=Nc, N=64, K=Ns, compute=torch.float32, lda=Ns, sa=(Nc * Ns, 0), nb=(BH, 1),
-         ldw=Ns, sw=(64 * Ns, 0), ldc=64, sc=(Nc * 64, 0))
+         ldw=ldt, sw=(64 * ldt, 0), ldc=64, sc=(Nc * 64, 0))
     return dq, dk, dv
 
 

@@ -235,3 +235,15 @@ def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, vt, BH, Nc, Ns, scale):
     ref = _ref(qd, kd, vd, x.double())
     err32 = _rel(_ref(q, k, v, x).double(), ref)
     assert _rel(out.double().cpu(), ref) < max(2e-4, 4 * err32)
+
+
+@pytest.mark.parametrize("BH,N", [(3, 300), (2, 64), (1, 4096), (4, 7)])
+def test_transpose64_is_the_exact_transpose(BH, N):
+    """mhada_transpose64 (K^T for the dS-spill dQ GEMM): [BH][N][64] -> [BH][64][ceil64(N)], the
+    transpose bit for bit, the padding columns zero."""
+    x = torch.randn(BH, N, 64, generator=torch.Generator().manual_seed(N)).to(DEV)
+    t = ops.transpose64(x)
+    ldt = (N + 63) // 64 * 64
+    assert t.shape == (BH, 64, ldt)
+    assert torch.equal(t[..., :N], x.transpose(1, 2))
+    assert bool((t[..., N:] == 0).all())
