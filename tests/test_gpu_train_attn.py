@@ -241,7 +241,7 @@ def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, vt, BH, Nc, Ns, scale):
 def test_transpose64_is_the_exact_transpose(BH, N):
     """mhada_transpose64 (K^T for the dS-spill dQ GEMM): [BH][N][64] -> [BH][64][ceil64(N)], the
     transpose bit for bit, the padding columns zero."""
-    x = torch.randn(BH, N, 64, generator=torch.Generator().manual_seed(N)).to(DEV)
+    x = torch.randn(BH, N, 64, generator=torch.Generator().manual_seed(N)).cuda()
     t = ops.transpose64(x)
     ldt = (N + 63) // 64 * 64
     assert t.shape == (BH, 64, ldt)
