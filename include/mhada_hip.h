@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 11 (mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 12 (mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -301,6 +301,14 @@ int mhada_pos_embed_bwd(const float* g, float* gpos, int C, int bh, int bw, int 
  * alpha / beta / mu [B][C] (all null: no statistics term), t [B][P][C] (null: no MSE term), kp a
  * device scalar (null: 1); C % 4 == 0, 16-byte aligned pointers.  relu = 1 (ABI 10): x is a ReLU
  * output and g is multiplied by its adjoint (x > 0) (the producing conv then skips mhada_relu_bwd). */
+/* Forward statistics of one feature map x (NHWC fp32 [B][P][C], C % 4 == 0) for the losses of
+ * lossfn.py:7-47: mu / sd [B][C] = the per-channel mean and UNBIASED std over the P pixels (x.mean /
+ * x.std(dim=(2,3))), and with a target t (same layout) mse[0] = mean((x - t)^2) (F.mse_loss) — one
+ * read of x (and t), fp64 partial sums reduced in a fixed order.  mu / sd may be NULL (then t and
+ * mse are required); work: mhada_feat_stats_work(B, P, C) doubles (ABI 12). */
+long long mhada_feat_stats_work(int B, long long P, int C);
+int mhada_feat_stats(const float* x, const float* t, float* mu, float* sd, float* mse, double* work,
+                     long long work_doubles, int B, long long P, int C, mhada_stream_t stream);
 int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha, const float* beta,
                         const float* kp, float ks, float* g, int B, long long P, int C, int relu, mhada_stream_t stream);
 /* ReLU backward on the saved output: dx = dy * (y > 0); n % 4 == 0 (dx may alias dy). */

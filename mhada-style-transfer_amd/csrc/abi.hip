@@ -75,7 +75,7 @@ const Tuning& tuning() {
 
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 11; }  // 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
+extern "C" int mhada_abi_version(void) { return 12; }  // 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }
 

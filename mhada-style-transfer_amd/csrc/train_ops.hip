@@ -1261,6 +1261,148 @@ extern "C" int mhada_relu_bwd(const float* dy, const float* y, float* dx, long l
   return check_launch("mhada_relu_bwd");
 }
 
+namespace mhada {
+// ---------------------------------------------------------------------------------------
+// Forward statistics of one VGG feature map for the losses (lossfn.py:7-47): per (b, c) the mean
+// and the UNBIASED std over the P pixels (x.mean / x.std(dim=(2,3))) and, with a target t, the
+// sum of (x - t)^2 (F.mse_loss numerator) — ONE read of x (and t) in place of aten's mean,
+// Welford-std and mse passes.  NHWC storage [B][P][C]; fp64 partial sums per (split, b, c) and
+// per (split, b, channel block), reduced in a fixed order (deterministic).
+// grid (C/64, B, splits), 256 threads = 64 channels x 4 row phases (in_partial_kernel's layout).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) feat_stats_partial_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ t,
+                                                                 double* __restrict__ work, double* __restrict__ sse,
+                                                                 int B, long long P, int C, int splits, int stats) {
+  __shared__ double red[3][16][65];
+  const int quad = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + 4 * quad;
+  const int b = blockIdx.y, s = blockIdx.z;
+  const long long per = (P + splits - 1) / splits;
+  const long long r0 = s * per, r1 = min(P, r0 + per);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0}, se = 0.0;
+  if (c0 < C) {  // C % 4 == 0 (checked by the entry point)
+    const float* xb = x + (long long)b * P * C + c0;
+    const float* tb = t ? t + (long long)b * P * C + c0 : nullptr;
+#pragma unroll 4
+    for (long long r = r0 + ph; r < r1; r += 16) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xb + r * C);
+      if (stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = (double)v[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+      }
+      if (tb) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(tb + r * C);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = (double)v[e] - (double)w[e];
+          se += d * d;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][ph][4 * quad + e] = s1[e];
+    red[1][ph][4 * quad + e] = s2[e];
+  }
+  red[2][ph][quad] = se;
+  __syncthreads();
+  if (threadIdx.x < 128 && stats) {
+    const int tt = threadIdx.x & 63, which = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + tt;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += red[which][k][tt];
+    if (c < C) work[(((long long)s * B + b) * C + c) * 2 + which] = a;
+  }
+  if (threadIdx.x == 128 && t) {
+    double a = 0.0;
+    for (int k = 0; k < 16; ++k)
+      for (int q = 0; q < 16; ++q) a += red[2][k][q];
+    sse[((long long)s * B + b) * gridDim.x + blockIdx.x] = a;
+  }
+}
+
+// mean / unbiased std per (b, c) from the partials (16 outputs x 16 split phases per block, as
+// in_finalize_kernel); block 0 also sums the sse partials in index order into mse = sse / n.
+__global__ void __launch_bounds__(256) feat_stats_finalize_kernel(const double* __restrict__ work,
+                                                                  const double* __restrict__ sse, float* __restrict__ mu,
+                                                                  float* __restrict__ sd, float* __restrict__ mse, int B,
+                                                                  long long P, int C, int splits, int nsse,
+                                                                  double inv_n, int stats) {
+  __shared__ double red[2][16][17];
+  const int o = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int idx = blockIdx.x * 16 + o;
+  if (stats) {
+    double a = 0.0, q = 0.0;
+    if (idx < B * C) {
+      for (int s = ph; s < splits; s += 16) {
+        a += work[((long long)s * B * C + idx) * 2];
+        q += work[((long long)s * B * C + idx) * 2 + 1];
+      }
+    }
+    red[0][ph][o] = a;
+    red[1][ph][o] = q;
+    __syncthreads();
+    if (ph == 0 && idx < B * C) {
+      double sa = 0.0, sq = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        sa += red[0][k][o];
+        sq += red[1][k][o];
+      }
+      const double mean = sa / (double)P;
+      double var = P > 1 ? (sq - mean * sa) / (double)(P - 1) : 0.0;
+      if (var < 0.0) var = 0.0;
+      mu[idx] = (float)mean;
+      sd[idx] = (float)sqrt(var);
+    }
+  }
+  if (mse && blockIdx.x == 0 && threadIdx.x == 0) {
+    double a = 0.0;
+    for (int i = 0; i < nsse; ++i) a += sse[i];
+    mse[0] = (float)(a * inv_n);
+  }
+}
+
+}  // namespace mhada
+
+extern "C" int mhada_feat_stats(const float* x, const float* t, float* mu, float* sd, float* mse, double* work,
+                                long long work_doubles, int B, long long P, int C, mhada_stream_t s_) {
+  const bool stats = mu && sd;
+  if (!x || B <= 0 || P <= 0 || C <= 0 || C % 4 || !al16(x) || (t && !al16(t)) || (!stats && !(t && mse)) ||
+      (bool)t != (bool)mse || !work)
+    return fail("mhada_feat_stats: bad args (C % 4 == 0, 16-byte aligned; mean + std and / or t + mse)");
+  const int cb = (C + 63) / 64;
+  int splits = (int)std::min<long long>(std::max<long long>(1, (4 * 256 + (long long)B * cb - 1) / ((long long)B * cb)),
+                                        std::max<long long>(1, P / 64));
+  splits = std::min(splits, 65535);
+  const long long need = (long long)splits * B * C * 2 + (long long)splits * B * cb;
+  if (work_doubles < need) return fail("mhada_feat_stats: workspace too small (mhada_feat_stats_work)");
+  double* sse = work + (long long)splits * B * C * 2;
+  const hipStream_t s = (hipStream_t)s_;
+  hipLaunchKernelGGL(feat_stats_partial_kernel, dim3(cb, B, splits), dim3(256), 0, s, x, t, work, sse, B, P, C, splits,
+                     stats ? 1 : 0);
+  if (int rc = check_launch("mhada_feat_stats/partial")) return rc;
+  hipLaunchKernelGGL(feat_stats_finalize_kernel, dim3(stats ? (B * C + 15) / 16 : 1), dim3(256), 0, s, work, sse, mu, sd,
+                     mse, B, P, C, splits, splits * B * cb, 1.0 / ((double)B * P * C), stats ? 1 : 0);
+  return check_launch("mhada_feat_stats/finalize");
+}
+
+extern "C" long long mhada_feat_stats_work(int B, long long P, int C) {
+  if (B <= 0 || P <= 0 || C <= 0) return 0;
+  const int cb = (C + 63) / 64;
+  long long splits = std::min<long long>(std::max<long long>(1, (4 * 256 + (long long)B * cb - 1) / ((long long)B * cb)),
+                                         std::max<long long>(1, P / 64));
+  splits = std::min<long long>(splits, 65535);
+  return splits * B * C * 2 + splits * B * cb;
+}
+
 extern "C" int mhada_feat_loss_bwd(const float* x, const float* t, const float* mu, const float* alpha,
                                    const float* beta, const float* kp, float ks, float* g, int B, long long P,
                                    int C, int relu, mhada_stream_t s_) {

@@ -90,6 +90,8 @@ SIGNATURES = {
     "mhada_attn_train_bwd_prep": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
+    "mhada_feat_stats_work": (_c_ll, [_I, _c_ll, _I]),
+    "mhada_feat_stats": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _I, _c_ll, _I, _vp]),
     "mhada_feat_loss_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _F, _vp, _I, _c_ll, _I, _I, _vp]),
     "mhada_reflect_fold": (_I, [_vp, _vp, _I, _I, _I, _I, _vp, _vp]),
     "mhada_maxpool2": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
@@ -134,7 +136,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 def get_tuning(name: str) -> int:

@@ -673,6 +673,30 @@ def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return dx
 
 
+def feat_stats(x: torch.Tensor, t: Optional[torch.Tensor] = None, stats: bool = True):
+    """``mhada_feat_stats`` on NHWC storage x [B][H][W][C] fp32 (t the same shape, or None):
+    (mean [B][C], unbiased std [B][C]) or (None, None) without ``stats``, and mean((x - t)^2) as a
+    0-dim fp32 device tensor (None without t)."""
+    _need_gpu(x, t)
+    B, H, W, C = x.shape
+    for u in (x, t):
+        if u is not None and (u.dtype != torch.float32 or not u.is_contiguous()):
+            raise ValueError("feat_stats: contiguous fp32 NHWC operands")
+    if t is not None and t.shape != x.shape:
+        raise ValueError("feat_stats: target shape")
+    if not stats and t is None:
+        raise ValueError("feat_stats: nothing to compute")
+    P = H * W
+    nwork = int(_lib.load().mhada_feat_stats_work(B, P, C))
+    work = torch.empty(max(1, nwork), device=x.device, dtype=torch.float64)
+    mu = torch.empty(B, C, device=x.device, dtype=torch.float32) if stats else None
+    sd = torch.empty(B, C, device=x.device, dtype=torch.float32) if stats else None
+    mse = torch.empty((), device=x.device, dtype=torch.float32) if t is not None else None
+    ptr = lambda u: None if u is None else u.data_ptr()  # noqa: E731
+    _call("mhada_feat_stats", x, x.data_ptr(), ptr(t), ptr(mu), ptr(sd), ptr(mse), work.data_ptr(), nwork, B, P, C)
+    return mu, sd, mse
+
+
 def feat_loss_bwd(x: torch.Tensor, mu: Optional[torch.Tensor], alpha: Optional[torch.Tensor],
                   beta: Optional[torch.Tensor], t: Optional[torch.Tensor], ks: float,
                   kp: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:

@@ -128,7 +128,7 @@ class Trainer:
         """global_style_loss, local_feature_loss and identity_loss_2 (lossfn.py:7-47) with each
         VGG feature map's terms on train_fns.FeatureLossFn: the same loss values, summed in the
         reference's order, and one backward pass per feature map."""
-        from .train_fns import feature_loss_terms
+        from .train_fns import feature_loss_terms, feature_mean_std
         gs = lf = id2 = 0
         for i in (1, 2, 3, 4, 5):
             k = f"relu{i}_1"
@@ -136,7 +136,7 @@ class Trainer:
             if i >= 3:  # lossfn.py:26-34: the AdaAttN target of the content / style features
                 t = self.no_learn[i - 3](fc[k], fs[k], L.feature_down_sample(fc, i), L.feature_down_sample(fs, i))
             m = i >= 2 and self.masked_vgg_features  # relu2_1 .. relu5_1 from vgg19_forward(masked_features=True)
-            lm, ls, lmse = feature_loss_terms(fcs[k], fs[k].mean(dim=(2, 3)), fs[k].std(dim=(2, 3)), t, relu_input=m)
+            lm, ls, lmse = feature_loss_terms(fcs[k], *feature_mean_std(fs[k]), t, relu_input=m)
             gs = gs + (lm + ls)  # lossfn.py:21: loss += mean_dist + std_dist
             if t is not None:
                 lf = lf + lmse

@@ -440,8 +440,9 @@ class FeatureLossFn(torch.autograd.Function):
     """The loss terms of train_image.py on ONE VGG feature map x (an NCHW view of NHWC storage):
       l_mean = mse(mean_hw(x), ref_mean), l_std = mse(std_hw(x), ref_std)  (lossfn.py:7-23; ref given)
       l_mse  = mse(x, t)                            (lossfn.py:26-34 and 41-47; t given)
-    The forward evaluates them with the reference's own aten expressions (same values); the
-    backward writes dL/dx = g_mean 2(mu - mu_r) / (BC HW) + g_std 2(sd - sd_r)(x - mu) / (BC (HW-1) sd)
+    On the device the forward takes the three reductions from ONE pass (mhada_feat_stats: fp64
+    partial sums, fixed order — the aten values up to their fp32 summation order); on the CPU the
+    reference's own aten expressions.  The backward writes dL/dx = g_mean 2(mu - mu_r) / (BC HW) + g_std 2(sd - sd_r)(x - mu) / (BC (HW-1) sd)
     + g_mse 2(x - t) / numel in ONE mhada_feat_loss_bwd pass, in place of ATen's mse / std / mean
     backward chains and the adds that sum the terms of a feature map."""
 
@@ -456,13 +457,22 @@ class FeatureLossFn(torch.autograd.Function):
         zero = x.new_zeros(())
         lm = ls = lmse = zero
         mu = sd = None
-        if ref_mean is not None:
-            mu = x.mean(dim=(2, 3))
-            sd = x.std(dim=(2, 3))
-            lm = F.mse_loss(mu, ref_mean)
-            ls = F.mse_loss(sd, ref_std)
-        if t is not None:
-            lmse = F.mse_loss(x, t)
+        xs, ts = _nhwc(x), None if t is None else _nhwc(t)
+        if xs is not None and (t is None or ts is not None) and (ref_mean is not None or t is not None):
+            mu, sd, m = ops.feat_stats(xs, ts, stats=ref_mean is not None)
+            if ref_mean is not None:
+                lm = F.mse_loss(mu, ref_mean)
+                ls = F.mse_loss(sd, ref_std)
+            if t is not None:
+                lmse = m
+        else:
+            if ref_mean is not None:
+                mu = x.mean(dim=(2, 3))
+                sd = x.std(dim=(2, 3))
+                lm = F.mse_loss(mu, ref_mean)
+                ls = F.mse_loss(sd, ref_std)
+            if t is not None:
+                lmse = F.mse_loss(x, t)
         ctx.save_for_backward(x, t, mu, sd, ref_mean, ref_std)
         return lm, ls, lmse
 
@@ -492,6 +502,24 @@ class FeatureLossFn(torch.autograd.Function):
         g = ops.feat_loss_bwd(xs, mu.contiguous() if alpha is not None else None, alpha, beta, tt, 2.0 / x.numel(), kp,
                               relu=ctx.relu_input)
         return g.permute(0, 3, 1, 2), None, None, None, None
+
+
+def _nhwc(x: torch.Tensor):
+    """x's NHWC storage as a contiguous [B][H][W][C] fp32 device view, or None (CPU, other layout)."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] % 4:
+        return None
+    v = x.permute(0, 2, 3, 1)
+    return v if v.is_contiguous() else None
+
+
+def feature_mean_std(x: torch.Tensor):
+    """(x.mean(dim=(2, 3)), x.std(dim=(2, 3))) of a feature map: one mhada_feat_stats pass on the
+    device (calc_mean_std of lossfn.py:10-19 for the style targets)."""
+    xs = _nhwc(x)
+    if xs is None:
+        return x.mean(dim=(2, 3)), x.std(dim=(2, 3))
+    mu, sd, _ = ops.feat_stats(xs)
+    return mu, sd
 
 
 def feature_loss_terms(x, ref_mean=None, ref_std=None, t=None, relu_input: bool = False):

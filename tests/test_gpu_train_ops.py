@@ -351,6 +351,25 @@ def test_linear_fn_fused_residual(M, K, N):
         assert rel(a, b_) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,C", [(2, 5, 7, 64), (3, 33, 20, 128), (1, 1, 2, 4), (2, 64, 64, 512), (8, 128, 128, 64)])
+def test_feat_stats_vs_fp64(B, H, W, C):
+    """mhada_feat_stats (the losses' per-channel mean / unbiased std and mse in one pass) against
+    fp64 torch on channels-last feature maps."""
+    g = torch.Generator().manual_seed(B * H * W + C)
+    x = (torch.rand(B, C, H, W, generator=g) * 3).to(DEV).contiguous(memory_format=torch.channels_last)
+    t = (torch.rand(B, C, H, W, generator=g) * 3).to(DEV).contiguous(memory_format=torch.channels_last)
+    mu, sd, mse = ops.feat_stats(x.permute(0, 2, 3, 1), t.permute(0, 2, 3, 1))
+    xd, td = x.double(), t.double()
+    torch.testing.assert_close(mu.double(), xd.mean(dim=(2, 3)), rtol=1e-6, atol=1e-6)
+    if H * W > 1:
+        torch.testing.assert_close(sd.double(), xd.std(dim=(2, 3)), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mse.double(), ((xd - td) ** 2).mean(), rtol=1e-6, atol=0)
+    mu2, sd2, none = ops.feat_stats(x.permute(0, 2, 3, 1))
+    assert none is None and torch.equal(mu2, mu) and torch.equal(sd2, sd)
+    _, _, mse2 = ops.feat_stats(x.permute(0, 2, 3, 1), t.permute(0, 2, 3, 1), stats=False)
+    assert torch.equal(mse2, mse)
+
+
 def test_mlp_relu_adjoint_folded_into_dgrad_gemm():
     """ViT MLP: Linear(ReLU) -> Linear with the first layer's ReLU adjoint applied in the second
     layer's input-gradient GEMM epilogue (mhada_gemm relu = 2, the mask in r) gives the bits of the
