@@ -35,6 +35,9 @@ for s in "$@"; do
                timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/winopmc2_$v -o run -- python3 tools/wino_only.py $v > $OUT/winopmc2_$v.log 2>&1 || exit 13
                timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum --output-format csv -d $OUT/winopmc3_$v -o run -- python3 tools/wino_only.py $v > $OUT/winopmc3_$v.log 2>&1 || exit 13
              done ;;
+    lapmc) timeout -k 10 120 python -u tools/lossattn_only.py 5 > $OUT/lossattn_time.log 2>&1 || exit 16
+           timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_LDS --output-format csv -d $OUT/lapmc -o run -- python3 tools/lossattn_only.py 2 > $OUT/lapmc.log 2>&1 || exit 16
+           timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/lapmc2 -o run -- python3 tools/lossattn_only.py 2 > $OUT/lapmc2.log 2>&1 || exit 16 ;;
     dkvpmc) for v in 0 1; do
               timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_LDS --output-format csv -d $OUT/dkvpmc_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc_$v.log 2>&1 || exit 10
               timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/dkvpmc2_$v -o run -- python3 tools/dkv_only.py $v > $OUT/dkvpmc2_$v.log 2>&1 || exit 10
