@@ -132,13 +132,14 @@ __global__ void __launch_bounds__(64 * W) loss_attn_kernel(const LossAttnP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        S[r] = key < p.Ns ? S[r] * kLog2e : -INFINITY;
+        S[r] *= kLog2e;
+        if (key0 + 32 > p.Ns && key >= p.Ns) S[r] = -INFINITY;  // uniform test first: tail tile only
         mx = fmaxf(mx, S[r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       if (mx > m2 + kLossRescaleThr || tt == 0) {  // per-lane (query) decision; O rows are per query
         const float mn = fmaxf(m2, mx);
-        const float alpha = m2 == -INFINITY ? 0.f : exp2f(m2 - mn);
+        const float alpha = m2 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
         l *= alpha;
 #pragma unroll
         for (int i = 0; i < 2 * NB; ++i)
@@ -149,7 +150,7 @@ __global__ void __launch_bounds__(64 * W) loss_attn_kernel(const LossAttnP p) {
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        S[r] = exp2f(S[r] - m2);
+        S[r] = __builtin_amdgcn_exp2f(S[r] - m2);  // bare v_exp_f32 (no denormal range fix-up)
         sum += S[r];
       }
       l += sum;
@@ -328,13 +329,14 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        S[r] = key < p.Ns ? S[r] * kLog2e : -INFINITY;
+        S[r] *= kLog2e;
+        if (key0 + 32 > p.Ns && key >= p.Ns) S[r] = -INFINITY;  // uniform test first: tail tile only
         mx = fmaxf(mx, S[r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       if (mx > m2 + kLossRescaleThr || tt == 0) {
         const float mn = fmaxf(m2, mx);
-        const float alpha = m2 == -INFINITY ? 0.f : exp2f(m2 - mn);
+        const float alpha = m2 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
         l *= alpha;
 #pragma unroll
         for (int i = 0; i < 2 * NB; ++i)
@@ -345,7 +347,7 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        S[r] = exp2f(S[r] - m2);
+        S[r] = __builtin_amdgcn_exp2f(S[r] - m2);  // bare v_exp_f32 (no denormal range fix-up)
         sum += S[r];
       }
       l += sum;
