@@ -1185,6 +1185,196 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 }
 
 // ------------------------------------------------------------------------------------
+// fp32 persistent GEMM, ONE barrier per K-tile (round 4; tuning gemm_f32b, ROWS A only).
+// The ping-pong kernel hands the MFMA pipe from one wave group to the other 8 times per
+// K-tile; at 32 fp32 MFMAs (2048 cycles) per phase each hand-over costs the barrier round
+// trip plus the first fragment reads, and the pipe measured busy 83 % of the active cycles
+// (profiles/r03_gemm_pmc.txt).  Here all 8 waves run the same schedule; per K-tile j (ring slot
+// j & 1, the same 2-slot [A0|A1|W0|W1] image with XOR-swizzled 128-B rows as gemm_ppp_kernel):
+//   1. ds_read the fragments of k-half 1 of K-tile j            (buffer B)
+//   2. 64 MFMAs on k-half 0                                        (buffer A, read earlier)
+//   3. wait for this wave's DMA of K-tile j+1, lgkmcnt(0), barrier: every wave is done with
+//      slot j & 1 and K-tile j+1 is visible
+//   4. 8 MFMAs on k-half 1, then the DMA of K-tile j+2 into slot j & 1 and the k-half-0
+//      fragments of K-tile j+1 (buffer A), then the other 56 MFMAs on k-half 1
+// so a wave reaches the barrier with its MFMAs issued and leaves it with operands already in
+// registers; the K-tile stream continues across this workgroup's tiles (the next tile's first
+// fragments are read before the epilogue).  Wave (grp, wc) owns rows grp*128 .. +127 and
+// columns wc*64 .. +63 of the 256x256 tile (4 x 2 blocks of v_mfma_f32_32x32x2_f32).
+// ------------------------------------------------------------------------------------
+template <typename TO>
+__global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total) {
+  constexpr int BK = 32, PE = 256, HALF = 128 * BK, TILE = 4 * HALF, SCR = 8 * 1024;
+  __shared__ __attribute__((aligned(16))) float smem[2 * TILE + SCR];  // 128 KiB ring + 32 KiB epilogue scratch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wc = wave & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int G = gridDim.x;
+  const float* A = reinterpret_cast<const float*>(p.a);
+  const float* W = reinterpret_cast<const float*>(p.w);
+
+  // staging: wave w DMAs rows 16w + 8i + (lane >> 3) of each 128-row half, logical 16-B chunk
+  // (lane & 7) ^ swz(row) into physical slot lane & 7 (swz(row) = (row >> 1) & 7 = 4i + (lane >> 4))
+  int cofs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) cofs[i] = 4 * ((lane & 7) ^ (4 * i + (lane >> 4)));
+  struct Tile { int m0, n0, z1, z2; };
+  auto setup = [&](int w) {
+    const int lg = xcd_remap(w, total);
+    const int z = lg / p.ntiles, t = lg - z * p.ntiles;
+    const int tm = t / p.tiles_n;
+    Tile s;
+    s.z1 = z / p.nb2;
+    s.z2 = z - s.z1 * p.nb2;
+    s.m0 = tm * 256;
+    s.n0 = (t - tm * p.tiles_n) * 256;
+    return s;
+  };
+  auto stage = [&](const Tile& s, int kt, int slot) {
+    const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
+    const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
+    float* dst = smem + slot * TILE + wave * 2 * PE;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rr = 128 * hh + 16 * wave + 8 * i + (lane >> 3);
+        const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
+        glds16(ab + (unsigned)(m * p.lda + cofs[i]), dst + hh * HALF + PE * i);
+        glds16(wb + (unsigned)(n * p.ldw + cofs[i]), dst + (2 + hh) * HALF + PE * i);
+      }
+  };
+
+  // fragments (as gemm_ppp_kernel's fp32 form): lane half h supplies k = 16h + 4c + e at MFMA
+  // step e of k-quarter c (logical 16-B chunk 4h + c of the row); one quarter = 4 A + 2 W chunks
+  const int swz = (r32 >> 1) & 7;
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = 4 * ((4 * h + ks) ^ swz);
+  const float* sA = smem + grp * HALF + r32 * BK;
+  const float* sW = smem + (2 + (wc >> 1)) * HALF + (64 * (wc & 1) + r32) * BK;
+  struct Frags { f32x4 a[4], w[2]; };
+  Frags fx, fy;
+  auto read = [&](int c, int cb, Frags& f) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) f.a[mt] = *reinterpret_cast<const f32x4*>(sA + cb * TILE + mt * 32 * BK + koff[c]);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) f.w[nt] = *reinterpret_cast<const f32x4*>(sW + cb * TILE + nt * 32 * BK + koff[c]);
+  };
+  f32x16 acc[4][2];
+  // MFMA steps e0 .. e1-1 of one k-quarter (8 independent accumulators per step)
+  auto compute = [&](const Frags& f, int e0, int e1) {
+#pragma unroll
+    for (int e = e0; e < e1; ++e)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w[nt][e], f.a[mt][e], acc[mt][nt], 0, 0, 0);
+  };
+  // accumulator init: zero, or (p.rinit) the tile's residual rows + bias (as gemm_ppp_kernel)
+  auto init_acc = [&](const Tile& s) {
+    if constexpr (sizeof(TO) == 4) {
+      if (p.rinit) {
+        const float* rb = reinterpret_cast<const float*>(p.r) + s.z1 * p.sr1 + s.z2 * p.sr2;
+        const float* bb = p.bias ? p.bias + s.z1 * p.sb1 + s.z2 * p.sb2 : nullptr;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = s.n0 + wc * 64 + nt * 32 + 8 * g + 4 * h;
+            const bool nok = n + 3 < p.N;
+            const f32x4 b4 = (bb && nok) ? *reinterpret_cast<const f32x4*>(bb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+              const int m = s.m0 + grp * 128 + mt * 32 + r32;
+              f32x4 r4 = {0.f, 0.f, 0.f, 0.f};
+              if (nok && m < p.M) r4 = *reinterpret_cast<const f32x4*>(rb + (long long)m * p.ldr + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[mt][nt][4 * g + e] = r4[e] + b4[e];
+            }
+          }
+        return;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  };
+  GemmP pe = p;
+  if (p.rinit) {
+    pe.r = nullptr;
+    pe.bias = nullptr;
+  }
+
+  const int KT = p.K / BK;
+  int cb = 0;
+  // One K-tile (fx holds its k-quarter-0 fragments on entry; each quarter's fragments are read
+  // while the previous quarter's 32 MFMAs run).  (s2, k2, a2): the K-tile two ahead (staged into
+  // this K-tile's slot); more: a next K-tile exists (block-uniform); epi: the previous tile's
+  // epilogue stores (>= 32 per wave, full tile) were issued after the DMA this wait covers, so
+  // they may stay in flight.
+  auto ktile = [&](const Tile& s2, int k2, bool a2, bool more, bool epi) __attribute__((always_inline)) {
+    read(1, cb, fy);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(fx, 0, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    read(2, cb, fx);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(fy, 0, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    read(3, cb, fy);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(fx, 0, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      if (epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PP_LGKM0();
+      PP_BARRIER();
+    }
+    compute(fy, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (a2) stage(s2, k2, cb);
+    if (more) read(0, cb ^ 1, fx);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(fy, 1, 4);
+    cb ^= 1;
+  };
+
+  int w = blockIdx.x;
+  Tile cur = setup(w), nxt = cur;
+  bool has_nxt = w + G < total;
+  if (has_nxt) nxt = setup(w + G);
+  init_acc(cur);
+  stage(cur, 0, 0);
+  stage(cur, 1, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  PP_BARRIER();
+  read(0, 0, fx);
+  bool pre = false;  // this tile's first K-tile waits behind the previous epilogue's stores
+  while (true) {
+    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 2, true, true, kt == 0 && pre);
+    ktile(nxt, 0, has_nxt, true, KT == 2 && pre);
+    ktile(nxt, 1, has_nxt, has_nxt, false);
+    pre = has_nxt && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
+    __builtin_amdgcn_sched_barrier(0);
+    float* scr = smem + 2 * TILE + wave * 1024;
+    store_tile_lds<TO, 4, 2>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * 64, lane, scr);
+    if (!has_nxt) break;
+    init_acc(nxt);
+    cur = nxt;
+    w += G;
+    has_nxt = w + G < total;
+    if (has_nxt) nxt = setup(w + G);
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // fp32 GEMM for N <= 64 columns over long K (the attention backward's dQ = dS K: M = Nc, K = Ns,
 // one problem per (batch, head); the grouped per-head 1x1 convs).  Streaming A is the whole
 // cost: at the fp32 MFMA rate a 128x64 tile consumes 8 B/clk/CU of A, ~5 TB/s chip-wide, so the
@@ -1325,6 +1515,21 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   return fail("mhada_gemm: no ping-pong form");
 }
 
+template <typename TO>
+static int launch_gemm_f32b(const GemmP& p0, int nz, hipStream_t stream) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + 255) / 256;
+  p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
+  p.lds_epi = 1;
+  p.rinit = (sizeof(TO) == 4 && p.r && !p.relu && tuning().gemm_rinit && ((uintptr_t)p.r & 15) == 0 &&
+             p.ldr % 4 == 0 && p.sr1 % 4 == 0 && p.sr2 % 4 == 0 && p.N % 4 == 0) ? 1 : 0;
+  const long long total = (long long)p.ntiles * nz;
+  if (total >= (1LL << 31)) return fail("mhada_gemm: too many tiles");
+  const int grid = (int)std::min<long long>(total, num_cus());
+  hipLaunchKernelGGL((gemm_f32b_kernel<TO>), dim3(grid), dim3(512), 0, stream, p, (int)total);
+  return check_launch("mhada_gemm");
+}
+
 // The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
 // spans addressable with 32-bit element offsets.  tuning gemm_pp = 0 disables it (A/B runs).
 static bool pp_enabled() { return tuning().gemm_pp != 0; }
@@ -1413,8 +1618,11 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
     if constexpr (sizeof(TA) == 4 && (AMODE == MHADA_A_ROWS || AMODE == MHADA_A_CONV3X3 || AMODE == MHADA_A_CONV3X3_ZERO)) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
-          pp_offsets_fit(p, AMODE))
+          pp_offsets_fit(p, AMODE)) {
+        if constexpr (AMODE == MHADA_A_ROWS)
+          if (tuning().gemm_f32b) return launch_gemm_f32b<TO>(p, nz, s);
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
+      }
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)
     }
     return launch_gemm<TC, TA, TO, AMODE, 128, 128, 2, 2>(p, nz, s);

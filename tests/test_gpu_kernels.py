@@ -53,6 +53,34 @@ def test_linear(cdt, M, N, K):
     assert rel(y2, ref2) < TOL[cdt] + (4e-3 if cdt == torch.bfloat16 else 0)
 
 
+@pytest.mark.parametrize("M,N,K", [(70000, 1024, 64), (70000, 768, 512), (32400, 512, 2048), (57000, 600, 96),
+                                   (65536, 2048, 512)])
+def test_gemm_f32b_bit_identical_to_pingpong(M, N, K):
+    """The one-barrier fp32 kernel (tuning gemm_f32b = 1) accumulates every output in the ping-pong
+    kernel's k order from the same initial value, so bias / ReLU / residual (preloaded or not) /
+    bf16 copy outputs are bit-identical; several tiles per CU, K = 2 and 3 K-tiles, partial row
+    and column tiles."""
+    x = rnd(M, K, seed=1)
+    w = rnd(N, K, scale=K ** -0.5, seed=2)
+    b = rnd(N, seed=3)
+    r = rnd(M, N, seed=4)
+    outs = {}
+    for knob in (0, 1):
+        with _lib.tuning(gemm_f32b=knob):
+            c2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            y0 = torch.empty(M, N, device=DEV)
+            ops.gemm(a=x, w=w, c=y0, M=M, N=N, K=K, compute=torch.float32, lda=K, ldw=K, bias=b, ldc=N,
+                     c2=c2, ldc2=N)
+            outs[knob] = (ops.linear(x, w, b, torch.float32, residual=r),
+                          ops.linear(x, w, b, torch.float32, relu=True),
+                          ops.linear(x, w, None, torch.float32), y0, c2)
+            torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    ref = x[:512].double() @ w.double().T + b.double() + r[:512].double()
+    assert rel(outs[1][0][:512], ref) < TOL[torch.float32]
+
+
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 def test_linear_fp32_input_converted_on_load(cdt):
     x = rnd(300, 512, seed=5)

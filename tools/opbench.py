@@ -41,9 +41,9 @@ def with_env(key, val, fn, *a, **k):
         return fn(*a, **k)
 
 
-def gemm_suite():
+def gemm_suite(dts=(torch.bfloat16, torch.float32)):
     dev = "cuda"
-    for dt in (torch.bfloat16, torch.float32):
+    for dt in dts:
         M = 65536 if dt == torch.bfloat16 else 32768
         for (N, K, out, res, relu) in [(1536, 512, dt, False, False), (2048, 512, dt, False, True),
                                        (512, 2048, torch.float32, True, False), (512, 512, torch.float32, True, False)]:
@@ -67,6 +67,8 @@ def gemm_suite():
             else:
                 fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
+                fns["f32b"] = lambda: with_env("MHADA_GEMM_F32B", "1", ops.linear, x, w, b, out, residual=r,
+                                               relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
@@ -194,6 +196,8 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     if what in ("gemm", "all"):
         gemm_suite()
+    if what == "gemm32":
+        gemm_suite((torch.float32,))
     if what in ("gemmk",):
         gemm_k_suite()
     if what in ("n64",):
