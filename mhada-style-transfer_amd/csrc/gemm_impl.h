@@ -1254,14 +1254,33 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
   for (int ks = 0; ks < 4; ++ks) koff[ks] = 4 * ((4 * h + ks) ^ swz);
   const float* sA = smem + grp * HALF + r32 * BK;
   const float* sW = smem + (2 + (wc >> 1)) * HALF + (64 * (wc & 1) + r32) * BK;
+  // The fragment reads are inline asm with counted waits whose "+v" operands tie each quarter's
+  // registers to the wait before its MFMAs: hipcc's own wait insertion emitted lgkmcnt(0) there
+  // (it cannot count across the loop back-edge), which exposed every quarter's LDS latency in
+  // all 8 waves at once.
   struct Frags { f32x4 a[4], w[2]; };
   Frags fx, fy;
+  const unsigned lA = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)sA;
+  const unsigned lW = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)sW;
   auto read = [&](int c, int cb, Frags& f) {
+    const unsigned a0 = lA + (unsigned)(cb * TILE + koff[c]) * 4u, w0 = lW + (unsigned)(cb * TILE + koff[c]) * 4u;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) f.a[mt] = *reinterpret_cast<const f32x4*>(sA + cb * TILE + mt * 32 * BK + koff[c]);
+    for (int mt = 0; mt < 4; ++mt)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[mt]) : "v"(a0 + mt * 32 * BK * 4));
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) f.w[nt] = *reinterpret_cast<const f32x4*>(sW + cb * TILE + nt * 32 * BK + koff[c]);
+    for (int nt = 0; nt < 2; ++nt)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(f.w[nt]) : "v"(w0 + nt * 32 * BK * 4));
   };
+  // wait until at most N LDS reads are outstanding; f's registers are defined by this wait
+  auto wait_frags = [&](Frags& f, auto n) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.w[0]), "+v"(f.w[1])
+                 : "i"(decltype(n)::value));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using N6 = std::integral_constant<int, 6>;
+  using N0 = std::integral_constant<int, 0>;
   f32x16 acc[4][2];
   // MFMA steps e0 .. e1-1 of one k-quarter (8 independent accumulators per step)
   auto compute = [&](const Frags& f, int e0, int e1) {
@@ -1320,23 +1339,23 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
   // they may stay in flight.
   auto ktile = [&](const Tile& s2, int k2, bool a2, bool more, bool epi) __attribute__((always_inline)) {
     read(1, cb, fy);
-    __builtin_amdgcn_sched_barrier(0);
+    wait_frags(fx, N6{});
     compute(fx, 0, 4);
     __builtin_amdgcn_sched_barrier(0);
     read(2, cb, fx);
-    __builtin_amdgcn_sched_barrier(0);
+    wait_frags(fy, N6{});
     compute(fy, 0, 4);
     __builtin_amdgcn_sched_barrier(0);
     read(3, cb, fy);
-    __builtin_amdgcn_sched_barrier(0);
+    wait_frags(fx, N6{});
     compute(fx, 0, 4);
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
       if (epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      PP_LGKM0();
-      PP_BARRIER();
     }
+    wait_frags(fy, N0{});
+    if (more) PP_BARRIER();
     compute(fy, 0, 1);
     __builtin_amdgcn_sched_barrier(0);
     if (a2) stage(s2, k2, cb);
