@@ -1231,6 +1231,17 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
     s.n0 = (t - tm * p.tiles_n) * 256;
     return s;
   };
+  // piece e of 4 of a K-tile's staging (half e >> 1, row group e & 1 of A and W)
+  auto stage_part = [&](const Tile& s, int kt, int slot, int e) {
+    const int hh = e >> 1, i = e & 1;
+    const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
+    const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
+    float* dst = smem + slot * TILE + wave * 2 * PE;
+    const int rr = 128 * hh + 16 * wave + 8 * i + (lane >> 3);
+    const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
+    glds16(ab + (unsigned)(m * p.lda + cofs[i]), dst + hh * HALF + PE * i);
+    glds16(wb + (unsigned)(n * p.ldw + cofs[i]), dst + (2 + hh) * HALF + PE * i);
+  };
   auto stage = [&](const Tile& s, int kt, int slot) {
     const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
     const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
@@ -1356,12 +1367,16 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
     }
     wait_frags(fy, N0{});
     if (more) PP_BARRIER();
-    compute(fy, 0, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (a2) stage(s2, k2, cb);
-    if (more) read(0, cb ^ 1, fx);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(fy, 1, 4);
+    // the DMA of K-tile j+2 in four pieces between the MFMA steps (a burst of 8 LDS-DMA issues
+    // per wave in all waves at once stalls the issue of the MFMAs behind it)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      compute(fy, e, e + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (a2) stage_part(s2, k2, cb, e);
+      if (e == 2 && more) read(0, cb ^ 1, fx);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     cb ^= 1;
   };
 
