@@ -1185,27 +1185,29 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 }
 
 // ------------------------------------------------------------------------------------
-// fp32 persistent GEMM, ONE barrier per K-tile (round 4; tuning gemm_f32b, ROWS A only).
-// The ping-pong kernel hands the MFMA pipe from one wave group to the other 8 times per
-// K-tile; at 32 fp32 MFMAs (2048 cycles) per phase each hand-over costs the barrier round
-// trip plus the first fragment reads, and the pipe measured busy 83 % of the active cycles
-// (profiles/r03_gemm_pmc.txt).  Here all 8 waves run the same schedule; per K-tile j (ring slot
-// j & 1, the same 2-slot [A0|A1|W0|W1] image with XOR-swizzled 128-B rows as gemm_ppp_kernel):
-//   1. ds_read the fragments of k-half 1 of K-tile j            (buffer B)
-//   2. 64 MFMAs on k-half 0                                        (buffer A, read earlier)
-//   3. wait for this wave's DMA of K-tile j+1, lgkmcnt(0), barrier: every wave is done with
-//      slot j & 1 and K-tile j+1 is visible
-//   4. 8 MFMAs on k-half 1, then the DMA of K-tile j+2 into slot j & 1 and the k-half-0
-//      fragments of K-tile j+1 (buffer A), then the other 56 MFMAs on k-half 1
-// so a wave reaches the barrier with its MFMAs issued and leaves it with operands already in
-// registers; the K-tile stream continues across this workgroup's tiles (the next tile's first
-// fragments are read before the epilogue).  Wave (grp, wc) owns rows grp*128 .. +127 and
-// columns wc*64 .. +63 of the 256x256 tile (4 x 2 blocks of v_mfma_f32_32x32x2_f32).
+// fp32 persistent GEMM, ONE barrier per 16-deep K-tile, 4-slot ring (round 4; tuning
+// gemm_f32b, ROWS A only).  The ping-pong kernel hands the MFMA pipe from one wave group to
+// the other 8 times per 32-deep K-tile and its 2-slot ring (3 x 64 KiB does not fit beside the
+// epilogue scratch) gives a K-tile's DMA 3-5 phases to land.  Here all 8 waves run the same
+// schedule over 16-deep K-tiles (64-B rows: A 256 x 16 | W 256 x 16 = 32 KiB per slot, 4 slots);
+// per K-tile j (slot j & 3):
+//   1. ds_read the k-quarter-1 fragments of K-tile j, 32 MFMAs on quarter 0 (read earlier)
+//   2. wait for this wave's DMA of K-tile j+1 (issued 3 K-tiles ago), lgkmcnt(0), barrier:
+//      every wave is done with slot j & 3 and K-tile j+1 is visible
+//   3. 8 MFMAs on quarter 1, the DMA of K-tile j+4 into slot j & 3 and the quarter-0 fragments
+//      of K-tile j+1, the other 24 MFMAs
+// The fragment reads are inline asm with counted waits whose "+v" operands tie each quarter's
+// registers to the wait before its MFMAs (hipcc's own wait insertion emitted lgkmcnt(0) there:
+// it cannot count across the loop back-edge).  The K-tile stream continues across this
+// workgroup's tiles.  Wave (grp, wc) owns rows grp*128 .. +127 and columns wc*64 .. +63 of the
+// 256x256 tile (4 x 2 blocks of v_mfma_f32_32x32x2_f32).  Row layout: 16-B chunk c of row r
+// sits at slot c ^ ((r >> 2) & 3), which spreads each 16-lane group of a ds_read_b128 (16 rows,
+// one logical chunk) over all 64 banks.
 // ------------------------------------------------------------------------------------
 template <typename TO>
 __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total) {
-  constexpr int BK = 32, PE = 256, HALF = 128 * BK, TILE = 4 * HALF, SCR = 8 * 1024;
-  __shared__ __attribute__((aligned(16))) float smem[2 * TILE + SCR];  // 128 KiB ring + 32 KiB epilogue scratch
+  constexpr int BK = 16, PE = 256, HALF = 256 * BK, SLOT = 2 * HALF, NS = 4, SCR = 8 * 1024;
+  __shared__ __attribute__((aligned(16))) float smem[NS * SLOT + SCR];  // 128 KiB ring + 32 KiB epilogue scratch
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wc = wave & 3;
@@ -1214,11 +1216,9 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
   const float* A = reinterpret_cast<const float*>(p.a);
   const float* W = reinterpret_cast<const float*>(p.w);
 
-  // staging: wave w DMAs rows 16w + 8i + (lane >> 3) of each 128-row half, logical 16-B chunk
-  // (lane & 7) ^ swz(row) into physical slot lane & 7 (swz(row) = (row >> 1) & 7 = 4i + (lane >> 4))
-  int cofs[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) cofs[i] = 4 * ((lane & 7) ^ (4 * i + (lane >> 4)));
+  // staging: one 1-KiB DMA = 16 rows x 64 B; lane L -> row 16i + (L >> 2) of the wave's 32-row
+  // band, physical chunk L & 3, logical chunk (L & 3) ^ (L >> 4)
+  const int cofs = 4 * ((lane & 3) ^ (lane >> 4));
   struct Tile { int m0, n0, z1, z2; };
   auto setup = [&](int w) {
     const int lg = xcd_remap(w, total);
@@ -1231,56 +1231,37 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
     s.n0 = (t - tm * p.tiles_n) * 256;
     return s;
   };
-  // piece e of 4 of a K-tile's staging (half e >> 1, row group e & 1 of A and W)
-  auto stage_part = [&](const Tile& s, int kt, int slot, int e) {
-    const int hh = e >> 1, i = e & 1;
-    const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
-    const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
-    float* dst = smem + slot * TILE + wave * 2 * PE;
-    const int rr = 128 * hh + 16 * wave + 8 * i + (lane >> 3);
-    const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
-    glds16(ab + (unsigned)(m * p.lda + cofs[i]), dst + hh * HALF + PE * i);
-    glds16(wb + (unsigned)(n * p.ldw + cofs[i]), dst + (2 + hh) * HALF + PE * i);
-  };
   auto stage = [&](const Tile& s, int kt, int slot) {
     const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
     const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
-    float* dst = smem + slot * TILE + wave * 2 * PE;
+    float* dst = smem + slot * SLOT + wave * 2 * PE;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int rr = 128 * hh + 16 * wave + 8 * i + (lane >> 3);
-        const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
-        glds16(ab + (unsigned)(m * p.lda + cofs[i]), dst + hh * HALF + PE * i);
-        glds16(wb + (unsigned)(n * p.ldw + cofs[i]), dst + (2 + hh) * HALF + PE * i);
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int rr = 32 * wave + 16 * i + (lane >> 2);
+      const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
+      glds16(ab + (unsigned)(m * p.lda + cofs), dst + PE * i);
+      glds16(wb + (unsigned)(n * p.ldw + cofs), dst + HALF + PE * i);
+    }
   };
 
-  // fragments (as gemm_ppp_kernel's fp32 form): lane half h supplies k = 16h + 4c + e at MFMA
-  // step e of k-quarter c (logical 16-B chunk 4h + c of the row); one quarter = 4 A + 2 W chunks
-  const int swz = (r32 >> 1) & 7;
-  int koff[4];
+  // fragments: lane half h supplies k = 8h + 4c + e at MFMA step e of k-quarter c (logical
+  // chunk 2h + c of its row); one quarter = 4 A + 2 W chunks
+  const int swz = (r32 >> 2) & 3;
+  int koff[2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) koff[ks] = 4 * ((4 * h + ks) ^ swz);
-  const float* sA = smem + grp * HALF + r32 * BK;
-  const float* sW = smem + (2 + (wc >> 1)) * HALF + (64 * (wc & 1) + r32) * BK;
-  // The fragment reads are inline asm with counted waits whose "+v" operands tie each quarter's
-  // registers to the wait before its MFMAs: hipcc's own wait insertion emitted lgkmcnt(0) there
-  // (it cannot count across the loop back-edge), which exposed every quarter's LDS latency in
-  // all 8 waves at once.
+  for (int c = 0; c < 2; ++c) koff[c] = 4 * ((2 * h + c) ^ swz);
+  const unsigned lA = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(smem + (grp * 128 + r32) * BK);
+  const unsigned lW = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(smem + HALF + (wc * 64 + r32) * BK);
   struct Frags { f32x4 a[4], w[2]; };
   Frags fx, fy;
-  const unsigned lA = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)sA;
-  const unsigned lW = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)sW;
-  auto read = [&](int c, int cb, Frags& f) {
-    const unsigned a0 = lA + (unsigned)(cb * TILE + koff[c]) * 4u, w0 = lW + (unsigned)(cb * TILE + koff[c]) * 4u;
+  auto read = [&](int c, int slot, Frags& f) {
+    const unsigned o = (unsigned)(slot * SLOT + koff[c]) * 4u;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
-      asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[mt]) : "v"(a0 + mt * 32 * BK * 4));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[mt]) : "v"(lA + o + mt * 32 * BK * 4));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
-      asm volatile("ds_read_b128 %0, %1" : "=v"(f.w[nt]) : "v"(w0 + nt * 32 * BK * 4));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(f.w[nt]) : "v"(lW + o + nt * 32 * BK * 4));
   };
   // wait until at most N LDS reads are outstanding; f's registers are defined by this wait
   auto wait_frags = [&](Frags& f, auto n) {
@@ -1341,43 +1322,38 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
     pe.bias = nullptr;
   }
 
-  const int KT = p.K / BK;
-  int cb = 0;
-  // One K-tile (fx holds its k-quarter-0 fragments on entry; each quarter's fragments are read
-  // while the previous quarter's 32 MFMAs run).  (s2, k2, a2): the K-tile two ahead (staged into
-  // this K-tile's slot); more: a next K-tile exists (block-uniform); epi: the previous tile's
-  // epilogue stores (>= 32 per wave, full tile) were issued after the DMA this wait covers, so
-  // they may stay in flight.
-  auto ktile = [&](const Tile& s2, int k2, bool a2, bool more, bool epi) __attribute__((always_inline)) {
-    read(1, cb, fy);
-    wait_frags(fx, N6{});
-    compute(fx, 0, 4);
-    __builtin_amdgcn_sched_barrier(0);
-    read(2, cb, fx);
-    wait_frags(fy, N6{});
-    compute(fy, 0, 4);
-    __builtin_amdgcn_sched_barrier(0);
-    read(3, cb, fy);
+  const int KT = p.K / BK;  // >= 4 (K >= 64, checked on the host)
+  int sl = 0;               // ring slot of the current K-tile
+  // One K-tile (fx holds its quarter-0 fragments on entry).  (s2, k2, a2): the K-tile four ahead,
+  // staged into this K-tile's slot; more: a next K-tile exists (block-uniform); nw: LDS-DMA /
+  // store operations issued after this wave's DMA of the next K-tile (the wait leaves them in
+  // flight): 4 per staged K-tile among the two before this one, + 32 epilogue stores when the
+  // previous tile (full) ended within the last three K-tiles
+  auto ktile = [&](const Tile& s2, int k2, bool a2, bool more, int nw) __attribute__((always_inline)) {
+    read(1, sl, fy);
     wait_frags(fx, N6{});
     compute(fx, 0, 4);
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
-      if (epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      switch (nw) {  // s_waitcnt takes an immediate
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+        case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+        case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
     }
     wait_frags(fy, N0{});
     if (more) PP_BARRIER();
-    // the DMA of K-tile j+2 in four pieces between the MFMA steps (a burst of 8 LDS-DMA issues
-    // per wave in all waves at once stalls the issue of the MFMAs behind it)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      compute(fy, e, e + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (a2) stage_part(s2, k2, cb, e);
-      if (e == 2 && more) read(0, cb ^ 1, fx);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    cb ^= 1;
+    compute(fy, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (a2) stage(s2, k2, sl);
+    sl = (sl + 1) & (NS - 1);
+    if (more) read(0, sl, fx);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(fy, 1, 4);
   };
 
   int w = blockIdx.x;
@@ -1385,19 +1361,23 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
   bool has_nxt = w + G < total;
   if (has_nxt) nxt = setup(w + G);
   init_acc(cur);
-  stage(cur, 0, 0);
-  stage(cur, 1, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < NS; ++k) stage(cur, k, k);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   PP_BARRIER();
   read(0, 0, fx);
-  bool pre = false;  // this tile's first K-tile waits behind the previous epilogue's stores
+  bool pre = false;  // the previous tile was full: its 32 epilogue stores per wave are in the count
   while (true) {
-    for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 2, true, true, kt == 0 && pre);
-    ktile(nxt, 0, has_nxt, true, KT == 2 && pre);
-    ktile(nxt, 1, has_nxt, has_nxt, false);
+    const int e = pre ? 32 : 0;
+    for (int kt = 0; kt + 4 < KT; ++kt) ktile(cur, kt + 4, true, true, 8 + (kt < 3 ? e : 0));
+    const int hn = has_nxt ? 4 : 0;
+    ktile(nxt, 0, has_nxt, true, 8 + (KT - 4 < 3 ? e : 0));
+    ktile(nxt, 1, has_nxt, true, 4 + hn + (KT - 3 < 3 ? e : 0));
+    ktile(nxt, 2, has_nxt, true, 2 * hn + (KT - 2 < 3 ? e : 0));
+    ktile(nxt, 3, has_nxt, has_nxt, 8);
     pre = has_nxt && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
     __builtin_amdgcn_sched_barrier(0);
-    float* scr = smem + 2 * TILE + wave * 1024;
+    float* scr = smem + NS * SLOT + wave * 1024;
     store_tile_lds<TO, 4, 2>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * 64, lane, scr);
     if (!has_nxt) break;
     init_acc(nxt);
