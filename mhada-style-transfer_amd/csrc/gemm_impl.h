@@ -896,8 +896,13 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
 // Needs two K-tiles (K >= 128 bf16 / 64 fp32: the A lookahead never skips a whole tile).
 // fp32 form: same 128-B rows (BK = 32), v_mfma_f32_32x32x2_f32, 32 MFMAs per phase.
 // ------------------------------------------------------------------------------------
-template <typename TC, typename TO, int AMODE, int BN>
+template <typename TC, typename TO, int AMODE, int BN, bool P2 = false>
 __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total) {
+  // P2 (fp32, BN = 256; tuning gemm_f32b = 2): two phases per K-tile of 64 MFMAs (both column
+  // blocks of one k-pair) instead of four of 32 — half the hand-overs of the MFMA pipe; A and
+  // W of K-tile g+1 are staged together in phase 0 of K-tile g (into the slot of g-1, which both
+  // groups have left) and waited for in phase 1.
+  static_assert(!P2 || (sizeof(TC) == 4 && BN == 256), "P2: fp32 256-column form only");
   // 128-B operand rows: BK = 64 bf16 or 32 fp32; CE elements per 16-B chunk, PE per 1-KiB piece.
   // BN = 256: each wave owns 128 rows x 64 columns (TN = 2 column blocks, 4 phases per K-tile);
   // BN = 128 (N <= 128 layers): 128 rows x 32 columns (TN = 1, 2 phases), one W half per stage;
@@ -1077,8 +1082,12 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   zero_acc(cur);
   stage_a(cur, 0, 0, 0); stage_a(cur, 1, 0, 0); stage_w(cur, 0, 0, 0);
   if constexpr (NWH == 2) stage_w(cur, 1, 0, 0);
-  stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if constexpr (P2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
   PP_BARRIER();
   if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
 
@@ -1094,6 +1103,22 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   auto ktile = [&](const St& s1, const int k1, const bool w1, const St& s2, const int k2, const bool a2,
                    const bool wx) __attribute__((always_inline)) {
     const int cb = sl0;
+    if constexpr (P2) {
+      // phase 0: k-pair 0, both column blocks; stage K-tile g+1 (A and W) into the free slot
+      read_a(0, cb); read_w(0, 0, cb); read_w(1, 0, cb);
+      if (w1) {
+        stage_a(s1, 0, k1, sl1); stage_a(s1, 1, k1, sl1);
+        stage_w(s1, 0, k1, sl1); stage_w(s1, 1, k1, sl1);
+      }
+      PP_LGKM0(); PP_BARRIER(); compute(0); compute(1); PP_BARRIER();
+      // phase 1: k-pair 1; this wave's DMA of K-tile g+1 has landed before the barrier
+      read_a(1, cb); read_w(0, 1, cb); read_w(1, 1, cb);
+      if (wx) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(EPI_MIN) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PP_LGKM0(); PP_BARRIER(); compute(0); compute(1); PP_BARRIER();
+      sl0 ^= 1; sl1 ^= 1; sl2 ^= 1;
+      return;
+    }
     if constexpr (TN == 2) {
       // phase 0
       read_a(0, cb); read_w(0, 0, cb);
@@ -1156,6 +1181,9 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     // K-tile raised register spills and measured slower)
     pre = AMODE == MHADA_A_ROWS && has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
     if (pre) {
+      if constexpr (P2) {
+        stage_a(nxt, 0, 1, sl1); stage_a(nxt, 1, 1, sl1);
+      }
       stage_w(nxt, 0, 1, sl1);
       if constexpr (NWH == 2) stage_w(nxt, 1, 1, sl1);
     }
@@ -1519,6 +1547,12 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   const long long total = (long long)p.ntiles * nz;
   if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
+    if constexpr (sizeof(TC) == 4 && BN == 256 && AMODE == MHADA_A_ROWS) {
+      if (tuning().gemm_f32b == 2) {
+        hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN, true>), dim3(grid), dim3(512), 0, stream, p, (int)total);
+        return check_launch("mhada_gemm");
+      }
+    }
     hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN>), dim3(grid), dim3(512), 0, stream, p, (int)total);
     return check_launch("mhada_gemm");
   }
@@ -1634,7 +1668,7 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE)) {
         if constexpr (AMODE == MHADA_A_ROWS)
-          if (tuning().gemm_f32b) return launch_gemm_f32b<TO>(p, nz, s);
+          if (tuning().gemm_f32b == 1) return launch_gemm_f32b<TO>(p, nz, s);
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       }
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)
