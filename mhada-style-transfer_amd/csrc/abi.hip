@@ -65,7 +65,7 @@ bool valid(const char* name, int v) {
   if (!strcmp(name, "attn_sched")) return v == 0 || (v >= 3 && v <= 8);
   if (!strcmp(name, "xknob")) return v >= 0 && v < 16;
   if (!strcmp(name, "wino_ws")) return v >= 0 && v <= 2;
-  if (!strcmp(name, "gemm_f32b")) return v >= 0 && v <= 2;
+  if (!strcmp(name, "gemm_f32b")) return v >= 0 && v <= 3;
   return v == 0 || v == 1;
 }
 }  // namespace

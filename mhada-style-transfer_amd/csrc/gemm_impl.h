@@ -1667,8 +1667,10 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE)) {
-        if constexpr (AMODE == MHADA_A_ROWS)
+        if constexpr (AMODE == MHADA_A_ROWS) {
           if (tuning().gemm_f32b == 1) return launch_gemm_f32b<TO>(p, nz, s);
+          if (tuning().gemm_f32b == 3) return launch_gemm_pp<float, TO, AMODE, 128>(p, nz, s);
+        }
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       }
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)

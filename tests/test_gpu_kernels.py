@@ -65,7 +65,7 @@ def test_gemm_f32b_matches_pingpong(M, N, K):
     b = rnd(N, seed=3)
     r = rnd(M, N, seed=4)
     outs = {}
-    for knob in (0, 1, 2):
+    for knob in (0, 1, 2, 3):
         with _lib.tuning(gemm_f32b=knob):
             c2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
             y0 = torch.empty(M, N, device=DEV)
@@ -78,10 +78,11 @@ def test_gemm_f32b_matches_pingpong(M, N, K):
             torch.cuda.synchronize()
     for a, c in zip(outs[0], outs[1]):
         assert rel(c, a) < 2e-6
-    # gemm_f32b = 2 (the ping-pong kernel with two phases per K-tile) keeps every accumulator's
-    # k order: bit-identical
-    for a, c in zip(outs[0] + (outs[0, "c2"],), outs[2] + (outs[2, "c2"],)):
-        assert torch.equal(a, c)
+    # gemm_f32b = 2 (the ping-pong kernel with two phases per K-tile) and = 3 (its 256x128 tiles)
+    # keep every accumulator's k order: bit-identical
+    for knob in (2, 3):
+        for a, c in zip(outs[0] + (outs[0, "c2"],), outs[knob] + (outs[knob, "c2"],)):
+            assert torch.equal(a, c)
     assert rel(outs[1, "c2"], outs[1][3]) < 4e-3
     # every row tile (last partial) against fp64 on a sample of rows
     rows = torch.cat([torch.arange(0, M, 997), torch.arange(M - 300, M)]).to(DEV)

@@ -71,6 +71,8 @@ def gemm_suite(dts=(torch.bfloat16, torch.float32)):
                                                relu=relu)
                 fns["pp2"] = lambda: with_env("MHADA_GEMM_F32B", "2", ops.linear, x, w, b, out, residual=r,
                                               relu=relu)
+                fns["pp128"] = lambda: with_env("MHADA_GEMM_F32B", "3", ops.linear, x, w, b, out, residual=r,
+                                                relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
