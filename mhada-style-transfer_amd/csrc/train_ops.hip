@@ -1363,10 +1363,17 @@ __global__ void __launch_bounds__(256) feat_stats_finalize_kernel(const double* 
       sd[idx] = (float)sqrt(var);
     }
   }
-  if (mse && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (mse && blockIdx.x == 0) {  // fixed-order block reduction of the per-block sse partials
+    __shared__ double rs[256];
     double a = 0.0;
-    for (int i = 0; i < nsse; ++i) a += sse[i];
-    mse[0] = (float)(a * inv_n);
+    for (int i = threadIdx.x; i < nsse; i += 256) a += sse[i];
+    rs[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) rs[threadIdx.x] += rs[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) mse[0] = (float)(rs[0] * inv_n);
   }
 }
 
