@@ -42,7 +42,7 @@ const Knob kKnobs[] = {
     {"attn_sched", &Tuning::attn_sched},             {"tn_skinny_lds", &Tuning::tn_skinny_lds},
     {"train_dkv_dma", &Tuning::train_dkv_dma},     {"wino_l2pf", &Tuning::wino_l2pf},
     {"wino_ws", &Tuning::wino_ws},                 {"xknob", &Tuning::xknob},
-    {"gemm_f32b", &Tuning::gemm_f32b},
+    {"gemm_f32b", &Tuning::gemm_f32b},             {"gemm_n64_pp", &Tuning::gemm_n64_pp},
 };
 
 Tuning g_tuning;

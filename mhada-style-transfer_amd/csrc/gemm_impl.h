@@ -1656,6 +1656,12 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
         return check_launch("mhada_gemm");
       }
     }
+    // bf16 3x3 conv with <= 64 output channels (the decoder's conv2.1, 128 -> 64): the 256x128
+    // persistent ping-pong form with the upper column half idle (tuning gemm_n64_pp)
+    if constexpr (sizeof(TC) == 2 && sizeof(TA) == 2 && AMODE == MHADA_A_CONV3X3) {
+      if (tuning().gemm_n64_pp && p.K % 64 == 0 && p.K >= 128 && pp_enabled() && pp_offsets_fit(p, AMODE))
+        return launch_gemm_pp<bf16, TO, AMODE, 128>(p, nz, s);
+    }
     if (tuning().gemm_n64 == 256) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
   }

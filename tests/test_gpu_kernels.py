@@ -192,6 +192,27 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
     assert rel(y.permute(0, 3, 1, 2), ref) < TOL[cdt]
 
 
+@pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Ci,Co,H,W", [(2, 128, 64, 64, 64), (1, 256, 64, 33, 20), (3, 128, 40, 17, 70),
+                                         (4, 128, 64, 128, 128)])
+def test_conv3x3_bf16_n64_pingpong(out, B, Ci, Co, H, W):
+    """bf16 3x3 conv with <= 64 output channels on the 256x128 ping-pong kernel (tuning
+    gemm_n64_pp = 1, the upper column half idle) against fp64 and the default 128x64 kernel."""
+    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(Ci + H)).to(DEV, torch.bfloat16)
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, seed=2)
+    b = rnd(Co, seed=3)
+    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).to(torch.bfloat16).contiguous()
+    ys = {}
+    for knob in (0, 1):
+        with _lib.tuning(gemm_n64_pp=knob):
+            ys[knob] = ops.conv3x3(x, wp, b, out, upsample=False)
+            torch.cuda.synchronize()
+    ref = torch.relu(F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
+                              w.to(torch.bfloat16).double(), b.double()))
+    assert rel(ys[1].permute(0, 3, 1, 2), ref) < TOL[torch.bfloat16]
+    assert rel(ys[1], ys[0]) < (1e-5 if out == torch.float32 else 8e-3)
+
+
 @pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
 @pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
                                               (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64),
