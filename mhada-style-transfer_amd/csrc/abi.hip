@@ -43,6 +43,7 @@ const Knob kKnobs[] = {
     {"train_dkv_dma", &Tuning::train_dkv_dma},     {"wino_l2pf", &Tuning::wino_l2pf},
     {"wino_ws", &Tuning::wino_ws},                 {"xknob", &Tuning::xknob},
     {"gemm_f32b", &Tuning::gemm_f32b},             {"gemm_n64_pp", &Tuning::gemm_n64_pp},
+    {"gemm_n64_cen", &Tuning::gemm_n64_cen},
 };
 
 Tuning g_tuning;

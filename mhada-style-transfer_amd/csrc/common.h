@@ -51,6 +51,7 @@ struct Tuning {
   int wino_ws = 0;           // fp32 Winograd conv: 0 wino_kernel; 1 warp-specialised (measured 7 % slower); 2 persistent 16x16x4 (see wino.hip)
   int gemm_f32b = 0;         // fp32 GEMM (ROWS A, N > 128): 0 ping-pong (4 phases per K-tile), 1 one-barrier-per-K-tile kernel, 2 ping-pong with 2 phases, 3 ping-pong 256x128 tiles
   int gemm_n64_pp = 0;       // bf16 3x3 conv, N <= 64: 256x128 persistent ping-pong (upper half idle) instead of the 128x64 tile kernel
+  int gemm_n64_cen = 0;      // fp32 N <= 64 GEMM with centred A (MHAda q projection): LDS-DMA ring kernel with the centring on the fragments
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };

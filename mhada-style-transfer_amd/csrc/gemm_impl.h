@@ -1427,7 +1427,10 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
 // CU (72 KiB each).  Rows are 128 B (32 floats), chunk c of row r at slot c ^ ((r >> 1) & 7)
 // (applied on the source address, as gemm_ppp_kernel: conflict-free ds_read_b128).
 // ------------------------------------------------------------------------------------
-template <int BM, int NS, int BK>
+// CEN (round 4): the centred-A form (kRowsCentred, the MHAda q projection): each A fragment
+// minus the column means p.a_mu in fp32 after its LDS read — the same operand values as the
+// register-staged kernel's centring on load.
+template <int BM, int NS, int BK, bool CEN = false>
 __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   constexpr int NWV = BM / 32, CH = BK / 4, RPI = 64 / CH;  // 16-B chunks per row, rows per DMA instruction
   constexpr int AH = BM * BK, WH = 64 * BK, STAGE = AH + WH;
@@ -1452,6 +1455,7 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   const int m0 = tile * BM;
   const float* ab = reinterpret_cast<const float*>(p.a) + z1 * p.sa1 + z2 * p.sa2;
   const float* wb = reinterpret_cast<const float*>(p.w) + z1 * p.sw1 + z2 * p.sw2;
+  const float* mub = CEN ? p.a_mu + z1 * p.smu1 + z2 * p.smu2 : nullptr;
   // chunk c of LDS row r sits at slot c ^ sw(r): conflict-free ds_read_b128 fragment reads
   auto sw = [](int r) { return CH == 8 ? (r >> 1) & 7 : r & 15; };
   // staging: one DMA instruction = RPI rows x 128 B (lane -> row lane / CH, slot lane % CH)
@@ -1509,6 +1513,10 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int q = 0; q < CH / 2; ++q) wf[n][q] = *reinterpret_cast<const f32x4*>(swp + n * 32 * BK + koff[q]);
+    if constexpr (CEN) {
+#pragma unroll
+      for (int q = 0; q < CH / 2; ++q) af[q] -= *reinterpret_cast<const f32x4*>(mub + kt * BK + 4 * ((CH / 2) * h + q));
+    }
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
@@ -1633,10 +1641,14 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (tuning gemm_n64 = 256
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
   if (p.N <= 64) {
-    if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 && AMODE == MHADA_A_ROWS) {
-      // fp32 rows, K % 32: the LDS-DMA ring kernel
+    if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 &&
+                  (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred)) {
+      // fp32 rows, K % 32: the LDS-DMA ring kernel (centred A: tuning gemm_n64_cen, 16-B aligned means)
+      constexpr bool CEN = AMODE == kRowsCentred;
       if (p.K % 32 == 0 && p.lda % 4 == 0 && p.ldw % 4 == 0 && p.sa1 % 4 == 0 && p.sa2 % 4 == 0 &&
-          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w)) {
+          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w) &&
+          (!CEN || (tuning().gemm_n64_cen && aligned16(p.a_mu) && p.smu1 % 4 == 0 && p.smu2 % 4 == 0 &&
+                    p.K < 1024))) {
         GemmP q = p;
         q.tiles_n = 1;
         // lds_epi (unused by this kernel's direct epilogue) = 4 flags the per-XCD grouping of the
@@ -1648,10 +1660,10 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
         // measured no faster)
         if (p.K >= 1024 && p.K % 64 == 0) {
           q.ntiles = (p.M + 255) / 256;
-          hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
+          if constexpr (!CEN) hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
         } else {
           q.ntiles = (p.M + 127) / 128;
-          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32, CEN>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
         }
         return check_launch("mhada_gemm");
       }

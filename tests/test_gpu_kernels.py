@@ -101,17 +101,21 @@ def test_linear_fp32_input_converted_on_load(cdt):
     assert rel(y, ref) < TOL[cdt]
 
 
-@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
-def test_grouped_centred_projection(cdt):
-    """The MHAda per-head projection pattern: z = (batch, head), A centred per column."""
-    B, H, N, C = 2, 8, 200, 512
+@pytest.mark.parametrize("cdt,ring", [(torch.float32, 0), (torch.float32, 1), (torch.bfloat16, 0)])
+@pytest.mark.parametrize("N", [200, 4096])
+def test_grouped_centred_projection(cdt, ring, N):
+    """The MHAda per-head projection pattern: z = (batch, head), A centred per column; ring = 1:
+    the fp32 LDS-DMA ring kernel with the centring on its fragments (tuning gemm_n64_cen)."""
+    B, H, C = 2, 8, 512
     x = rnd(B, N, C, seed=7) * 3 + 1.5
     mu = x.mean(dim=1)  # [B][C]
     w = rnd(B, H, 64, 64, scale=0.125, seed=8, dtype=cdt)
     bias = rnd(H, 64, seed=9)
     q = torch.empty(B, H, N, 64, device=DEV, dtype=cdt)
-    ops.gemm(a=x, w=w, c=q, M=N, N=64, K=64, compute=cdt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
-             smu=(C, 64), ldw=64, sw=(H * 4096, 4096), bias=bias, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
+    with _lib.tuning(gemm_n64_cen=ring):
+        ops.gemm(a=x, w=w, c=q, M=N, N=64, K=64, compute=cdt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
+                 smu=(C, 64), ldw=64, sw=(H * 4096, 4096), bias=bias, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
+        torch.cuda.synchronize()
     xc = (x - mu[:, None, :]).view(B, N, H, 64).permute(0, 2, 1, 3).to(cdt).double()
     ref = xc @ w.double().transpose(-1, -2) + bias.double()[None, :, None, :]
     assert rel(q, ref) < TOL[cdt]

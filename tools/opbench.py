@@ -198,6 +198,38 @@ def n64_suite():
         del a
 
 
+def proj_suite():
+    """The MHAda block's per-head projections as engine.block_forward issues them (512^2 B8:
+    Nc = Ns = 4096, 8 heads, fp32 and bf16): q (N = 64, centred A) and K|V' (N = 128 with the
+    V'^T image); plus the uncentred q form (which routes to the fp32 LDS-DMA ring kernel)."""
+    dev = "cuda"
+    B, H, N, C = 8, 8, 4096, 512
+    for dt in (torch.float32, torch.bfloat16):
+        x = torch.randn(B, N, C, device=dev)
+        mu = x.mean(dim=1)
+        wq = (torch.randn(B, H, 64, 64, device=dev) / 8).to(dt)
+        wkv = (torch.randn(B, H, 128, 64, device=dev) / 8).to(dt)
+        bq = torch.randn(H, 64, device=dev)
+        bkv = torch.randn(H, 128, device=dev)
+        q = torch.empty(B, H, N, 64, device=dev, dtype=dt)
+        kv = torch.empty(B, H, N, 128, device=dev, dtype=dt)
+        vt = torch.empty(B, H, 128, N, device=dev, dtype=dt)
+        qa = dict(a=x, w=wq, c=q, M=N, N=64, K=64, compute=dt, lda=C, sa=(N * C, 64), nb=(B, H), ldw=64,
+                  sw=(H * 4096, 4096), bias=bq, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
+        ka = dict(a=x, w=wkv, c=kv, M=N, N=128, K=64, compute=dt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
+                  smu=(C, 64), ldw=64, sw=(H * 8192, 8192), bias=bkv, sb=(0, 128), ldc=128,
+                  sc=(H * N * 128, N * 128), vt=vt, ldt=N, svt=(H * 128 * N, 128 * N))
+        fns = {"q": lambda: ops.gemm(a_mu=mu, smu=(C, 64), **qa),
+               "q_n64_256": lambda: with_env("MHADA_GEMM_N64", "256", ops.gemm, a_mu=mu, smu=(C, 64), **qa),
+               "q_ring": lambda: with_env("MHADA_GEMM_N64_CEN", "1", ops.gemm, a_mu=mu, smu=(C, 64), **qa),
+               "q_uncentred": lambda: ops.gemm(**qa),
+               "kv_vt": lambda: ops.gemm(**ka)}
+        t = bench(fns)
+        qb, kb = 4 * B * N * C // 8 + B * H * N * 64 * q.element_size(), 4 * B * N * C // 8 + 3 * B * H * N * 64 * q.element_size()
+        print(f"proj {str(dt)[6:]:8s}: " + "  ".join(
+            f"{k} {v * 1e3:6.1f} us {(kb if k.startswith('kv') else qb) / v / 1e6:6.0f} GB/s" for k, v in t.items()))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     torch.manual_seed(0)
@@ -209,6 +241,8 @@ if __name__ == "__main__":
         gemm_k_suite()
     if what in ("n64",):
         n64_suite()
+    if what == "proj":
+        proj_suite()
     if what in ("conv", "all"):
         conv_suite()
     if what in ("out3", "conv", "all"):
