@@ -22,7 +22,9 @@ no collective on the data path (barrier + max-over-ranks timing only) -> scaling
 
 Roofline: the dominant kernel is the fused MHAda attention (mhada_attn, 6 launches/step);
 its algorithmic FLOPs per launch = 6*Nc*Ns*C*B (QK^T, PV, PV^2; 2 FLOP/MAC), timed live with
-HIP events on its launch stream over the timed region.  CPU baseline (rank 0, N=1): the
+HIP events on its launch stream over the timed region.  After every timed region the same process
+runs a shader-clock probe (csrc/probe.hip) and reports the box's clock under dense MFMA load
+("clock_ghz"; "frac_at_clock" = the fraction of the peak scaled to that clock).  CPU baseline (rank 0, N=1): the
 reference's aten fp32 expression (tests/torch_ref.py, golden-pinned) at B=1 on the job's host
 cores, with the numpy oracle beside it.
 """
@@ -113,6 +115,30 @@ def pmc_traffic(cfg_key):
     return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
+def shader_clock(launches: int = 20, iters: int = 300000) -> float:
+    """The box's sustained shader clock under dense bf16 MFMA load, in GHz, measured in THIS process
+    right after a timed region (mhada_clock_probe, csrc/probe.hip: s_memtime / s_memrealtime around a
+    dependent MFMA chain per workgroup, ~10 ms per launch, `launches` back to back; median over the
+    workgroups of the last launch).  The chip's clock under load differs between boxes by up to
+    ~10 % (MI355X_MICROARCH.md, DVFS give-back), so this number separates a code change from a box
+    change between two bench lines."""
+    from mhada_hip import _lib
+    lib = _lib.load()
+    dev = bench_device()
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    buf = torch.zeros(2 * n, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(launches):
+        _lib.check(lib.mhada_clock_probe(buf.data_ptr(), n, iters, st), "mhada_clock_probe")
+    torch.cuda.synchronize(dev)
+    v = buf.view(n, 2).double().cpu()
+    ghz = (v[:, 0] / v[:, 1].clamp(min=1) * 0.1).sort().values
+    return round(float(ghz[n // 2]), 4)
+
+
+PEAK_CLOCK_GHZ = 2.4  # the clock the dense peaks above are quoted at (MI355X_MICROARCH.md)
+
+
 def build_models(dtype):
     import network
     from mhada_hip.recipe import load_recipe
@@ -158,6 +184,7 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
         elapsed = time.perf_counter() - t0
         engine.record_kernel_events(None)
     assert torch.isfinite(out[1]).all()
+    clock = shader_clock()
     ev = log.get("mhada_attn", [])
     attn_ms = [a.elapsed_time(b) for a, b in ev]
     elapsed = max_over_ranks(elapsed, world)
@@ -178,7 +205,9 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
                      "peak": PEAK_TFLOPS[dts], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dts], 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
                      "avg_launch_ms": round(avg_attn_s * 1e3, 4),
-                     "flop_per_launch": attn_flops, "launches_timed": len(attn_ms)},
+                     "flop_per_launch": attn_flops, "launches_timed": len(attn_ms),
+                     "clock_ghz": clock, "frac_at_clock": round(achieved / (PEAK_TFLOPS[dts] * clock / PEAK_CLOCK_GHZ), 4)},
+        "clock_ghz": clock,
         "config": {"workload": f"stylize {res}x{res} content+style, batch {batch}", "resolution": res,
                    "batch_per_gpu": batch, "global_batch": batch * world, "compute_dtype": dts,
                    "parallelism": f"replicas x{world}"},
@@ -234,6 +263,7 @@ def run_video(dtype, steps, warmup, rank, world):
         elapsed = time.perf_counter() - t0
     assert torch.isfinite(err).all()
     elapsed = max_over_ranks(elapsed, world)
+    clock = shader_clock()
     nc, ns = (H // 8) * (W // 8), (256 // 8) ** 2
     d = 64
     fl = (72 * nc * C * C + 196608 * nc + 6 * (6 * nc * ns * C + 2 * nc * C * d + 2 * nc * C * C)
@@ -241,6 +271,7 @@ def run_video(dtype, steps, warmup, rank, world):
     dts = "f32" if dtype == torch.float32 else "bf16"
     return {"value": steps * world / elapsed, "unit": "frames/s", "ms_per_frame": elapsed / steps * 1e3,
             "dtype": dts, "tflops": fl * steps / elapsed / 1e12, "warping_error_last": float(err[0]),
+            "clock_ghz": clock,
             "config": {"workload": "infer_video.py: 1080x1920 u8 BGR frames -> ingest (cv2_to_tensor) -> stylise "
                                    "against a cached 256x256 style, + warping error",
                        "batch_per_gpu": 1, "compute_dtype": dts, "parallelism": f"replicas x{world}"}}
@@ -325,6 +356,7 @@ def run_train(steps, warmup, rank, world, res=512, batch=8):
     sync()
     el = time.perf_counter() - t0
     el = max_over_ranks(el, world)
+    clock = shader_clock() if dev.type == "cuda" else None
     agree = None
     if world > 1:
         agree = rank_agreement([tr.vit_c, tr.vit_s, tr.ada])
@@ -343,7 +375,7 @@ def run_train(steps, warmup, rank, world, res=512, batch=8):
                                   "dS-spill attention backward, TN weight-gradient GEMMs); losses, Adam and glue on "
                                   "PyTorch-ROCm (DESIGN.md §3b)" if dev.type == "cuda" else
                                   "CPU rehearsal of the rank protocol: the reference's aten expression")},
-            "last_losses": last, "rank_agreement": agree}
+            "last_losses": last, "rank_agreement": agree, "clock_ghz": clock}
 
 
 def rank_agreement(modules) -> dict:
@@ -585,16 +617,18 @@ def main():
             "config": main_cfg["config"],
             "roofline": main_cfg["roofline"],
             "tflops_whole_step": round(main_cfg["tflops_whole_step"], 2),
+            "clock_ghz": main_cfg["clock_ghz"],
         }
         if second is not None:
             line["configs"] = {"1024x1024_b4_bf16": {k: second[k] for k in
                                                     ("value", "ms_per_step", "frames_per_s_per_gpu", "dtype",
-                                                     "tflops_whole_step", "roofline", "config")}}
+                                                     "tflops_whole_step", "roofline", "clock_ghz", "config")}}
         if videos:
             line.setdefault("configs", {}).update(videos)
         if train is not None:
             line.setdefault("configs", {})["train_512_b8_f32"] = {
-                k: train[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "last_losses")}
+                k: train[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "last_losses",
+                                      "clock_ghz")}
         if probes:
             line.setdefault("configs", {}).update(probes)
         if not args.no_cpu_baseline and world == 1:

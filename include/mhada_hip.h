@@ -40,20 +40,31 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 12 (mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 13 (mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
  * measurements and tests that force a rare path.  Initialised ONCE, at the first call into the
  * library, from MHADA_<NAME> environment variables (NAME upper-cased); afterwards only these
  * calls change it (not thread-safe against concurrent launches: set knobs between launches).
- * Knobs (value range): attn_fixed_shift (0|1), attn_waves (4|8), attn_tk (64|128),
- * attn_prio (0|1), vit_attn_vec (0|1), out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1),
- * gemm_persist (0|1), gemm_pp128 (0|1), gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1).
+ * Knobs (value range): attn_fixed_shift (0|1), attn_waves (0|4|8; 0 = auto: 8, or 4 when the
+ * 8-wave grid has fewer blocks than CUs), attn_tk (64|128), attn_prio (0|1), vit_attn_vec (0|1),
+ * out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1), gemm_persist (0|1), gemm_pp128 (0|1),
+ * gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1), gemm_rinit (0|1), tn_skinny_lds (0|1),
+ * train_dkv_dma (0|1), xknob (0..15, read by no shipped dispatch).
  * Returns MHADA_ERR_ARG for an unknown knob or an out-of-range value.  No reference
  * counterpart (the reference has no kernels). */
 int mhada_set_tuning(const char* name, int value);
 int mhada_get_tuning(const char* name, int* value);
+
+/* Sustained shader-clock probe (ABI 13; probe.hip): nblk workgroups of 4 waves each run a dependent
+ * v_mfma_f32_16x16x32_bf16 chain of 4 * iters MFMAs per wave on non-trivial operands; workgroup b
+ * writes stamps[2b] = shader-clock ticks (s_memtime) and stamps[2b + 1] = 100 MHz ticks
+ * (s_memrealtime) spent in the chain (device buffer of 2 * nblk).  clock = stamps[2b] /
+ * stamps[2b + 1] * 100 MHz.  bench.py runs it after each timed region so a box's clock under dense
+ * MFMA load is reported beside its throughput.  No reference counterpart (infer_time.py:64-87 is
+ * the reference's only timer). */
+int mhada_clock_probe(unsigned long long* stamps, int nblk, int iters, mhada_stream_t stream);
 
 /*
  * Batched NT GEMM with fused epilogue:

@@ -39,11 +39,8 @@ const Knob kKnobs[] = {
     {"gemm_persist", &Tuning::gemm_persist},         {"gemm_pp128", &Tuning::gemm_pp128},
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
     {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
-    {"attn_sched", &Tuning::attn_sched},             {"tn_skinny_lds", &Tuning::tn_skinny_lds},
-    {"train_dkv_dma", &Tuning::train_dkv_dma},     {"wino_l2pf", &Tuning::wino_l2pf},
-    {"wino_ws", &Tuning::wino_ws},                 {"xknob", &Tuning::xknob},
-    {"gemm_f32b", &Tuning::gemm_f32b},             {"gemm_n64_pp", &Tuning::gemm_n64_pp},
-    {"gemm_n64_cen", &Tuning::gemm_n64_cen},
+    {"tn_skinny_lds", &Tuning::tn_skinny_lds},       {"train_dkv_dma", &Tuning::train_dkv_dma},
+    {"xknob", &Tuning::xknob},
 };
 
 Tuning g_tuning;
@@ -60,13 +57,10 @@ void read_env_once() {
 }
 
 bool valid(const char* name, int v) {
-  if (!strcmp(name, "attn_waves")) return v == 4 || v == 8;
+  if (!strcmp(name, "attn_waves")) return v == 0 || v == 4 || v == 8;
   if (!strcmp(name, "attn_tk")) return v == 64 || v == 128;
   if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
-  if (!strcmp(name, "attn_sched")) return v == 0 || (v >= 3 && v <= 8);
   if (!strcmp(name, "xknob")) return v >= 0 && v < 16;
-  if (!strcmp(name, "wino_ws")) return v >= 0 && v <= 2;
-  if (!strcmp(name, "gemm_f32b")) return v >= 0 && v <= 3;
   return v == 0 || v == 1;
 }
 }  // namespace
@@ -78,7 +72,7 @@ const Tuning& tuning() {
 
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 12; }  // 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
+extern "C" int mhada_abi_version(void) { return 13; }  // 13: mhada_clock_probe, knobs of removed variants dropped (attn_sched, wino_ws, wino_l2pf, gemm_f32b, gemm_n64_pp, gemm_n64_cen), attn_waves 0 = auto; 12: mhada_feat_stats; 10-12 also added a trailing relu_mask / relu argument to mhada_conv3x3_wino, mhada_reflect_fold and mhada_feat_loss_bwd and mhada_gemm relu = 2; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }
 

@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) attn_bf16_kernel(con
 // (attn_exact_half).  Branch-free clamped tile loads (keys past Ns re-read valid rows and are
 // masked in the last tile).
 // --------------------------------------------------------------------------------------
-template <int NW, int TK, bool EARLY = false>
+template <int NW, int TK>
 __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p) {
   constexpr int NT = 64 * NW, NKB = TK / 32;
   constexpr int LK = 72, LV = TK + 8;  // padded rows: conflict-free 16-B reads
@@ -648,9 +648,6 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
   for (int t = 1; t < NFULL; ++t) {
     const int cb = t & 1;
     issue(min(t + 1, NTILE - 1) * TK);
-    // EARLY: keep the next tile's global loads at the top of the iteration (hipcc otherwise sinks
-    // them next to their LDS writes, exposing the load latency right before the barrier)
-    if constexpr (EARLY) __builtin_amdgcn_sched_barrier(0);
     f32x16 S[NKB];
     qk(sK[cb], S, Cm);
     finish(sV[cb], S);
@@ -670,326 +667,21 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 }
 
 // --------------------------------------------------------------------------------------
-// Fixed-shift kernel with LDS-DMA staging (tuning attn_sched = 3; the bf16 softmax default of round
-// 3, 4.5 % faster than register staging at 1024^2 B4; round 4's default is its 16x16x32 form fsq1): attn_bf16_fs_kernel's loop with
-// the K / V'^T tiles staged by global_load_lds (16 B per lane) instead of through registers: no
-// staging registers, no LDS write pass, the next tile's DMA in flight for the whole iteration
-// (hipcc sinks the register-staged kernel's global loads next to their LDS writes).  LDS images
-// are lane-linear per wave-instruction and XOR-swizzled on the SOURCE address (rule 21): K rows
-// (128 B, two per 256-B bank row) keep 16-B chunk c at slot c ^ ((row >> 1) & 7) — the rows of
-// a ds_read_b128 lane group then land on 16 distinct slots (c ^ (row & 7) left them 2-way
-// conflicted: PMC SQ_LDS_BANK_CONFLICT 1.3e8 cycles per launch); V'^T rows (256 B) at slot
-// c ^ (row & 15); the fragment reads apply the same XOR (conflict-free ds_read_b128).  2-slot ring, retired with
-// vmcnt(0) before the one barrier per tile.  Whole key tiles only.  (A second score set for
-// cross-tile pipelining at 128 keys spilled; attn_bf16_fsh_kernel pipelines by half tiles.)
+// LDS-DMA (global_load_lds, 16 B per lane) for the fixed-shift kernel's K / V'^T ring below.
 // --------------------------------------------------------------------------------------
 MHADA_DEV void attn_glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsg_kernel(const AttnP p) {
-  constexpr int TK = 128, NKB = 4, NSL = 2;
-  constexpr int KSZ = TK * 64, VSZ = 128 * TK;  // bf16 elements per slot: K [128][64], V'^T [128][128]
-  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;  // 1-KiB pieces per wave
-  static_assert(KPW >= 1 && VPW >= 1, "tile config");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 96 KiB, the only LDS object
-  int b, hh, qb;
-  decode_block(p, b, hh, qb);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, r32 = lane & 31;
-  const int q = qb * (32 * NW) + wave * 32 + r32;
-  const long long bh = (long long)b * p.H + hh;
-  const int Ns = p.Ns;
-  const f32x16 zero = {};
-
-  bf16x8 qf[4];
-  {
-    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
-      if (q >= p.Nc) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
-      }
-    }
-  }
-  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
-  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
-  // per-lane source offsets (elements) of this wave's pieces, relative to the tile's first key
-  int ksrc[KPW], vsrc[VPW];
-#pragma unroll
-  for (int i = 0; i < KPW; ++i) {
-    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = row * 128 + 8 * (slot ^ ((row >> 1) & 7));
-  }
-#pragma unroll
-  for (int i = 0; i < VPW; ++i) {
-    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
-    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
-  }
-  auto stage = [&](int key0, int sl) {
-    bf16* kd = smem + sl * (KSZ + VSZ);
-    bf16* vd = kd + KSZ;
-    const bf16* ks = kvb + (long long)key0 * 128;
-    const bf16* vs = vtb + key0;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
-#pragma unroll
-    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
-  };
-  auto qk = [&](int sl, f32x16 (&S)[NKB], const f32x16& init) {
-    const bf16* ck = smem + sl * (KSZ + VSZ);
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-      const bf16* krow = ck + (kb * 32 + r32) * 64;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ ((r32 >> 1) & 7)));
-        S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[kb], 0, 0, 0);
-      }
-    }
-  };
-  f32x16 O[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) O[i] = zero;
-  float l = 0.f;
-  auto finish = [&](int sl, const f32x16 (&S)[NKB]) {
-    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
-    float part[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float e = fast_exp2(S[kb][8 * s + j]);
-          part[j & 3] += e;
-          pf[j] = (bf16)e;
-        }
-        const int ch = (4 * kb + 2 * s + h) ^ (r32 & 15);
-#pragma unroll
-        for (int blk = 0; blk < 4; ++blk) {
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (blk * 32 + r32) * TK + 8 * ch);
-          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
-        }
-      }
-    }
-    l += (part[0] + part[1]) + (part[2] + part[3]);
-  };
-
-  const int NTILE = Ns / TK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  f32x16 Sa[NKB], Cm;
-  {  // tile 0: unshifted scores, m2 = their max, then shift
-    qk(0, Sa, zero);
-    const float m2 = tile_max_log2<NKB>(Sa);
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) Sa[kb][r] -= m2;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Cm[r] = -m2;
-  }
-  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  ATTN_STAMP(0);
-  {
-    // tile t+1's LDS-DMA into the other slot (last read in iteration t-1, before its barrier)
-    // flies during tile t's MFMAs; retired at the end of the iteration
-    if (NTILE > 1) stage(TK, 1);
-    finish(0, Sa);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int t = 1; t < NTILE; ++t) {
-      if (t + 1 < NTILE) stage((t + 1) * TK, (t + 1) & 1);
-      qk(t & 1, Sa, Cm);
-      finish(t & 1, Sa);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  ATTN_STAMP(1);
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
-  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
-}
-
 // --------------------------------------------------------------------------------------
-// Half-tile pipelined fixed-shift kernel (tuning attn_sched = 5; 1.2 % slower than the LDS-DMA kernel
-// once the K image's bank conflicts were fixed, kept as the measured alternative).  A 128-key tile's scores are
-// two halves, A (keys 0-63) and B (64-127), 32 registers each; iteration t runs
-//   step 1: QK^T of half B of tile t      beside  exp / row sum / pack / PV of half A of tile t
-//   step 2: QK^T of half A of tile t+1    beside  exp / row sum / pack / PV of half B of tile t
-// so every MFMA group has independent VALU next to it inside the wave, with the SAME 64 score
-// registers as the unpipelined kernel.  K / V'^T tiles arrive by LDS-DMA (attn_bf16_fsg_kernel's
-// swizzled images) into a 3-slot ring; the one barrier per tile sits between the two steps:
-// before it each wave retires tile t+1's pieces (vmcnt(0)), after it tile t+2 is issued into
-// the slot tile t-1 left (its last reads, step 2 of iteration t-1, precede the barrier).
-// Measured (before the K swizzle fix): +4.4 % over the register-staged kernel at 1024^2 B4; an explicit sched_group_barrier
-// interleave of each step (1 MFMA : 1 LDS read : 1-2 exp : 2 VALU) measured 5.8 % SLOWER, and the
-// static priority of the younger wave half makes no difference here (both kept out / as is).
-// --------------------------------------------------------------------------------------
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p) {
-  constexpr int TK = 128, NSL = 3;
-  constexpr int KSZ = TK * 64, VSZ = 128 * TK;
-  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;
-  static_assert(KPW >= 1 && VPW >= 1, "tile config");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 144 KiB, the only LDS object
-  int b, hh, qb;
-  decode_block(p, b, hh, qb);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, r32 = lane & 31;
-  const int q = qb * (32 * NW) + wave * 32 + r32;
-  const long long bh = (long long)b * p.H + hh;
-  const int Ns = p.Ns;
-  const f32x16 zero = {};
-
-  bf16x8 qf[4];
-  {
-    const bf16* qp = reinterpret_cast<const bf16*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * h;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
-      if (q >= p.Nc) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qf[s][e] = (bf16)0.0f;
-      }
-    }
-  }
-  const bf16* kvb = reinterpret_cast<const bf16*>(p.kv) + bh * (long long)Ns * 128;
-  const bf16* vtb = reinterpret_cast<const bf16*>(p.vt) + bh * 128 * (long long)p.ldt;
-  int ksrc[KPW], vsrc[VPW];
-#pragma unroll
-  for (int i = 0; i < KPW; ++i) {
-    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = row * 128 + 8 * (slot ^ ((row >> 1) & 7));
-  }
-#pragma unroll
-  for (int i = 0; i < VPW; ++i) {
-    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
-    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
-  }
-  auto stage = [&](int key0, int sl) {
-    bf16* kd = smem + sl * (KSZ + VSZ);
-    bf16* vd = kd + KSZ;
-    const bf16* ks = kvb + (long long)key0 * 128;
-    const bf16* vs = vtb + key0;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
-#pragma unroll
-    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
-  };
-  // half hf (0: keys 0-63 = key blocks 0,1; 1: keys 64-127 = key blocks 2,3) of a tile
-  auto qk = [&](int sl, int hf, f32x16 (&S)[2], const f32x16& init) {
-    const bf16* ck = smem + sl * (KSZ + VSZ);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bf16* krow = ck + ((2 * hf + j) * 32 + r32) * 64;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 8 * ((2 * s + h) ^ ((r32 >> 1) & 7)));
-        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? init : S[j], 0, 0, 0);
-      }
-    }
-  };
-  f32x16 O[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) O[i] = zero;
-  float l = 0.f;
-  auto finish = [&](int sl, int hf, const f32x16 (&S)[2]) {
-    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
-    float part[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kb = 2 * hf + j;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pf;
-#pragma unroll
-        for (int e8 = 0; e8 < 8; ++e8) {
-          const float e = fast_exp2(S[j][8 * s + e8]);
-          part[e8 & 3] += e;
-          pf[e8] = (bf16)e;
-        }
-        const int ch = (4 * kb + 2 * s + h) ^ (r32 & 15);
-#pragma unroll
-        for (int blk = 0; blk < 4; ++blk) {
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (blk * 32 + r32) * TK + 8 * ch);
-          O[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, O[blk], 0, 0, 0);
-        }
-      }
-    }
-    l += (part[0] + part[1]) + (part[2] + part[3]);
-  };
-
-  const int NTILE = Ns / TK;
-  stage(0, 0);
-  if (NTILE > 1) stage(TK, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (NTILE > 2) stage(2 * TK, 2);
-  f32x16 SA[2], SB[2], Cm;
-  {  // tile 0: unshifted scores of both halves, m2 = their max, then shift
-    qk(0, 0, SA, zero);
-    qk(0, 1, SB, zero);
-    float mx = SA[0][0];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(SA[j][r], SB[j][r]));
-    const float m2 = fmaxf(mx, __shfl_xor(mx, 32, 64));
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        SA[j][r] -= m2;
-        SB[j][r] -= m2;
-      }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Cm[r] = -m2;
-  }
-  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  // iteration 0: half B's scores are already there
-  finish(0, 0, SA);
-  if (NTILE > 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 2 (issued above) is tile t+2 here
-    __builtin_amdgcn_s_barrier();
-    qk(1, 0, SA, Cm);
-  }
-  finish(0, 1, SB);
-  int sl = 1;  // t % 3
-  for (int t = 1; t + 1 < NTILE; ++t) {
-    const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;
-    qk(sl, 1, SB, Cm);  // step 1
-    finish(sl, 0, SA);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (this wave's pieces)
-    __builtin_amdgcn_s_barrier();
-    if (t + 2 < NTILE) stage((t + 2) * TK, sl2);
-    qk(sl1, 0, SA, Cm);  // step 2
-    finish(sl, 1, SB);
-    sl = sl1;
-  }
-  if (NTILE > 1) {  // last tile
-    qk(sl, 1, SB, Cm);
-    finish(sl, 0, SA);
-    finish(sl, 1, SB);
-  }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (__any(!(lt <= kShiftSumThr))) attn_exact_half(p, kvb, vtb, qf, O, l, h, r32);
-  attn_epilogue<bf16>(p, O, l, b, hh, q, h);
-}
-
-// --------------------------------------------------------------------------------------
-// Fixed-shift LDS-DMA kernel on v_mfma_f32_16x16x32_bf16 ("fsq", tuning attn_sched = 6 / 7): the
-// fsg kernel's loop (same LDS-DMA ring, same fixed shift, same FLOPs and LDS bytes per FLOP) with
-// the 16 x 16 output shape, which the chip runs at a higher sustained clock under load than the
-// 32 x 32 shape at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).
+// Fixed-shift LDS-DMA kernel on v_mfma_f32_16x16x32_bf16 ("fsq1", the bf16 softmax default when
+// Ns % 128 == 0): the fixed shift of attn_bf16_fs_kernel with the K / V'^T tiles staged by
+// global_load_lds into a 2-slot ring (no staging registers, no LDS write pass, the next tile's DMA
+// in flight for the whole iteration), on the 16 x 16 output shape, which the chip runs at a higher
+// sustained clock under load than the 32 x 32 shape at equal cycles per FLOP (MI355X_MICROARCH.md,
+// DVFS give-back item 7).  LDS images are lane-linear per wave-instruction and XOR-swizzled on the
+// SOURCE address: V'^T rows (256 B) keep 16-B chunk c at slot c ^ (row & 15).
 // Orientation as before (swapped products, the query on the MFMA column):
 //   S^T (16 keys x 16 queries) = K (16 x 32 d) . Q^T (32 d x 16 queries): lane = query r16 of a
 //       16-query group qg, rows 4g..4g+3 (g = lane >> 4); a wave owns 32 queries = 2 groups, and
@@ -1001,16 +693,15 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsh_kernel(const AttnP p
 //       group g then holds exactly its 8 B slots (j < 4 from t = 0, j >= 4 from t = 1) — the
 //       permutation costs only the K row address, no lane movement, no second vt layout.
 // K image: chunk c of key row k at 16-B slot c ^ (k & 7) (conflict-free for these row sets
-// under the ds_read_b128 lane groups of MI355X_MICROARCH.md's LDS table); V'^T as in fsg.
-// Measured (tools/attn_clock.py, profiles/r04_attn_clock.log, 1024^2 B4): the 32x32x16 kernel (fsg)
-// holds 1.78-1.83 GHz at 0.62-0.63 of the clock-adjusted peak; this shape holds 2.15-2.19 GHz at
-// 0.54-0.55 (the 16-cycle MFMA blocks vector issue for 8 of its 16 cycles, so the softmax VALU
-// competes harder); net fsq 3 %, fsq1 4-6 % faster than fsg.
-// ONES (attn_sched = 7, the bf16 softmax default when Ns % 128 == 0): the row sum l comes out of
-// one extra MFMA per (32 keys, 16 queries)
-// with an all-ones A operand (D rows = sum_k P[k][q]), removing the 64 v_add_f32 per tile and
-// lane from the VALU stream at +8 MFMAs (72 instead of 64 PV MFMAs per tile and wave); l is then
-// the sum of the bf16-rounded P that the PV products use.
+// under the ds_read_b128 lane groups of MI355X_MICROARCH.md's LDS table).
+// Measured in round 4 (tools/attn_clock.py, profiles/r04_attn_clock.log, 1024^2 B4): the 32x32x16
+// form of this loop (removed in round 5) held 1.78-1.83 GHz at 0.62-0.63 of the clock-adjusted
+// peak; this shape holds 2.15-2.19 GHz at 0.54-0.55 (the 16-cycle MFMA blocks vector issue for 8
+// of its 16 cycles, so the softmax VALU competes harder); net 4-6 % faster.
+// The row sum l comes out of one extra MFMA per (32 keys, 16 queries) with an all-ones A operand
+// (D rows = sum_k P[k][q]), removing the 64 v_add_f32 per tile and lane from the VALU stream at
+// +8 MFMAs (72 instead of 64 PV MFMAs per tile and wave); l is then the sum of the bf16-rounded P
+// that the PV products use.
 // --------------------------------------------------------------------------------------
 MHADA_DEV int fsq_key(int r, int t) { return 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3) + 8 * t; }
 
@@ -1119,7 +810,7 @@ MHADA_DEV void attn_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], const flo
   }
 }
 
-template <int NW, bool ONES>
+template <int NW>
 __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p) {
   constexpr int TK = 128, NSL = 2;
   constexpr int KSZ = TK * 64, VSZ = 128 * TK;  // bf16 elements per slot: K [128][64], V'^T [128][128]
@@ -1195,14 +886,11 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p
       }
   };
   f32x4 O[2][8], L[2];
-  float part[2][4];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     L[qg] = z4;
 #pragma unroll
     for (int i = 0; i < 8; ++i) O[qg][i] = z4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) part[qg][j] = 0.f;
   }
   bf16x8 ones;
 #pragma unroll
@@ -1216,14 +904,10 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p
       for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float e = fast_exp2(S[qg][kg][j >> 2][j & 3]);
-          if constexpr (!ONES) part[qg][j & 3] += e;
-          pf[qg][j] = (bf16)e;
+          pf[qg][j] = (bf16)fast_exp2(S[qg][kg][j >> 2][j & 3]);
         }
-      if constexpr (ONES) {
 #pragma unroll
-        for (int qg = 0; qg < 2; ++qg) L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qg], L[qg], 0, 0, 0);
-      }
+      for (int qg = 0; qg < 2; ++qg) L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qg], L[qg], 0, 0, 0);
       const int ch = (4 * kg + g) ^ r16;  // row 16 dvb + r16: row & 15 == r16
 #pragma unroll
       for (int dvb = 0; dvb < 8; ++dvb) {
@@ -1278,225 +962,17 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsq_kernel(const AttnP p
   ATTN_STAMP(1);
   float lt[2];
 #pragma unroll
-  for (int qg = 0; qg < 2; ++qg) {
-    if constexpr (ONES) {
-      lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
-    } else {
-      float l = (part[qg][0] + part[qg][1]) + (part[qg][2] + part[qg][3]);
-      l += __shfl_xor(l, 16, 64);
-      lt[qg] = l + __shfl_xor(l, 32, 64);
-    }
-  }
+  for (int qg = 0; qg < 2; ++qg) lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
   if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q(p, kvb, vtb, qf, O, lt, g, r16);
   attn_epilogue_q<bf16>(p, O, lt, b, hh, q0, g, r16);
 }
 
-// --------------------------------------------------------------------------------------
-// Persistent form of the fsq kernel with the all-ones row sum ("fsp", tuning attn_sched = 8):
-// (Measured SLOWER than fsq1: 2.95 vs 2.65 ms at 1024^2 B4 although it holds 2.36 GHz — its
-// loop compiles to 403 instead of 317 instructions (45 waits, 26 register moves for the
-// cur / next block state); kept as an A/B variant.)
-// one workgroup per CU walks the (b, h, query-block) blocks w, w + G, w + 2G, ... (the hardware
-// block ids a one-shot launch would use, so xcd_remap keeps the 32 workgroups of an XCD on 32
-// query blocks of one (b, h): K / V' shared in its L2), and the K / V'^T tile stream is continuous
-// across blocks: the 2-slot ring's next-tile DMA in the last tile of a block already fetches the
-// NEXT block's tile 0, and that block's Q rows are loaded in the same iteration, so a block
-// starts with its operands resident instead of paying the HBM latency of its prologue (the
-// one-shot kernel spends ~5 % of its time outside the key loop, tools/attn_clock.py).
-// --------------------------------------------------------------------------------------
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fsp_kernel(const AttnP p) {
-  constexpr int TK = 128, NSL = 2;
-  constexpr int KSZ = TK * 64, VSZ = 128 * TK;
-  constexpr int KPW = TK * 128 / 1024 / NW, VPW = 128 * TK * 2 / 1024 / NW;
-  static_assert(KPW >= 1 && VPW >= 1, "tile config");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NSL * (KSZ + VSZ)];  // 96 KiB
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
-  const int Ns = p.Ns, NTILE = Ns / TK, G = gridDim.x;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-
-  struct Blk {
-    int b, hh, q0;
-    const bf16* kvb;
-    const bf16* vtb;
-  };
-  auto decode = [&](int hw, Blk& k) {
-    const int t = xcd_remap(hw, p.nblk);
-    const int qb = t % p.nqb, bh = t / p.nqb;
-    k.b = bh / p.H;
-    k.hh = bh - k.b * p.H;
-    k.q0 = qb * (32 * NW) + wave * 32;
-    k.kvb = reinterpret_cast<const bf16*>(p.kv) + (long long)bh * Ns * 128;
-    k.vtb = reinterpret_cast<const bf16*>(p.vt) + (long long)bh * 128 * p.ldt;
-  };
-  auto load_q = [&](const Blk& k, bf16x8 (&qf)[2][2]) {
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg) {
-      const int q = k.q0 + 16 * qg + r16;
-      const bf16* qp = reinterpret_cast<const bf16*>(p.q) +
-                       (((long long)k.b * p.H + k.hh) * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * g;
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) qf[qg][dh] = *reinterpret_cast<const bf16x8*>(qp + 32 * dh);
-    }
-  };
-  auto mask_q = [&](const Blk& k, bf16x8 (&qf)[2][2]) {
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg)
-      if (k.q0 + 16 * qg + r16 >= p.Nc) {
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) qf[qg][dh][e] = (bf16)0.0f;
-      }
-  };
-  int ksrc[KPW], vsrc[VPW];
-#pragma unroll
-  for (int i = 0; i < KPW; ++i) {
-    const int row = 8 * (KPW * wave + i) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = row * 128 + 8 * (slot ^ (row & 7));
-  }
-#pragma unroll
-  for (int i = 0; i < VPW; ++i) {
-    const int row = 4 * (VPW * wave + i) + (lane >> 4), slot = lane & 15;
-    vsrc[i] = row * p.ldt + 8 * (slot ^ (row & 15));
-  }
-  auto stage = [&](const Blk& k, int key0, int sl) {
-    bf16* kd = smem + sl * (KSZ + VSZ);
-    bf16* vd = kd + KSZ;
-    const bf16* ks = k.kvb + (long long)key0 * 128;
-    const bf16* vs = k.vtb + key0;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (KPW * wave + i));
-#pragma unroll
-    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (VPW * wave + i));
-  };
-  int krow[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) krow[t] = fsq_key(r16, t) * 64;
-  bf16x8 qf[2][2], qn[2][2];
-  auto qk = [&](int sl, f32x4 (&S)[2][4][2], const f32x4 (&init)[2]) {
-    const bf16* ck = smem + sl * (KSZ + VSZ);
-#pragma unroll
-    for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const bf16* kr = ck + kg * 32 * 64 + krow[t];
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + 8 * ((4 * dh + g) ^ (r16 & 7)));
-#pragma unroll
-          for (int qg = 0; qg < 2; ++qg)
-            S[qg][kg][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][dh], dh == 0 ? init[qg] : S[qg][kg][t],
-                                                                   0, 0, 0);
-        }
-      }
-  };
-  f32x4 O[2][8], L[2];
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  auto finish = [&](int sl, const f32x4 (&S)[2][4][2]) {
-    const bf16* cv = smem + sl * (KSZ + VSZ) + KSZ;
-#pragma unroll
-    for (int kg = 0; kg < 4; ++kg) {
-      bf16x8 pf[2];
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[qg][j] = (bf16)fast_exp2(S[qg][kg][j >> 2][j & 3]);
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qg], L[qg], 0, 0, 0);
-      const int ch = (4 * kg + g) ^ r16;
-#pragma unroll
-      for (int dvb = 0; dvb < 8; ++dvb) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cv + (16 * dvb + r16) * TK + 8 * ch);
-#pragma unroll
-        for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg], O[qg][dvb], 0, 0, 0);
-      }
-    }
-  };
-
-  int hw = blockIdx.x;
-  if (hw >= p.nblk) return;
-  Blk cur, nxt;
-  decode(hw, cur);
-  load_q(cur, qf);
-  int sl = 0;
-  stage(cur, 0, sl);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  while (true) {
-    const bool more = hw + G < p.nblk;
-    if (more) decode(hw + G, nxt);
-    mask_q(cur, qf);
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg) {
-      L[qg] = z4;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) O[qg][i] = z4;
-    }
-    ATTN_STAMP(0);
-    f32x4 Sa[2][4][2], Cm[2];
-    {  // tile 0: unshifted scores, m2 = their max, then shift
-      const f32x4 zi[2] = {z4, z4};
-      qk(sl, Sa, zi);
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) {
-        float m = -INFINITY;
-#pragma unroll
-        for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) m = fmaxf(m, Sa[qg][kg][t][j]);
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-#pragma unroll
-        for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Sa[qg][kg][t][j] -= m;
-        Cm[qg] = f32x4{-m, -m, -m, -m};
-      }
-    }
-    // tiles 0 .. NTILE-1: the DMA of the stream's next tile (this block's t+1, or the next block's
-    // tile 0 in the last iteration, with the next block's Q rows) flies during tile t
-    for (int t = 0; t < NTILE; ++t) {
-      if (t + 1 < NTILE) {
-        stage(cur, (t + 1) * TK, sl ^ 1);
-      } else if (more) {
-        stage(nxt, 0, sl ^ 1);
-        load_q(nxt, qn);
-      }
-      if (t > 0) qk(sl, Sa, Cm);
-      finish(sl, Sa);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      sl ^= 1;
-    }
-    ATTN_STAMP(1);
-    float lt[2];
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg) lt[qg] = L[qg][0];
-    if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q(p, cur.kvb, cur.vtb, qf, O, lt, g, r16);
-    attn_epilogue_q<bf16>(p, O, lt, cur.b, cur.hh, cur.q0, g, r16);
-    if (!more) break;
-    hw += G;
-    cur = nxt;
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg)
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) qf[qg][dh] = qn[qg][dh];
-  }
-}
-
-// Variant selection (Tuning, common.h): the fixed-shift kernel is the bf16 softmax default; the
-// online-max kernel serves the cosine activation and, through attn_fixed_shift = 0, tests / A-B.
+// Variant selection: the fixed-shift kernels are the bf16 softmax default (fsq1 when Ns % 128 == 0,
+// attn_bf16_fs_kernel for ragged Ns); the online-max kernel serves the cosine activation and, through
+// tuning attn_fixed_shift = 0, tests / A-B.  Round 5 removed the measured-slower fixed-shift variants
+// (the 32x32x16 LDS-DMA kernel, the half-tile pipelined and the persistent forms; their logs are
+// profiles/r03_attn_variants_ab*.log and profiles/r04_attn_variants_ab*.log).
 static bool attn_bf16_fixed_shift() { return tuning().attn_fixed_shift != 0; }
-static int attn_waves(int) { return tuning().attn_waves; }
 static int attn_tk() { return tuning().attn_tk; }
 
 static int attn_num_cus() {
@@ -1517,51 +993,25 @@ static void launch_attn(const AttnP& p, int dtype, int activation, hipStream_t s
       hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_SOFTMAX, NW>), grid, blk, 0, s, p);
     else
       hipLaunchKernelGGL((attn_f32_kernel<MHADA_ACT_COSINE, NW>), grid, blk, 0, s, p);
+    return;
+  }
+  if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift()) {
+    if (p.Ns % 128 == 0) {  // whole 128-key tiles: the LDS-DMA 16x16x32 kernel
+      hipLaunchKernelGGL((attn_bf16_fsq_kernel<NW>), grid, blk, 0, s, p);
+      return;
+    }
+    if constexpr (NW == 8) {  // ragged Ns: register-staged fixed shift (2 x 106 KiB at 4 waves does not fit)
+      hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 128>), grid, blk, 0, s, p);
+      return;
+    }
+  }
+  const bool t128 = NW == 8 && attn_tk() == 128;  // 2 x 106 KiB of LDS does not fit a CU
+  if (activation == MHADA_ACT_SOFTMAX) {
+    if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
+    else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, 64>), grid, blk, 0, s, p);
   } else {
-    if constexpr (NW == 4) {  // small grids (mhada_attn): the 16x16x32 fixed-shift kernel at 4 waves
-      if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift() && tuning().attn_sched == 7 &&
-          p.Ns % 128 == 0) {
-        hipLaunchKernelGGL((attn_bf16_fsq_kernel<4, true>), grid, blk, 0, s, p);
-        return;
-      }
-    }
-    if constexpr (NW == 8) {
-      if (activation == MHADA_ACT_SOFTMAX && attn_bf16_fixed_shift()) {
-        if (tuning().attn_sched == 3 && p.Ns % 128 == 0) {  // LDS-DMA staging, 128-key tiles
-          hipLaunchKernelGGL((attn_bf16_fsg_kernel<8>), grid, blk, 0, s, p);
-          return;
-        }
-        if (tuning().attn_sched == 8 && p.Ns % 128 == 0) {  // persistent 16x16x32, continuous tile stream
-          const dim3 pgrid((unsigned)std::min<long long>(p.nblk, attn_num_cus()));
-          hipLaunchKernelGGL((attn_bf16_fsp_kernel<8>), pgrid, blk, 0, s, p);
-          return;
-        }
-        if ((tuning().attn_sched == 6 || tuning().attn_sched == 7) && p.Ns % 128 == 0) {  // 16x16x32 MFMA
-          if (tuning().attn_sched == 7) hipLaunchKernelGGL((attn_bf16_fsq_kernel<8, true>), grid, blk, 0, s, p);
-          else hipLaunchKernelGGL((attn_bf16_fsq_kernel<8, false>), grid, blk, 0, s, p);
-          return;
-        }
-        if (tuning().attn_sched == 5 && p.Ns % 128 == 0) {  // half-tile pipelined, LDS-DMA staging
-          hipLaunchKernelGGL((attn_bf16_fsh_kernel<8>), grid, blk, 0, s, p);
-          return;
-        }
-        if (tuning().attn_sched == 4 && attn_tk() == 128) {  // register staging, loads kept early
-          hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 128, true>), grid, blk, 0, s, p);
-          return;
-        }
-        if (attn_tk() == 128) hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 128>), grid, blk, 0, s, p);
-        else hipLaunchKernelGGL((attn_bf16_fs_kernel<8, 64>), grid, blk, 0, s, p);
-        return;
-      }
-    }
-    const bool t128 = NW == 8 && attn_tk() == 128;  // 2 x 106 KiB of LDS does not fit a CU
-    if (activation == MHADA_ACT_SOFTMAX) {
-      if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
-      else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_SOFTMAX, NW, 64>), grid, blk, 0, s, p);
-    } else {
-      if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
-      else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, 64>), grid, blk, 0, s, p);
-    }
+    if (t128) hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, (NW == 8 ? 128 : 64)>), grid, blk, 0, s, p);
+    else hipLaunchKernelGGL((attn_bf16_kernel<MHADA_ACT_COSINE, NW, 64>), grid, blk, 0, s, p);
   }
 }
 
@@ -1583,10 +1033,11 @@ extern "C" int mhada_attn(const void* q, const void* kv, const void* vt, const f
   p.prio = tuning().attn_prio;
   p.ldk = 128;
   p.ldt = (Ns + 63) / 64 * 64;
-  int nw = attn_waves(dtype);
-  // a grid of 8-wave blocks smaller than the CU count (B = 1 at 512^2: 128 blocks) leaves CUs idle:
-  // 4-wave blocks cover twice as many CUs (one wave per SIMD instead of two)
-  if (nw == 8 && (long long)B * H * ((Nc + 255) / 256) < attn_num_cus()) nw = 4;
+  // tuning attn_waves: 4 or 8 waves per block as set; 0 (default) = 8, except that a grid of 8-wave
+  // blocks smaller than the CU count (B = 1 at 512^2: 128 blocks) leaves CUs idle, so it runs 4-wave
+  // blocks there (one wave per SIMD instead of two, twice as many CUs covered)
+  int nw = tuning().attn_waves;
+  if (nw == 0) nw = (long long)B * H * ((Nc + 255) / 256) < attn_num_cus() ? 4 : 8;
   p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
   const long long nblk = (long long)B * H * p.nqb;
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn: grid too large");

@@ -29,7 +29,7 @@ int check_launch(const char* what);  // hipGetLastError -> MHADA_ERR_LAUNCH
 // through mhada_set_tuning() (include/mhada_hip.h) — never per launch from the environment.
 struct Tuning {
   int attn_fixed_shift = 1;  // bf16 softmax attention: fixed-shift kernel (0: online-max kernel)
-  int attn_waves = 8;        // attention waves per workgroup (4 | 8)
+  int attn_waves = 0;        // attention waves per workgroup: 4 | 8 as set; 0 = 8, or 4 when the 8-wave grid is smaller than the CU count
   int attn_tk = 128;         // bf16 attention keys per tile (64 | 128)
   int attn_prio = 1;         // fixed-shift kernel: s_setprio(1) for the younger wave half
   int vit_attn_vec = 1;      // bf16 batch-axis attention: vectorised form
@@ -42,16 +42,7 @@ struct Tuning {
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
-  int attn_sched = 7;        // bf16 fixed-shift attention (Ns % 128 == 0): 7 LDS-DMA staging on 16x16x32
-                             // MFMAs with the all-ones row sum (fsq1, round 4), 6 the same with VALU row
-                             // sums, 8 its persistent form, 3 LDS-DMA on 32x32x16 (fsg), 5 half-tile
-                             // pipelined + LDS-DMA, 4 register staging with early loads, 0 register staging
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
-  int wino_l2pf = 0;         // fp32 Winograd conv: L2 warm-up of the filter chunk two ahead (0: none; 1 measured 1.3 % slower)
-  int wino_ws = 0;           // fp32 Winograd conv: 0 wino_kernel; 1 warp-specialised (measured 7 % slower); 2 persistent 16x16x4 (see wino.hip)
-  int gemm_f32b = 0;         // fp32 GEMM (ROWS A, N > 128): 0 ping-pong (4 phases per K-tile), 1 one-barrier-per-K-tile kernel, 2 ping-pong with 2 phases, 3 ping-pong 256x128 tiles
-  int gemm_n64_pp = 0;       // bf16 3x3 conv, N <= 64: 256x128 persistent ping-pong (upper half idle) instead of the 128x64 tile kernel
-  int gemm_n64_cen = 0;      // fp32 N <= 64 GEMM with centred A (MHAda q projection): LDS-DMA ring kernel with the centring on the fragments
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };

@@ -896,13 +896,8 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmP p) {
 // Needs two K-tiles (K >= 128 bf16 / 64 fp32: the A lookahead never skips a whole tile).
 // fp32 form: same 128-B rows (BK = 32), v_mfma_f32_32x32x2_f32, 32 MFMAs per phase.
 // ------------------------------------------------------------------------------------
-template <typename TC, typename TO, int AMODE, int BN, bool P2 = false>
+template <typename TC, typename TO, int AMODE, int BN>
 __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total) {
-  // P2 (fp32, BN = 256; tuning gemm_f32b = 2): two phases per K-tile of 64 MFMAs (both column
-  // blocks of one k-pair) instead of four of 32 — half the hand-overs of the MFMA pipe; A and
-  // W of K-tile g+1 are staged together in phase 0 of K-tile g (into the slot of g-1, which both
-  // groups have left) and waited for in phase 1.
-  static_assert(!P2 || (sizeof(TC) == 4 && BN == 256), "P2: fp32 256-column form only");
   // 128-B operand rows: BK = 64 bf16 or 32 fp32; CE elements per 16-B chunk, PE per 1-KiB piece.
   // BN = 256: each wave owns 128 rows x 64 columns (TN = 2 column blocks, 4 phases per K-tile);
   // BN = 128 (N <= 128 layers): 128 rows x 32 columns (TN = 1, 2 phases), one W half per stage;
@@ -1082,12 +1077,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   zero_acc(cur);
   stage_a(cur, 0, 0, 0); stage_a(cur, 1, 0, 0); stage_w(cur, 0, 0, 0);
   if constexpr (NWH == 2) stage_w(cur, 1, 0, 0);
-  if constexpr (P2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  }
+  stage_a(cur, 0, 1, 1); stage_a(cur, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   PP_BARRIER();
   if (grp == 1) PP_BARRIER();  // group 1 runs one barrier behind
 
@@ -1103,22 +1094,6 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   auto ktile = [&](const St& s1, const int k1, const bool w1, const St& s2, const int k2, const bool a2,
                    const bool wx) __attribute__((always_inline)) {
     const int cb = sl0;
-    if constexpr (P2) {
-      // phase 0: k-pair 0, both column blocks; stage K-tile g+1 (A and W) into the free slot
-      read_a(0, cb); read_w(0, 0, cb); read_w(1, 0, cb);
-      if (w1) {
-        stage_a(s1, 0, k1, sl1); stage_a(s1, 1, k1, sl1);
-        stage_w(s1, 0, k1, sl1); stage_w(s1, 1, k1, sl1);
-      }
-      PP_LGKM0(); PP_BARRIER(); compute(0); compute(1); PP_BARRIER();
-      // phase 1: k-pair 1; this wave's DMA of K-tile g+1 has landed before the barrier
-      read_a(1, cb); read_w(0, 1, cb); read_w(1, 1, cb);
-      if (wx) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(EPI_MIN) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      PP_LGKM0(); PP_BARRIER(); compute(0); compute(1); PP_BARRIER();
-      sl0 ^= 1; sl1 ^= 1; sl2 ^= 1;
-      return;
-    }
     if constexpr (TN == 2) {
       // phase 0
       read_a(0, cb); read_w(0, 0, cb);
@@ -1181,9 +1156,6 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     // K-tile raised register spills and measured slower)
     pre = AMODE == MHADA_A_ROWS && has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
     if (pre) {
-      if constexpr (P2) {
-        stage_a(nxt, 0, 1, sl1); stage_a(nxt, 1, 1, sl1);
-      }
       stage_w(nxt, 0, 1, sl1);
       if constexpr (NWH == 2) stage_w(nxt, 1, 1, sl1);
     }
@@ -1213,210 +1185,6 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 }
 
 // ------------------------------------------------------------------------------------
-// fp32 persistent GEMM, ONE barrier per 16-deep K-tile, 4-slot ring (round 4; tuning
-// gemm_f32b, ROWS A only).  The ping-pong kernel hands the MFMA pipe from one wave group to
-// the other 8 times per 32-deep K-tile and its 2-slot ring (3 x 64 KiB does not fit beside the
-// epilogue scratch) gives a K-tile's DMA 3-5 phases to land.  Here all 8 waves run the same
-// schedule over 16-deep K-tiles (64-B rows: A 256 x 16 | W 256 x 16 = 32 KiB per slot, 4 slots);
-// per K-tile j (slot j & 3):
-//   1. ds_read the k-quarter-1 fragments of K-tile j, 32 MFMAs on quarter 0 (read earlier)
-//   2. wait for this wave's DMA of K-tile j+1 (issued 3 K-tiles ago), lgkmcnt(0), barrier:
-//      every wave is done with slot j & 3 and K-tile j+1 is visible
-//   3. 8 MFMAs on quarter 1, the DMA of K-tile j+4 into slot j & 3 and the quarter-0 fragments
-//      of K-tile j+1, the other 24 MFMAs
-// The fragment reads are inline asm with counted waits whose "+v" operands tie each quarter's
-// registers to the wait before its MFMAs (hipcc's own wait insertion emitted lgkmcnt(0) there:
-// it cannot count across the loop back-edge).  The K-tile stream continues across this
-// workgroup's tiles.  Wave (grp, wc) owns rows grp*128 .. +127 and columns wc*64 .. +63 of the
-// 256x256 tile (4 x 2 blocks of v_mfma_f32_32x32x2_f32).  Row layout: 16-B chunk c of row r
-// sits at slot c ^ ((r >> 2) & 3), which spreads each 16-lane group of a ds_read_b128 (16 rows,
-// one logical chunk) over all 64 banks.
-// ------------------------------------------------------------------------------------
-template <typename TO>
-__global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total) {
-  constexpr int BK = 16, PE = 256, HALF = 256 * BK, SLOT = 2 * HALF, NS = 4, SCR = 8 * 1024;
-  __shared__ __attribute__((aligned(16))) float smem[NS * SLOT + SCR];  // 128 KiB ring + 32 KiB epilogue scratch
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2, wc = wave & 3;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int G = gridDim.x;
-  const float* A = reinterpret_cast<const float*>(p.a);
-  const float* W = reinterpret_cast<const float*>(p.w);
-
-  // staging: one 1-KiB DMA = 16 rows x 64 B; lane L -> row 16i + (L >> 2) of the wave's 32-row
-  // band, physical chunk L & 3, logical chunk (L & 3) ^ (L >> 4)
-  const int cofs = 4 * ((lane & 3) ^ (lane >> 4));
-  struct Tile { int m0, n0, z1, z2; };
-  auto setup = [&](int w) {
-    const int lg = xcd_remap(w, total);
-    const int z = lg / p.ntiles, t = lg - z * p.ntiles;
-    const int tm = t / p.tiles_n;
-    Tile s;
-    s.z1 = z / p.nb2;
-    s.z2 = z - s.z1 * p.nb2;
-    s.m0 = tm * 256;
-    s.n0 = (t - tm * p.tiles_n) * 256;
-    return s;
-  };
-  auto stage = [&](const Tile& s, int kt, int slot) {
-    const float* ab = A + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
-    const float* wb = W + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
-    float* dst = smem + slot * SLOT + wave * 2 * PE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int rr = 32 * wave + 16 * i + (lane >> 2);
-      const int m = min(s.m0 + rr, p.M - 1), n = min(s.n0 + rr, p.N - 1);
-      glds16(ab + (unsigned)(m * p.lda + cofs), dst + PE * i);
-      glds16(wb + (unsigned)(n * p.ldw + cofs), dst + HALF + PE * i);
-    }
-  };
-
-  // fragments: lane half h supplies k = 8h + 4c + e at MFMA step e of k-quarter c (logical
-  // chunk 2h + c of its row); one quarter = 4 A + 2 W chunks
-  const int swz = (r32 >> 2) & 3;
-  int koff[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) koff[c] = 4 * ((2 * h + c) ^ swz);
-  const unsigned lA = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(smem + (grp * 128 + r32) * BK);
-  const unsigned lW = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(smem + HALF + (wc * 64 + r32) * BK);
-  struct Frags { f32x4 a[4], w[2]; };
-  Frags fx, fy;
-  auto read = [&](int c, int slot, Frags& f) {
-    const unsigned o = (unsigned)(slot * SLOT + koff[c]) * 4u;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-      asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[mt]) : "v"(lA + o + mt * 32 * BK * 4));
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      asm volatile("ds_read_b128 %0, %1" : "=v"(f.w[nt]) : "v"(lW + o + nt * 32 * BK * 4));
-  };
-  // wait until at most N LDS reads are outstanding; f's registers are defined by this wait
-  auto wait_frags = [&](Frags& f, auto n) {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(%6)"
-                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.w[0]), "+v"(f.w[1])
-                 : "i"(decltype(n)::value));
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using N6 = std::integral_constant<int, 6>;
-  using N0 = std::integral_constant<int, 0>;
-  f32x16 acc[4][2];
-  // MFMA steps e0 .. e1-1 of one k-quarter (8 independent accumulators per step)
-  auto compute = [&](const Frags& f, int e0, int e1) {
-#pragma unroll
-    for (int e = e0; e < e1; ++e)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w[nt][e], f.a[mt][e], acc[mt][nt], 0, 0, 0);
-  };
-  // accumulator init: zero, or (p.rinit) the tile's residual rows + bias (as gemm_ppp_kernel)
-  auto init_acc = [&](const Tile& s) {
-    if constexpr (sizeof(TO) == 4) {
-      if (p.rinit) {
-        const float* rb = reinterpret_cast<const float*>(p.r) + s.z1 * p.sr1 + s.z2 * p.sr2;
-        const float* bb = p.bias ? p.bias + s.z1 * p.sb1 + s.z2 * p.sb2 : nullptr;
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n = s.n0 + wc * 64 + nt * 32 + 8 * g + 4 * h;
-            const bool nok = n + 3 < p.N;
-            const f32x4 b4 = (bb && nok) ? *reinterpret_cast<const f32x4*>(bb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-              const int m = s.m0 + grp * 128 + mt * 32 + r32;
-              f32x4 r4 = {0.f, 0.f, 0.f, 0.f};
-              if (nok && m < p.M) r4 = *reinterpret_cast<const f32x4*>(rb + (long long)m * p.ldr + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[mt][nt][4 * g + e] = r4[e] + b4[e];
-            }
-          }
-        return;
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  };
-  GemmP pe = p;
-  if (p.rinit) {
-    pe.r = nullptr;
-    pe.bias = nullptr;
-  }
-
-  const int KT = p.K / BK;  // >= 4 (K >= 64, checked on the host)
-  int sl = 0;               // ring slot of the current K-tile
-  // One K-tile (fx holds its quarter-0 fragments on entry).  (s2, k2, a2): the K-tile four ahead,
-  // staged into this K-tile's slot; more: a next K-tile exists (block-uniform); nw: LDS-DMA /
-  // store operations issued after this wave's DMA of the next K-tile (the wait leaves them in
-  // flight): 4 per staged K-tile among the two before this one, + 32 epilogue stores when the
-  // previous tile (full) ended within the last three K-tiles
-  auto ktile = [&](const Tile& s2, int k2, bool a2, bool more, int nw) __attribute__((always_inline)) {
-    read(1, sl, fy);
-    wait_frags(fx, N6{});
-    compute(fx, 0, 4);
-    __builtin_amdgcn_sched_barrier(0);
-    if (more) {
-      switch (nw) {  // s_waitcnt takes an immediate
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-        case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-        case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-      }
-    }
-    wait_frags(fy, N0{});
-    if (more) PP_BARRIER();
-    compute(fy, 0, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (a2) stage(s2, k2, sl);
-    sl = (sl + 1) & (NS - 1);
-    if (more) read(0, sl, fx);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(fy, 1, 4);
-  };
-
-  int w = blockIdx.x;
-  Tile cur = setup(w), nxt = cur;
-  bool has_nxt = w + G < total;
-  if (has_nxt) nxt = setup(w + G);
-  init_acc(cur);
-#pragma unroll
-  for (int k = 0; k < NS; ++k) stage(cur, k, k);
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  PP_BARRIER();
-  read(0, 0, fx);
-  bool pre = false;  // the previous tile was full: its 32 epilogue stores per wave are in the count
-  while (true) {
-    const int e = pre ? 32 : 0;
-    for (int kt = 0; kt + 4 < KT; ++kt) ktile(cur, kt + 4, true, true, 8 + (kt < 3 ? e : 0));
-    const int hn = has_nxt ? 4 : 0;
-    ktile(nxt, 0, has_nxt, true, 8 + (KT - 4 < 3 ? e : 0));
-    ktile(nxt, 1, has_nxt, true, 4 + hn + (KT - 3 < 3 ? e : 0));
-    ktile(nxt, 2, has_nxt, true, 2 * hn + (KT - 2 < 3 ? e : 0));
-    ktile(nxt, 3, has_nxt, has_nxt, 8);
-    pre = has_nxt && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
-    __builtin_amdgcn_sched_barrier(0);
-    float* scr = smem + NS * SLOT + wave * 1024;
-    store_tile_lds<TO, 4, 2>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * 64, lane, scr);
-    if (!has_nxt) break;
-    init_acc(nxt);
-    cur = nxt;
-    w += G;
-    has_nxt = w + G < total;
-    if (has_nxt) nxt = setup(w + G);
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // fp32 GEMM for N <= 64 columns over long K (the attention backward's dQ = dS K: M = Nc, K = Ns,
 // one problem per (batch, head); the grouped per-head 1x1 convs).  Streaming A is the whole
 // cost: at the fp32 MFMA rate a 128x64 tile consumes 8 B/clk/CU of A, ~5 TB/s chip-wide, so the
@@ -1427,10 +1195,7 @@ __global__ void __launch_bounds__(512) gemm_f32b_kernel(const GemmP p, int total
 // CU (72 KiB each).  Rows are 128 B (32 floats), chunk c of row r at slot c ^ ((r >> 1) & 7)
 // (applied on the source address, as gemm_ppp_kernel: conflict-free ds_read_b128).
 // ------------------------------------------------------------------------------------
-// CEN (round 4): the centred-A form (kRowsCentred, the MHAda q projection): each A fragment
-// minus the column means p.a_mu in fp32 after its LDS read — the same operand values as the
-// register-staged kernel's centring on load.
-template <int BM, int NS, int BK, bool CEN = false>
+template <int BM, int NS, int BK>
 __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   constexpr int NWV = BM / 32, CH = BK / 4, RPI = 64 / CH;  // 16-B chunks per row, rows per DMA instruction
   constexpr int AH = BM * BK, WH = 64 * BK, STAGE = AH + WH;
@@ -1455,7 +1220,6 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   const int m0 = tile * BM;
   const float* ab = reinterpret_cast<const float*>(p.a) + z1 * p.sa1 + z2 * p.sa2;
   const float* wb = reinterpret_cast<const float*>(p.w) + z1 * p.sw1 + z2 * p.sw2;
-  const float* mub = CEN ? p.a_mu + z1 * p.smu1 + z2 * p.smu2 : nullptr;
   // chunk c of LDS row r sits at slot c ^ sw(r): conflict-free ds_read_b128 fragment reads
   auto sw = [](int r) { return CH == 8 ? (r >> 1) & 7 : r & 15; };
   // staging: one DMA instruction = RPI rows x 128 B (lane -> row lane / CH, slot lane % CH)
@@ -1513,10 +1277,6 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int q = 0; q < CH / 2; ++q) wf[n][q] = *reinterpret_cast<const f32x4*>(swp + n * 32 * BK + koff[q]);
-    if constexpr (CEN) {
-#pragma unroll
-      for (int q = 0; q < CH / 2; ++q) af[q] -= *reinterpret_cast<const f32x4*>(mub + kt * BK + 4 * ((CH / 2) * h + q));
-    }
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
@@ -1555,12 +1315,6 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   const long long total = (long long)p.ntiles * nz;
   if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
-    if constexpr (sizeof(TC) == 4 && BN == 256 && AMODE == MHADA_A_ROWS) {
-      if (tuning().gemm_f32b == 2) {
-        hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN, true>), dim3(grid), dim3(512), 0, stream, p, (int)total);
-        return check_launch("mhada_gemm");
-      }
-    }
     hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN>), dim3(grid), dim3(512), 0, stream, p, (int)total);
     return check_launch("mhada_gemm");
   }
@@ -1569,21 +1323,6 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
     return check_launch("mhada_gemm");
   }
   return fail("mhada_gemm: no ping-pong form");
-}
-
-template <typename TO>
-static int launch_gemm_f32b(const GemmP& p0, int nz, hipStream_t stream) {
-  GemmP p = p0;
-  p.tiles_n = (p.N + 255) / 256;
-  p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
-  p.lds_epi = 1;
-  p.rinit = (sizeof(TO) == 4 && p.r && !p.relu && tuning().gemm_rinit && ((uintptr_t)p.r & 15) == 0 &&
-             p.ldr % 4 == 0 && p.sr1 % 4 == 0 && p.sr2 % 4 == 0 && p.N % 4 == 0) ? 1 : 0;
-  const long long total = (long long)p.ntiles * nz;
-  if (total >= (1LL << 31)) return fail("mhada_gemm: too many tiles");
-  const int grid = (int)std::min<long long>(total, num_cus());
-  hipLaunchKernelGGL((gemm_f32b_kernel<TO>), dim3(grid), dim3(512), 0, stream, p, (int)total);
-  return check_launch("mhada_gemm");
 }
 
 // The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
@@ -1641,14 +1380,11 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
   // barriers interleave: +2-10 % over one 256x64 workgroup of 8 waves (tuning gemm_n64 = 256
   // selects that form); a 4-wave 64x64-per-wave form measured 1.3-2x slower
   if (p.N <= 64) {
-    if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 &&
-                  (AMODE == MHADA_A_ROWS || AMODE == kRowsCentred)) {
-      // fp32 rows, K % 32: the LDS-DMA ring kernel (centred A: tuning gemm_n64_cen, 16-B aligned means)
-      constexpr bool CEN = AMODE == kRowsCentred;
+    if constexpr (sizeof(TC) == 4 && sizeof(TA) == 4 && sizeof(TO) == 4 && AMODE == MHADA_A_ROWS) {
+      // fp32 rows, K % 32: the LDS-DMA ring kernel (the centred-A q projection stays on the
+      // register-staged tile: a ring form with the centring on its fragments measured slower, round 4)
       if (p.K % 32 == 0 && p.lda % 4 == 0 && p.ldw % 4 == 0 && p.sa1 % 4 == 0 && p.sa2 % 4 == 0 &&
-          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w) &&
-          (!CEN || (tuning().gemm_n64_cen && aligned16(p.a_mu) && p.smu1 % 4 == 0 && p.smu2 % 4 == 0 &&
-                    p.K < 1024))) {
+          p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w)) {
         GemmP q = p;
         q.tiles_n = 1;
         // lds_epi (unused by this kernel's direct epilogue) = 4 flags the per-XCD grouping of the
@@ -1660,19 +1396,13 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
         // measured no faster)
         if (p.K >= 1024 && p.K % 64 == 0) {
           q.ntiles = (p.M + 255) / 256;
-          if constexpr (!CEN) hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
+          hipLaunchKernelGGL((gemm_n64_kernel<256, 2, 64>), dim3(q.ntiles, nz), dim3(512), 0, s, q);
         } else {
           q.ntiles = (p.M + 127) / 128;
-          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32, CEN>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
+          hipLaunchKernelGGL((gemm_n64_kernel<128, 2, 32>), dim3(q.ntiles, nz), dim3(256), 0, s, q);
         }
         return check_launch("mhada_gemm");
       }
-    }
-    // bf16 3x3 conv with <= 64 output channels (the decoder's conv2.1, 128 -> 64): the 256x128
-    // persistent ping-pong form with the upper column half idle (tuning gemm_n64_pp)
-    if constexpr (sizeof(TC) == 2 && sizeof(TA) == 2 && AMODE == MHADA_A_CONV3X3) {
-      if (tuning().gemm_n64_pp && p.K % 64 == 0 && p.K >= 128 && pp_enabled() && pp_offsets_fit(p, AMODE))
-        return launch_gemm_pp<bf16, TO, AMODE, 128>(p, nz, s);
     }
     if (tuning().gemm_n64 == 256) return launch_gemm<TC, TA, TO, AMODE, 256, 64, 8, 1>(p, nz, s);
     return launch_gemm<TC, TA, TO, AMODE, 128, 64, 4, 1>(p, nz, s);
@@ -1685,10 +1415,6 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE)) {
-        if constexpr (AMODE == MHADA_A_ROWS) {
-          if (tuning().gemm_f32b == 1) return launch_gemm_f32b<TO>(p, nz, s);
-          if (tuning().gemm_f32b == 3) return launch_gemm_pp<float, TO, AMODE, 128>(p, nz, s);
-        }
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       }
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)

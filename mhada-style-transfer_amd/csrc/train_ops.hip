@@ -1357,7 +1357,8 @@ __global__ void __launch_bounds__(256) feat_stats_finalize_kernel(const double* 
         sq += red[1][k][o];
       }
       const double mean = sa / (double)P;
-      double var = P > 1 ? (sq - mean * sa) / (double)(P - 1) : 0.0;
+      // unbiased (torch.std): a single-pixel map has no variance estimate, NaN as in the reference
+      double var = P > 1 ? (sq - mean * sa) / (double)(P - 1) : (double)NAN;
       if (var < 0.0) var = 0.0;
       mu[idx] = (float)mean;
       sd[idx] = (float)sqrt(var);

@@ -61,7 +61,6 @@ struct WinoP {
   float* y;           // NHWC [B][Ho][Wo][ldc]
   const float* mask;  // null, or [B][Ho][Wo][ldc]: y = 0 where mask <= 0 (a ReLU adjoint folded into a dgrad)
   int B, H, W, Cin, Cout, Ho, Wo, pad, zero, relu;
-  int l2pf;           // tuning wino_l2pf: L2 warm-up of the U chunk two ahead
   long long ldc;
   int nbx, nby, nbn, nblk;
 };
@@ -82,24 +81,9 @@ MHADA_DEV void glds16(const float* src, float* lds) {  // LDS-DMA: lane l -> lds
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-// LDS operand reads issued as inline asm, so that the MFMAs of position x wait only for their own
-// three operands (s_waitcnt lgkmcnt(N) with the operands as in-out dependencies): the compiler's
-// own wait insertion puts lgkmcnt(0) in front of the first MFMA of a chunk here, i.e. it waits for
-// every read of the chunk before the matrix pipe starts
-MHADA_DEV unsigned lds_byte_off(const float* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
-}
-MHADA_DEV void ds_read16(f32x4& r, unsigned byte_off) { asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(byte_off)); }
-template <int N>
-MHADA_DEV void lgkm_wait3(f32x4& a, f32x4& b, f32x4& c) {
-  __builtin_amdgcn_sched_barrier(0);  // the MFMAs before stay before, those after stay after
-  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "i"(N));
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
-  // + 64 floats: the landing area of the L2 warm-up loads (wino_l2pf, below), never read
-  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS) + 64];  // 150 KiB
+  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS)];  // 150 KiB
   auto sV = [&](int i) { return lds + i * kVS; };
   auto sU = [&](int i) { return lds + 2 * kVS + i * kUS; };
   auto sR = [&](int i) { return lds + 2 * (kVS + kUS) + i * kRS; };
@@ -161,22 +145,6 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
     glds16(p.x + roff[0] + cr * kCK, sr + wave * 256);
     if (wave + 8 < kRDma) glds16(p.x + roff[1] + cr * kCK, sr + (wave + 8) * 256);
   };
-  // L2 warm-up of U(k + 2) (p.l2pf): every wave issues one 4-byte LDS-DMA per lane, one per 128-B
-  // line of the chunk's 16 x 2-KiB U segments (waves 4-7 repeat waves 0-3), into a landing area
-  // nobody reads.  U(k + 1)'s DMA then finds its lines in L2 instead of paying the HBM latency
-  // inside the chunk (all workgroups of an XCD ask for the same lines at the same moment).  The
-  // warm-up is the wave's youngest memory operation, so publish waits with vmcnt(1).
-  const int pfl = 64 * (wave & 3) + lane;  // line 0..255: segment xi = pfl / 16, 128-B line pfl % 16
-  const int pfoff = ((pfl >> 4) * p.Cout + co0) * kCK + (pfl & 15) * 32;
-  auto l2warm = [&](int cu) {
-#if WINO_DBG & 2
-    return;
-#endif
-    cu = min(cu, nck - 1);
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.u + cu * ustride + pfoff),
-                                     (__attribute__((address_space(3))) void*)(lds + 2 * (kVS + kUS + kRS)), 4, 0, 0);
-  };
-
   // transform item: channel tc of tile tt; zero-padding positions of its 4x4 patch
   const int tc = tid & 7, tt = tid >> 3;
   // LDS float offsets of the item's 16 raw values (swizzled 16-B slots, see rswz)
@@ -264,20 +232,10 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   for (int k = 0; k < nck; ++k) {
     const int c = k & 1, n = c ^ 1;
     dma(k + 1, sU(n), k + 2, sR(c));
-    if (p.l2pf) l2warm(k + 2);
     mfmas(sV(c), sU(c));
     transform(sR(n), sV(n));
-    if (p.l2pf) {  // this wave's DMA landed (all but its youngest operation, the warm-up), then the barrier
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's V writes
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      publish();
-    }
+    publish();
   }
-  if (p.l2pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last warm-up has landed
 
   // output transform Y = A^T M A (A^T = [[1,1,1,0],[0,1,-1,-1]]): row partials
   // P_i[q] = sum_j M[i][j] A[j][q]; Y[0][q] = P0 + P1 + P2, Y[1][q] = P1 - P2 - P3.  Waves
@@ -339,608 +297,6 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Warp-specialised form (tuning wino_ws, round 4).  The form above runs every wave through the
-// same MFMA / transform / DMA sequence between two barriers, so the MFMA pipe of each SIMD idles
-// while both of its waves transform or wait for their DMA (ablation: MFMAs alone 79 % of the
-// peak, everything 55-60 %).  Here the 8 waves split the roles:
-//   * waves 0-3 (one per SIMD) only multiply: wave w holds row w of the 4 x 4 position grid
-//     (xi = 4w .. 4w+3) for all 32 tiles x 64 channels of the workgroup (4 x 2 accumulator
-//     blocks = 128 registers): per 8-channel chunk 12 ds_read_b128 and 32 MFMAs, then the barrier;
-//   * waves 4-7 (the other wave of each SIMD) issue all the LDS-DMA and transform: each thread one
-//     (tile, channel) item V = B^T d B of the next chunk (32 tiles x 8 channels = 256 items).
-// Workgroup = 4 x 8 tiles (8 x 16 output pixels) x 64 output channels.  The DMA runs two chunks
-// ahead of the MFMAs (U in a 3-slot ring, the raw patch in a 3-slot ring; the per-chunk wait
-// leaves the youngest chunk's 10 pieces per wave in flight), so an L2 / HBM round trip has two
-// chunk times to land instead of one.  The products, their order per accumulator and the output
-// transform's operation order are those of wino_kernel: the result is bit-identical.
-// Measured (profiles/r04_wino_variants.log): 5-13 % SLOWER than wino_kernel on every decoder /
-// VGG19 shape.  Ablation at 256 -> 256 @ 128^2 B8: the MFMA waves alone run within 4 % of
-// wino_kernel's MFMA-only build, but the single transform wave per SIMD (10 LDS-DMA pieces at
-// 60-185 issue cycles each, the transform, the waits) is on the critical path of every chunk, and
-// 32-tile workgroups need twice the U stream per MFMA.  Kept as tuning wino_ws = 1.
-// ------------------------------------------------------------------------------------
-constexpr int kWY = 4, kWX = 8, kWTT = kWY * kWX;      // 32 tiles: 8 x 16 output pixels
-constexpr int kWRX = 2 * kWX + 2, kWRY = 2 * kWY + 2;  // raw patch: 18 x 10 pixels
-constexpr int kWRaw = kWRX * kWRY;                     // 180 pixels x 32 B = 360 16-B slots
-constexpr int kWRDma = 8;                              // raw DMA pieces: 6 used, 2 per transform wave
-constexpr int kWVS = 16 * kWTT * kCK;                  // V buffer (floats): [16][32 tiles][8]
-constexpr int kWRS = kWRDma * 64 * 4;                  // raw buffer (floats): 512 16-B slots
-static_assert(2 * kWRaw <= kWRDma * 64, "raw patch must fit its DMA pieces");
-static_assert((2 * kWVS + 3 * kUS + 3 * kWRS) * 4 <= 160 * 1024, "LDS budget");
-static_assert(4 * 2 * 2 * 16 * 64 <= 2 * kWVS + 3 * kUS, "epilogue exchange must fit sV + sU");
-
-MHADA_DEV void ws_barrier() {  // LDS traffic of this wave done, then the workgroup barrier
-  __builtin_amdgcn_sched_barrier(0);
-  // lgkmcnt(0) as the builtin (not inline asm): the compiler's wait insertion sees it and drops the
-  // pending scalar loads it otherwise carries into the loop (which force every later LDS wait to 0)
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-__global__ void __launch_bounds__(512, 1) wino_ws_kernel(const WinoP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kWVS + 3 * kUS + 3 * kWRS];  // 152 KiB
-  auto sV = [&](int i) { return lds + i * kWVS; };
-  auto sU = [&](int i) { return lds + 2 * kWVS + i * kUS; };
-  auto sR = [&](int i) { return lds + 2 * kWVS + 3 * kUS + i * kWRS; };
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-  int id = xcd_remap(blockIdx.x, p.nblk);  // output-channel block fastest, as wino_kernel
-  const int nb = id % p.nbn;
-  id /= p.nbn;
-  const int bx = id % p.nbx;
-  id /= p.nbx;
-  const int by = id % p.nby;
-  const int b = id / p.nby;
-  const int co0 = nb * kCO;
-  const int P = p.zero ? p.pad : 1;
-  const int nck = p.Cin / kCK;
-
-  f32x16 acc[4][2];
-  if (wave < 4) {
-    // ---- MFMA wave: positions 4 wave + x, A rows = tiles r32, B rows = channels 32 c + r32;
-    // k-step s of lane half h takes channel 4h + s (wino_kernel's operand order)
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[x][c][q] = 0.f;
-    const int arow = swz(r32, h) + 4 * wave * (kWTT * kCK);
-    const int brow0 = swz(r32, h) + 4 * wave * (kCO * kCK), brow1 = swz(32 + r32, h) + 4 * wave * (kCO * kCK);
-    ws_barrier();  // prologue: raw(0) landed
-    ws_barrier();  // prologue: V(0) written
-    {
-      int cu = 0;  // k % 3
-      for (int k = 0; k < nck; ++k) {
-#if !(WINO_DBG & 1)
-        const float* sv = sV(k & 1);
-        const float* su = sU(cu);
-        const unsigned va = lds_byte_off(sv + arow), vb0 = lds_byte_off(su + brow0), vb1 = lds_byte_off(su + brow1);
-        f32x4 av[4], b0[4], b1[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          ds_read16(av[x], va + x * (kWTT * kCK * 4));
-          ds_read16(b0[x], vb0 + x * (kCO * kCK * 4));
-          ds_read16(b1[x], vb1 + x * (kCO * kCK * 4));
-        }
-        auto mf = [&](int x) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            acc[x][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x][s], b0[x][s], acc[x][0], 0, 0, 0);
-            acc[x][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x][s], b1[x][s], acc[x][1], 0, 0, 0);
-          }
-        };
-        lgkm_wait3<9>(av[0], b0[0], b1[0]);
-        mf(0);
-        lgkm_wait3<6>(av[1], b0[1], b1[1]);
-        mf(1);
-        lgkm_wait3<3>(av[2], b0[2], b1[2]);
-        mf(2);
-        lgkm_wait3<0>(av[3], b0[3], b1[3]);
-        mf(3);
-#endif
-        cu = cu == 2 ? 0 : cu + 1;
-        ws_barrier();
-      }
-    }
-    ws_barrier();  // the transform waves' trailing DMA has landed: LDS free for the exchange
-  } else {
-    // ---- transform / DMA wave tw: U pieces 8 tw .. 8 tw + 7 of 32, raw pieces tw and tw + 4
-    const int tw = wave - 4;
-    int uoff[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int slot = 64 * (8 * tw + t) + lane;
-      const int xi = slot >> 7, row = (slot >> 1) & 63, sh = slot & 1;
-      uoff[t] = (xi * p.Cout + co0 + row) * kCK + 4 * (sh ^ ((row >> 3) & 1));
-    }
-    int roff[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int slot = rswz(64 * (tw + 4 * t) + lane);  // logical slot stored at this position
-      const int px = min(slot >> 1, kWRaw - 1);
-      int iy = 2 * by * kWY - P + px / kWRX, ix = 2 * bx * kWX - P + px % kWRX;
-      if (p.zero) {
-        iy = min(max(iy, 0), p.H - 1);
-        ix = min(max(ix, 0), p.W - 1);
-      } else {
-        iy = reflect_clamp(iy, p.H);
-        ix = reflect_clamp(ix, p.W);
-      }
-      roff[t] = ((b * p.H + iy) * p.W + ix) * p.Cin + 4 * (slot & 1);
-    }
-    const long long ustride = (long long)16 * p.Cout * kCK;
-    auto dma_u = [&](int c, float* su) {
-#if !(WINO_DBG & 2)
-      const float* uc = p.u + min(c, nck - 1) * ustride;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) glds16(uc + uoff[t], su + (8 * tw + t) * 256);
-#endif
-    };
-    auto dma_r = [&](int c, float* sr) {
-#if !(WINO_DBG & 2)
-      const int cr = min(c, nck - 1) * kCK;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) glds16(p.x + roff[t] + cr, sr + (tw + 4 * t) * 256);
-#endif
-    };
-    const int ti = tid - 256, tc = ti & 7, tt = ti >> 3;  // item: channel tc of tile tt
-    int roffs[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int pix = (2 * (tt >> 3) + i) * kWRX + 2 * (tt & 7) + j;
-        roffs[4 * i + j] = rswz(2 * pix + (tc >> 2)) * 4 + (tc & 3);
-      }
-    const int vdst = swz(tt, tc >> 2) + (tc & 3);
-    unsigned zmask = 0;
-    if (p.zero) {
-      const int y0 = 2 * (by * kWY + (tt >> 3)) - P, x0 = 2 * (bx * kWX + (tt & 7)) - P;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (y0 + i < 0 || y0 + i >= p.H || x0 + j < 0 || x0 + j >= p.W) zmask |= 1u << (4 * i + j);
-    }
-    auto transform = [&](const float* sr, float* sv) {
-#if !(WINO_DBG & 4)
-      float d[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = sr[roffs[i]];
-        d[i] = (zmask >> i) & 1 ? 0.f : v;
-      }
-      float t[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        t[0 * 4 + j] = d[0 * 4 + j] - d[2 * 4 + j];
-        t[1 * 4 + j] = d[1 * 4 + j] + d[2 * 4 + j];
-        t[2 * 4 + j] = d[2 * 4 + j] - d[1 * 4 + j];
-        t[3 * 4 + j] = d[1 * 4 + j] - d[3 * 4 + j];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        sv[(4 * i + 0) * kWTT * kCK + vdst] = t[4 * i + 0] - t[4 * i + 2];
-        sv[(4 * i + 1) * kWTT * kCK + vdst] = t[4 * i + 1] + t[4 * i + 2];
-        sv[(4 * i + 2) * kWTT * kCK + vdst] = t[4 * i + 2] - t[4 * i + 1];
-        sv[(4 * i + 3) * kWTT * kCK + vdst] = t[4 * i + 1] - t[4 * i + 3];
-      }
-#endif
-    };
-    // prologue: {U(0), raw(0)}, {U(1), raw(1)}, {raw(2)}; transform raw(0) into V[0]
-    dma_u(0, sU(0));
-    dma_r(0, sR(0));
-    dma_u(1, sU(1));
-    dma_r(1, sR(1));
-    dma_r(2, sR(2));
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // U(0), raw(0)
-    ws_barrier();
-    transform(sR(0), sV(0));
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // U(1), raw(1)
-    ws_barrier();
-    // chunk k: DMA U(k+2) -> U[(k+2)%3] (last read by chunk k-1's MFMAs) and raw(k+3) -> R[k%3]
-    // (raw(k), transformed during chunk k-1); transform raw(k+1) into V[(k+1)&1] (read by chunk
-    // k-1's MFMAs); wait until only this chunk's 10 pieces are in flight (U(k+1), raw(k+2) landed)
-    int ck = 0;  // k % 3
-    for (int k = 0; k < nck; ++k) {
-      const int c1 = ck == 2 ? 0 : ck + 1, c2 = c1 == 2 ? 0 : c1 + 1;
-      dma_u(k + 2, sU(c2));
-      dma_r(k + 3, sR(ck));
-      transform(sR(c1), sV((k + 1) & 1));
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      ws_barrier();
-      ck = c1;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMA past the end
-    ws_barrier();
-  }
-
-  // output transform (wino_kernel's operation order): row partials P_w[q] = sum_j M[w][j] A[j][q]
-  // through LDS [w][q][c][r][64 lanes]; Y[0][q] = P0 + P1 + P2, Y[1][q] = P1 + (-P2 - P3)
-  if (wave < 4) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float m0 = acc[0][c][r], m1 = acc[1][c][r], m2 = acc[2][c][r], m3 = acc[3][c][r];
-        lds[(((wave * 2 + 0) * 2 + c) * 16 + r) * 64 + lane] = m0 + m1 + m2;
-        lds[(((wave * 2 + 1) * 2 + c) * 16 + r) * 64 + lane] = m1 - m2 - m3;
-      }
-  }
-  ws_barrier();
-  const int c = wave & 1, rq = wave >> 1;
-  const int co = co0 + 32 * c + r32;
-  const float bias = p.bias ? p.bias[co] : 0.f;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int r = 4 * rq + rr;
-    const int tile = rr + 8 * rq + 4 * h;  // (r & 3) + 8 (r >> 2) + 4 h
-    const int oy0 = 2 * (by * kWY + (tile >> 3)), ox0 = 2 * (bx * kWX + (tile & 7));
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float pw[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) pw[w] = lds[(((w * 2 + q) * 2 + c) * 16 + r) * 64 + lane];
-      float y0 = pw[0] + pw[1] + pw[2] + bias;
-      float y1 = pw[1] + (-pw[2] - pw[3]) + bias;
-      if (p.relu) {
-        y0 = fmaxf(y0, 0.f);
-        y1 = fmaxf(y1, 0.f);
-      }
-      const int ox = ox0 + q;
-      if (ox < p.Wo) {
-        const long long i0 = ((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co;
-        const long long i1 = i0 + (long long)p.Wo * p.ldc;
-        if (p.mask) {
-          if (oy0 < p.Ho && !(p.mask[i0] > 0.f)) y0 = 0.f;
-          if (oy0 + 1 < p.Ho && !(p.mask[i1] > 0.f)) y1 = 0.f;
-        }
-        if (oy0 < p.Ho) p.y[i0] = y0;
-        if (oy0 + 1 < p.Ho) p.y[i1] = y1;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Persistent warp-specialised form on v_mfma_f32_16x16x4_f32 (tuning wino_ws = 2, round 4).
-// wino_ws_kernel's role split, without its three losses:
-//   * no output exchange: MFMA wave w holds ALL 16 positions for 16 tiles x 32 channels
-//     (tiles 16 (w & 1).., channels 32 (w >> 1)..: 16 positions x 2 blocks of 16 x 16 = 128
-//     accumulator registers), so the output transform runs in its own registers;
-//   * persistent: one workgroup per CU walks its items (32 tiles x 64 channels each) as one
-//     continuous chunk stream — the DMA / transform waves run into the next item while the MFMA
-//     waves finish the current one and store it, so an item pays neither a pipeline fill nor a
-//     drain (a launch of 16-32 items per CU paid both per item);
-//   * no read-latency bubble at the chunk boundary: two barriers per chunk step s.  The
-//     transform waves write V(s+1) and wait for U(s+1) BEFORE the middle barrier; past it the
-//     MFMA waves' rolling operand window (reads issued 3 positions ahead, inline-asm ds_read_b64
-//     with counted lgkmcnt waits) runs on into chunk s+1, across the end barrier.
-// Per chunk of 8 input channels and MFMA wave: 16 positions x (1 + 2 ds_read_b64, 2 k-steps x 2
-// blocks = 4 MFMAs): 48 reads and 64 MFMAs (2048 matrix cycles).  The k-steps split the chunk's
-// channels as lane group j = lane >> 4 -> channels (2j, 2j+1): one 8-byte read per operand from
-// the same swizzled 32-B rows the DMA and transform produce (swz; conflict-free ds_read_b64).
-// Rings: V 2 x 16 KiB, U 3 x 32 KiB, raw 3 x 8 KiB (the U DMA runs two chunks ahead).
-// Measured (profiles/r04_wino_variants.log): 8-26 % SLOWER than wino_kernel.  Its MFMA waves alone
-// (ablation build, no loads, no transform) are as fast as wino_kernel's MFMA-only build (536 vs
-// 538 us at 256 -> 256 @ 128^2 B8), so the lost time is the transform / DMA waves': 486 us alone
-// for that shape, and the two roles meet at two barriers per chunk; staging the pieces through
-// registers (global_load + ds_write_b128) instead of LDS-DMA was slower still (1.32x).  Kept as
-// tuning wino_ws = 2: the design notes for a faster transform path are in DESIGN.md §3a.
-// ------------------------------------------------------------------------------------
-template <class F, int... I>
-MHADA_DEV void static_for(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int OFF>
-MHADA_DEV void ds_read8(f32x2& r, unsigned byte_off) {
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(byte_off), "i"(OFF));
-}
-template <int N>
-MHADA_DEV void lgkm_wait3x2(f32x2& a, f32x2& b, f32x2& c) {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "i"(N));
-  __builtin_amdgcn_sched_barrier(0);
-}
-MHADA_DEV void bare_barrier() {  // no wait of this wave's own memory traffic
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-struct PkItem {
-  int b, by, bx, co0;
-};
-MHADA_DEV PkItem pk_item(const WinoP& p, int j) {  // item j of this workgroup
-  int id = xcd_remap(j * (int)gridDim.x + (int)blockIdx.x, p.nblk);
-  PkItem it;
-  const int nb = id % p.nbn;
-  id /= p.nbn;
-  it.bx = id % p.nbx;
-  id /= p.nbx;
-  it.by = id % p.nby;
-  it.b = id / p.nby;
-  it.co0 = nb * kCO;
-  return it;
-}
-
-__global__ void __launch_bounds__(512, 1) wino_pk_kernel(const WinoP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kWVS + 3 * kUS + 3 * kWRS];  // 152 KiB
-  auto sV = [&](int i) { return lds + i * kWVS; };
-  auto sU = [&](int i) { return lds + 2 * kWVS + i * kUS; };
-  auto sR = [&](int i) { return lds + 2 * kWVS + 3 * kUS + i * kWRS; };
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int P = p.zero ? p.pad : 1;
-  const int nck = p.Cin / kCK;
-  const int G = gridDim.x;
-  const int nit = (p.nblk - (int)blockIdx.x + G - 1) / G;  // >= 1: the grid never exceeds the items
-  const int nst = nit * nck;                              // chunk steps of this workgroup
-
-  if (wave < 4) {
-    // ---- MFMA wave: tiles T0 + (lane & 15), channels C0 + 16 c + (lane & 15); lane group
-    // j = lane >> 4 supplies channels 2j (k-step 0) and 2j + 1 (k-step 1) of every chunk
-    const int j = lane >> 4, t16 = lane & 15;
-    const int T0 = 16 * (wave & 1), C0 = 32 * (wave >> 1);
-    const unsigned offA = 4 * (swz(T0 + t16, j >> 1) + 2 * (j & 1));
-    const unsigned offB = 4 * (swz(C0 + t16, j >> 1) + 2 * (j & 1));  // block c = 1: +16 rows = +512 B
-    const unsigned ldsV = lds_byte_off(sV(0)), ldsU = lds_byte_off(sU(0));
-    auto baseA = [&](int c) { return ldsV + (unsigned)((c & 1) * kWVS * 4) + offA; };
-    auto baseB = [&](int c) { return ldsU + (unsigned)((c % 3) * kUS * 4) + offB; };
-    f32x4 acc[16][2];
-#pragma unroll
-    for (int x = 0; x < 16; ++x)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) acc[x][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x2 ra[4], rb0[4], rb1[4];  // operand window: position xi in slot xi % 4
-    constexpr int D = 3;          // reads issued D positions ahead
-    auto issue = [&](auto XIc, unsigned a, unsigned bb) {  // the reads of position XI of a chunk
-      constexpr int XI = decltype(XIc)::value;
-      ds_read8<XI * kWTT * kCK * 4>(ra[XI & 3], a);
-      ds_read8<XI * kCO * kCK * 4>(rb0[XI & 3], bb);
-      ds_read8<XI * kCO * kCK * 4 + 16 * kCK * 4>(rb1[XI & 3], bb);
-    };
-    auto store_item = [&](const PkItem& it) {  // output transform of the finished item
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int co = it.co0 + C0 + 16 * c + t16;
-        const float bias = p.bias ? p.bias[co] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float pr[4][2];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float m0 = acc[4 * r][c][i], m1 = acc[4 * r + 1][c][i], m2 = acc[4 * r + 2][c][i],
-                        m3 = acc[4 * r + 3][c][i];
-            pr[r][0] = m0 + m1 + m2;
-            pr[r][1] = m1 - m2 - m3;
-          }
-          const int tile = T0 + 4 * j + i;
-          const int oy0 = 2 * (it.by * kWY + (tile >> 3)), ox0 = 2 * (it.bx * kWX + (tile & 7));
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            float y0 = pr[0][q] + pr[1][q] + pr[2][q] + bias;
-            float y1 = pr[1][q] + (-pr[2][q] - pr[3][q]) + bias;
-            if (p.relu) {
-              y0 = fmaxf(y0, 0.f);
-              y1 = fmaxf(y1, 0.f);
-            }
-            const int ox = ox0 + q;
-            if (ox < p.Wo) {
-              const long long i0 = ((long long)(it.b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co;
-              const long long i1 = i0 + (long long)p.Wo * p.ldc;
-              if (p.mask) {
-                if (oy0 < p.Ho && !(p.mask[i0] > 0.f)) y0 = 0.f;
-                if (oy0 + 1 < p.Ho && !(p.mask[i1] > 0.f)) y1 = 0.f;
-              }
-              if (oy0 < p.Ho) p.y[i0] = y0;
-              if (oy0 + 1 < p.Ho) p.y[i1] = y1;
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int x = 0; x < 16; ++x)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[x][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-
-    bare_barrier();  // prologue: U(0), raw(0) landed
-    bare_barrier();  // prologue: V(0) written, U(1) landed
-    static_for([&](auto XIc) { issue(XIc, baseA(0), baseB(0)); }, std::make_integer_sequence<int, D>{});
-    int item = 0, k = 0;  // the item / chunk of step s
-    for (int s = 0; s < nst; ++s) {
-      const unsigned a0 = baseA(s), b0 = baseB(s), a1 = baseA(s + 1), b1 = baseB(s + 1);
-      static_for(
-          [&](auto XIc) {
-            constexpr int XI = decltype(XIc)::value;
-            if constexpr (XI == 16 - D) bare_barrier();  // middle: V(s+1) written, U(s+1) landed
-            if constexpr (XI + D < 16)
-              issue(std::integral_constant<int, XI + D>{}, a0, b0);
-            else
-              issue(std::integral_constant<int, XI + D - 16>{}, a1, b1);
-            lgkm_wait3x2<3 * D>(ra[XI & 3], rb0[XI & 3], rb1[XI & 3]);
-#if !(WINO_DBG & 1)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-              acc[XI][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[XI & 3][ks], rb0[XI & 3][ks], acc[XI][0], 0, 0, 0);
-              acc[XI][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[XI & 3][ks], rb1[XI & 3][ks], acc[XI][1], 0, 0, 0);
-            }
-#endif
-          },
-          std::make_integer_sequence<int, 16>{});
-      if (++k == nck) {
-        store_item(pk_item(p, item));
-        k = 0;
-        ++item;
-      }
-      bare_barrier();  // end: this step's U / V slots free
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the window's reads past the end
-  } else {
-    // ---- transform / DMA wave tw: U pieces 8 tw .. 8 tw + 7 of 32, raw pieces tw and tw + 4
-    const int tw = wave - 4;
-    int uoff[8];  // item-independent part: (xi, co row, stored half) of the slot
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int slot = 64 * (8 * tw + t) + lane;
-      const int xi = slot >> 7, row = (slot >> 1) & 63, sh = slot & 1;
-      uoff[t] = (xi * p.Cout + row) * kCK + 4 * (sh ^ ((row >> 3) & 1));
-    }
-    int rpx[2];  // the raw-patch pixel of this lane's slot in pieces tw, tw + 4
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int slot = rswz(64 * (tw + 4 * t) + lane);
-      rpx[t] = min(slot >> 1, kWRaw - 1) | ((slot & 1) << 16);
-    }
-    const long long ustride = (long long)16 * p.Cout * kCK;
-    // stream cursors (chunk, item, chunk within the item; clamped to the last chunk), advanced
-    // once per step, with the per-item quantities cached: no divisions in the loop
-    struct Cur {
-      int c, it, k;
-    };
-    auto cur_at = [&](int c) {
-      c = min(c, nst - 1);
-      Cur q;
-      q.c = c;
-      q.it = c / nck;
-      q.k = c - q.it * nck;
-      return q;
-    };
-    auto adv = [&](Cur& q) {
-      if (q.c < nst - 1) {
-        ++q.c;
-        if (++q.k == nck) {
-          q.k = 0;
-          ++q.it;
-        }
-      }
-    };
-    int u_it = -1, u_co = 0;         // U DMA: item, its output-channel offset
-    int r_it = -1, r_off[2] = {0, 0};  // raw DMA: item, this lane's two source pixels
-    auto u_src = [&](const Cur& cu) {
-      if (cu.it != u_it) {
-        u_it = cu.it;
-        u_co = pk_item(p, u_it).co0 * kCK;
-      }
-      return p.u + cu.k * ustride + u_co;
-    };
-    auto r_src = [&](const Cur& cr) {
-      if (cr.it != r_it) {
-        r_it = cr.it;
-        const PkItem ri = pk_item(p, r_it);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int px = rpx[t] & 0xffff;
-          int iy = 2 * ri.by * kWY - P + px / kWRX, ix = 2 * ri.bx * kWX - P + px % kWRX;
-          if (p.zero) {
-            iy = min(max(iy, 0), p.H - 1);
-            ix = min(max(ix, 0), p.W - 1);
-          } else {
-            iy = reflect_clamp(iy, p.H);
-            ix = reflect_clamp(ix, p.W);
-          }
-          r_off[t] = ((ri.b * p.H + iy) * p.W + ix) * p.Cin + 4 * (rpx[t] >> 16);
-        }
-      }
-      return p.x + cr.k * kCK;
-    };
-    auto dma = [&](const Cur& cu, float* su, const Cur& cr, float* sr) {
-#if !(WINO_DBG & 2)
-      const float* uc = u_src(cu);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) glds16(uc + uoff[t], su + (8 * tw + t) * 256);
-      const float* xc = r_src(cr);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) glds16(xc + r_off[t], sr + (tw + 4 * t) * 256);
-#endif
-    };
-    const int ti = tid - 256, tc = ti & 7, tt = ti >> 3;  // item: channel tc of tile tt
-    int roffs[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int pix = (2 * (tt >> 3) + i) * kWRX + 2 * (tt & 7) + jj;
-        roffs[4 * i + jj] = rswz(2 * pix + (tc >> 2)) * 4 + (tc & 3);
-      }
-    const int vdst = swz(tt, tc >> 2) + (tc & 3);
-    int t_it = -1;
-    unsigned rv = 15u, cv = 15u;  // rows / columns of the item's 4 x 4 patch inside the image (zero pad)
-    auto transform = [&](const Cur& ct, const float* sr, float* sv) {
-#if !(WINO_DBG & 4)
-      if (p.zero && ct.it != t_it) {
-        t_it = ct.it;
-        const PkItem ti2 = pk_item(p, t_it);
-        const int y0 = 2 * (ti2.by * kWY + (tt >> 3)) - P, x0 = 2 * (ti2.bx * kWX + (tt & 7)) - P;
-        rv = cv = 0u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          rv |= (unsigned)((unsigned)(y0 + i) < (unsigned)p.H) << i;
-          cv |= (unsigned)((unsigned)(x0 + i) < (unsigned)p.W) << i;
-        }
-      }
-      float d[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float v = sr[roffs[4 * i + jj]];
-          d[4 * i + jj] = ((rv >> i) & (cv >> jj) & 1u) ? v : 0.f;
-        }
-      float t[16];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        t[0 * 4 + jj] = d[0 * 4 + jj] - d[2 * 4 + jj];
-        t[1 * 4 + jj] = d[1 * 4 + jj] + d[2 * 4 + jj];
-        t[2 * 4 + jj] = d[2 * 4 + jj] - d[1 * 4 + jj];
-        t[3 * 4 + jj] = d[1 * 4 + jj] - d[3 * 4 + jj];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        sv[(4 * i + 0) * kWTT * kCK + vdst] = t[4 * i + 0] - t[4 * i + 2];
-        sv[(4 * i + 1) * kWTT * kCK + vdst] = t[4 * i + 1] + t[4 * i + 2];
-        sv[(4 * i + 2) * kWTT * kCK + vdst] = t[4 * i + 2] - t[4 * i + 1];
-        sv[(4 * i + 3) * kWTT * kCK + vdst] = t[4 * i + 1] - t[4 * i + 3];
-      }
-#endif
-    };
-    // prologue: {U(0), raw(0)}, {U(1), raw(1)}, {raw(2) (+ a duplicate U(1))}; transform raw(0)
-    dma(cur_at(0), sU(0), cur_at(0), sR(0));
-    dma(cur_at(1), sU(1), cur_at(1), sR(1));
-    dma(cur_at(1), sU(1), cur_at(2), sR(2));
-    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // U(0), raw(0)
-    bare_barrier();
-    transform(cur_at(0), sR(0), sV(0));
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // U(1), raw(1)
-    __builtin_amdgcn_s_waitcnt(0xc07f);                 // this wave's V writes
-    bare_barrier();
-    // step s: DMA U(s+2) -> U[(s+2)%3] (U(s-1)'s slot) and raw(s+3) -> R[s%3] (raw(s)'s); transform
-    // raw(s+1) into V[(s+1)&1]; the previous step's DMA (U(s+1), raw(s+2)) landed + V(s+1)
-    // written -> middle barrier; end barrier
-    Cur ct = cur_at(1), cu = cur_at(2), cr = cur_at(3);
-    int su2 = 2, sr0 = 0;  // (s + 2) % 3, s % 3
-    for (int s = 0; s < nst; ++s) {
-      const int sr1 = sr0 == 2 ? 0 : sr0 + 1;  // (s + 1) % 3
-      dma(cu, sU(su2), cr, sR(sr0));
-      transform(ct, sR(sr1), sV((s + 1) & 1));
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      bare_barrier();  // middle
-      bare_barrier();  // end
-      adv(ct);
-      adv(cu);
-      adv(cr);
-      su2 = su2 == 2 ? 0 : su2 + 1;
-      sr0 = sr1;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMA past the end
-  }
-}
 
 // U = G g G^T per (co, ci); w [Cout][3][3][Cin] -> u [Cin/8][16][Cout][8]
 __global__ void wino_weights_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
@@ -1294,16 +650,6 @@ extern "C" int mhada_wino_weights(const float* w, float* u, int Cout, int Cin, m
   return check_launch("mhada_wino_weights");
 }
 
-static int wino_num_cus() {
-  static const int n = [] {
-    int d = 0, v = 0;
-    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      v = 0;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
-
 extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* bias, float* y, int B, int H, int W,
                                   int Cin, int Cout, long long ldc, int pad_mode, int pad, int relu,
                                   const float* relu_mask, mhada_stream_t s_) {
@@ -1323,21 +669,14 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   p.Wo = p.zero ? W + 2 * (pad - 1) : W;
   p.relu = relu;
   p.ldc = ldc;
-  p.l2pf = tuning().wino_l2pf;
-  const int ws = tuning().wino_ws;
   const int TY = (p.Ho + 1) / 2, TX = (p.Wo + 1) / 2;
-  p.nby = ws ? (TY + kWY - 1) / kWY : (TY + kT - 1) / kT;
-  p.nbx = ws ? (TX + kWX - 1) / kWX : (TX + kT - 1) / kT;
+  p.nby = (TY + kT - 1) / kT;
+  p.nbx = (TX + kT - 1) / kT;
   p.nbn = Cout / kCO;
   const long long nblk = (long long)B * p.nby * p.nbx * p.nbn;
   if (nblk > (1LL << 31) - 1 || (long long)B * H * W * Cin > (1LL << 31) - 1)
     return fail("mhada_conv3x3_wino: problem too large for 32-bit indexing");
   p.nblk = (int)nblk;
-  if (ws == 2)  // persistent: one workgroup per CU (152 KiB of LDS each)
-    hipLaunchKernelGGL(wino_pk_kernel, dim3(std::min(p.nblk, wino_num_cus())), dim3(512), 0, (hipStream_t)s_, p);
-  else if (ws)
-    hipLaunchKernelGGL(wino_ws_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
-  else
-    hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
+  hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
   return check_launch("mhada_conv3x3_wino");
 }

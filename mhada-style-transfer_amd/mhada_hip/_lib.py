@@ -58,6 +58,7 @@ SIGNATURES = {
     "mhada_last_error": (ctypes.c_char_p, []),
     "mhada_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "mhada_get_tuning": (_I, [ctypes.c_char_p, ctypes.POINTER(_I)]),
+    "mhada_clock_probe": (_I, [_vp, _I, _I, _vp]),
     "mhada_gemm": (_I, [ctypes.POINTER(GemmArgs), _vp]),
     "mhada_layernorm": (_I, [_vp, _vp, _I, _vp, _vp, _I, _I, _F, _vp]),
     "mhada_vit_batch_attn": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
@@ -136,7 +137,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 def get_tuning(name: str) -> int:

@@ -527,8 +527,19 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
     if lse.shape != (BH, Nc) or dmo.shape != (BH, Nc, 128) or dd.shape != (BH, Nc) or k.shape != (BH, Ns, 64) \
             or v.shape != k.shape:
         raise ValueError("attn_train_bwd: bad shapes")
-    if spill is None:
+    auto = spill is None
+    if auto:
         spill = ds_spill_eligible(BH, Nc, Ns)
+    ds = None
+    if spill:
+        try:
+            ds = torch.empty(BH, Nc, Ns, device=q.device, dtype=torch.float32)
+        except torch.cuda.OutOfMemoryError:
+            # the shape rule chose the spill but the device has no room for dS (a smaller card or a
+            # larger batch): the recompute backward needs no workspace (same gradients to fp32 order)
+            if not auto:
+                raise
+            spill = False
     BWD_PATH_COUNTS["spill" if spill else "recompute"] += 1
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
@@ -539,7 +550,6 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
         return dq, dk, dv
     if Ns % 4:
         raise ValueError("attn_train_bwd: the dS spill needs Ns % 4 == 0")
-    ds = torch.empty(BH, Nc, Ns, device=q.device, dtype=torch.float32)
     _call("mhada_attn_train_dkv", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
           dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, Nc, Ns)
     kt = transpose64(k)  # W[n = d][k = key] of the NT GEMM, rows padded to ceil64(Ns)

@@ -27,7 +27,8 @@ def _json_lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-SMALL = ["--train", "--device", "cpu", "--train-res", "64", "--train-batch", "1", "--steps", "1", "--warmup", "0"]
+# two images per rank: each rank's micro-batch is one coupled forward call
+SMALL = ["--train", "--device", "cpu", "--train-res", "64", "--train-batch", "2", "--steps", "1", "--warmup", "0"]
 
 
 def test_gpus_2_self_launches_two_ranks():
@@ -37,7 +38,7 @@ def test_gpus_2_self_launches_two_ranks():
     assert len(lines) == 1, p.stdout  # rank 0 only
     r = lines[0]
     assert r["n_gpus"] == 2
-    assert r["config"]["global_batch"] == 2 and r["config"]["backend"] == "gloo"
+    assert r["config"]["global_batch"] == 4 and r["config"]["backend"] == "gloo"
     ag = r["rank_agreement"]
     assert ag["identical"] and ag["world"] == 2 and ag["backend"] == "gloo", ag
     assert all(v == v for v in r["last_losses"].values())  # finite (not NaN)

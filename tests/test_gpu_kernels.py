@@ -55,41 +55,34 @@ def test_linear(cdt, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(70000, 1024, 64), (70000, 768, 512), (32400, 512, 2048), (57000, 600, 96),
                                    (65536, 2048, 512)])
-def test_gemm_f32b_matches_pingpong(M, N, K):
-    """The one-barrier fp32 kernel (tuning gemm_f32b = 1; 16-deep K-tiles, so its MFMAs pair other
-    k than the ping-pong kernel's and the fp32 rounding differs) against fp64 and the ping-pong
-    kernel: bias / ReLU / residual (preloaded) / bf16 copy outputs; several tiles per CU, the
-    K-tile stream across tiles with 4 to 128 K-tiles, partial row and column tiles."""
+def test_gemm_f32_persistent_epilogues(M, N, K):
+    """The fp32 persistent ping-pong GEMM: bias / ReLU / residual (preloaded into the
+    accumulators) / bf16 copy outputs against fp64 on every row tile (last partial), several tiles
+    per CU, 2 to 64 K-tiles, partial column tiles; a second run is bit-identical."""
     x = rnd(M, K, seed=1)
     w = rnd(N, K, scale=K ** -0.5, seed=2)
     b = rnd(N, seed=3)
     r = rnd(M, N, seed=4)
-    outs = {}
-    for knob in (0, 1, 2, 3):
-        with _lib.tuning(gemm_f32b=knob):
-            c2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-            y0 = torch.empty(M, N, device=DEV)
-            ops.gemm(a=x, w=w, c=y0, M=M, N=N, K=K, compute=torch.float32, lda=K, ldw=K, bias=b, ldc=N,
-                     c2=c2, ldc2=N)
-            outs[knob] = (ops.linear(x, w, b, torch.float32, residual=r),
-                          ops.linear(x, w, b, torch.float32, relu=True),
-                          ops.linear(x, w, None, torch.float32), y0)
-            outs[knob, "c2"] = c2
-            torch.cuda.synchronize()
+    outs = []
+    for _ in range(2):
+        c2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        y0 = torch.empty(M, N, device=DEV)
+        ops.gemm(a=x, w=w, c=y0, M=M, N=N, K=K, compute=torch.float32, lda=K, ldw=K, bias=b, ldc=N,
+                 c2=c2, ldc2=N)
+        outs.append((ops.linear(x, w, b, torch.float32, residual=r),
+                     ops.linear(x, w, b, torch.float32, relu=True),
+                     ops.linear(x, w, None, torch.float32), y0, c2))
+        torch.cuda.synchronize()
     for a, c in zip(outs[0], outs[1]):
-        assert rel(c, a) < 2e-6
-    # gemm_f32b = 2 (the ping-pong kernel with two phases per K-tile) and = 3 (its 256x128 tiles)
-    # keep every accumulator's k order: bit-identical
-    for knob in (2, 3):
-        for a, c in zip(outs[0] + (outs[0, "c2"],), outs[knob] + (outs[knob, "c2"],)):
-            assert torch.equal(a, c)
-    assert rel(outs[1, "c2"], outs[1][3]) < 4e-3
-    # every row tile (last partial) against fp64 on a sample of rows
+        assert torch.equal(a, c)
+    res, rl, plain, y0, c2 = outs[0]
+    assert rel(c2, y0) < 4e-3
     rows = torch.cat([torch.arange(0, M, 997), torch.arange(M - 300, M)]).to(DEV)
     ref = x[rows].double() @ w.double().T + b.double()
-    assert rel(outs[1][0][rows], ref + r[rows].double()) < TOL[torch.float32]
-    assert rel(outs[1][1][rows], torch.relu(ref)) < TOL[torch.float32]
-    assert rel(outs[1][3][rows], ref) < TOL[torch.float32]
+    assert rel(res[rows], ref + r[rows].double()) < TOL[torch.float32]
+    assert rel(rl[rows], torch.relu(ref)) < TOL[torch.float32]
+    assert rel(y0[rows], ref) < TOL[torch.float32]
+    assert rel(plain[rows], ref - b.double()) < TOL[torch.float32]
 
 
 @pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
@@ -101,21 +94,19 @@ def test_linear_fp32_input_converted_on_load(cdt):
     assert rel(y, ref) < TOL[cdt]
 
 
-@pytest.mark.parametrize("cdt,ring", [(torch.float32, 0), (torch.float32, 1), (torch.bfloat16, 0)])
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("N", [200, 4096])
-def test_grouped_centred_projection(cdt, ring, N):
-    """The MHAda per-head projection pattern: z = (batch, head), A centred per column; ring = 1:
-    the fp32 LDS-DMA ring kernel with the centring on its fragments (tuning gemm_n64_cen)."""
+def test_grouped_centred_projection(cdt, N):
+    """The MHAda per-head projection pattern: z = (batch, head), A centred per column."""
     B, H, C = 2, 8, 512
     x = rnd(B, N, C, seed=7) * 3 + 1.5
     mu = x.mean(dim=1)  # [B][C]
     w = rnd(B, H, 64, 64, scale=0.125, seed=8, dtype=cdt)
     bias = rnd(H, 64, seed=9)
     q = torch.empty(B, H, N, 64, device=DEV, dtype=cdt)
-    with _lib.tuning(gemm_n64_cen=ring):
-        ops.gemm(a=x, w=w, c=q, M=N, N=64, K=64, compute=cdt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
-                 smu=(C, 64), ldw=64, sw=(H * 4096, 4096), bias=bias, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
-        torch.cuda.synchronize()
+    ops.gemm(a=x, w=w, c=q, M=N, N=64, K=64, compute=cdt, lda=C, sa=(N * C, 64), nb=(B, H), a_mu=mu,
+             smu=(C, 64), ldw=64, sw=(H * 4096, 4096), bias=bias, sb=(0, 64), ldc=64, sc=(H * N * 64, N * 64))
+    torch.cuda.synchronize()
     xc = (x - mu[:, None, :]).view(B, N, H, 64).permute(0, 2, 1, 3).to(cdt).double()
     ref = xc @ w.double().transpose(-1, -2) + bias.double()[None, :, None, :]
     assert rel(q, ref) < TOL[cdt]
@@ -196,27 +187,6 @@ def test_conv3x3(cdt, up, Ci, Co, H, W):
     assert rel(y.permute(0, 3, 1, 2), ref) < TOL[cdt]
 
 
-@pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,Ci,Co,H,W", [(2, 128, 64, 64, 64), (1, 256, 64, 33, 20), (3, 128, 40, 17, 70),
-                                         (4, 128, 64, 128, 128)])
-def test_conv3x3_bf16_n64_pingpong(out, B, Ci, Co, H, W):
-    """bf16 3x3 conv with <= 64 output channels on the 256x128 ping-pong kernel (tuning
-    gemm_n64_pp = 1, the upper column half idle) against fp64 and the default 128x64 kernel."""
-    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(Ci + H)).to(DEV, torch.bfloat16)
-    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, seed=2)
-    b = rnd(Co, seed=3)
-    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).to(torch.bfloat16).contiguous()
-    ys = {}
-    for knob in (0, 1):
-        with _lib.tuning(gemm_n64_pp=knob):
-            ys[knob] = ops.conv3x3(x, wp, b, out, upsample=False)
-            torch.cuda.synchronize()
-    ref = torch.relu(F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
-                              w.to(torch.bfloat16).double(), b.double()))
-    assert rel(ys[1].permute(0, 3, 1, 2), ref) < TOL[torch.bfloat16]
-    assert rel(ys[1], ys[0]) < (1e-5 if out == torch.float32 else 8e-3)
-
-
 @pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
 @pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
                                               (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64),
@@ -234,6 +204,7 @@ def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
     Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
     xn = x.permute(0, 3, 1, 2).double()
     xp = F.pad(xn, (1, 1, 1, 1), mode="reflect") if pad_mode == "reflect" else F.pad(xn, (pad,) * 4)
+    mask = (torch.rand(B, Ho, Wo, ldc, generator=torch.Generator().manual_seed(Ci)) - 0.5).to(DEV)
     for bias, relu in ((b, True), (None, False)):
         out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
         y = ops.conv3x3_wino(x, ops.wino_weights(wp), bias, relu, pad_mode, pad, out=out)
@@ -241,6 +212,12 @@ def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
         ref = torch.relu(ref) if relu else ref
         assert rel(y[..., :Co].permute(0, 3, 1, 2), ref) < 2e-6
         assert bool((y[..., Co:] == 7.0).all())
+        # the folded ReLU adjoint (relu_mask): zero exactly where mask <= 0, the same values elsewhere
+        outm = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
+        ym = ops.conv3x3_wino(x, ops.wino_weights(wp), bias, relu, pad_mode, pad, out=outm, relu_mask=mask)
+        keep = mask[..., :Co] > 0
+        assert torch.equal(ym[..., :Co], torch.where(keep, y[..., :Co], torch.zeros_like(y[..., :Co])))
+        assert bool((ym[..., Co:] == 7.0).all())
         if Ci % 32:  # the fp32 implicit GEMM gathers 32-channel chunks
             continue
         ops.WINO = False
@@ -249,74 +226,6 @@ def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
         finally:
             ops.WINO = True
         assert rel(y[..., :Co], yd) < 2e-6
-
-
-@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
-@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
-                                              (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64), (2, 2, 5, 24, 192, 196),
-                                              (1, 40, 36, 96, 64, 64), (2, 64, 48, 16, 64, 64)])
-def test_conv3x3_wino_ws_bit_identical(pad_mode, pad, B, H, W, Ci, Co, ldc):
-    """The warp-specialised Winograd kernel (tuning wino_ws = 1, the default: MFMA waves + transform /
-    DMA waves, 4 x 8-tile workgroups, DMA two chunks ahead) computes the same products in the same
-    order as wino_kernel (wino_ws = 0): bit-identical outputs, bias + ReLU, the folded ReLU mask
-    (relu_mask), padded ldc columns untouched; 1 and 2 chunks (Ci = 8, 16) exercise the prologue."""
-    g = torch.Generator().manual_seed(B * H * W + Ci)
-    x = (torch.rand(B, H, W, Ci, generator=g) - 0.3).to(DEV)
-    wp = (torch.randn(Co, 9 * Ci, generator=g) * (9 * Ci) ** -0.5).to(DEV)
-    bias = torch.randn(Co, generator=g).to(DEV)
-    u = ops.wino_weights(wp)
-    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
-    mask = (torch.rand(B, Ho, Wo, ldc, generator=g) - 0.5).to(DEV)
-    for kw in (dict(bias=bias, relu=True), dict(bias=None, relu=False), dict(bias=bias, relu=False, relu_mask=mask)):
-        outs = []
-        for ws in (0, 1):
-            out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
-            with _lib.tuning(wino_ws=ws):
-                outs.append(ops.conv3x3_wino(x, u, kw["bias"], kw["relu"], pad_mode, pad, out=out,
-                                             relu_mask=kw.get("relu_mask")))
-        assert torch.equal(outs[0], outs[1]), kw.keys()
-        assert bool((outs[1][..., Co:] == 7.0).all())
-
-
-@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
-@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
-                                              (1, 3, 2, 16, 64, 64), (3, 17, 70, 256, 64, 64), (2, 2, 5, 24, 192, 196),
-                                              (4, 128, 128, 16, 128, 128), (8, 64, 64, 8, 64, 64),
-                                              (3, 50, 70, 24, 128, 132), (1, 16, 16, 512, 256, 256)])
-@pytest.mark.parametrize("ws", [2])
-def test_conv3x3_wino_persistent(ws, pad_mode, pad, B, H, W, Ci, Co, ldc):
-    """The persistent 16x16x4 Winograd kernel (tuning wino_ws = 2: one workgroup per CU walking its
-    items as one chunk stream, MFMA waves holding all 16 positions) against fp64 conv2d and against
-    wino_kernel: bias + ReLU, no bias, the folded ReLU mask (zeros exactly where mask <= 0), padded
-    ldc columns untouched; shapes with 1-64 chunks per item and 1-4 items per workgroup (the stream
-    crossing item boundaries every chunk for Ci = 8)."""
-    g = torch.Generator().manual_seed(B * H * W + Ci + Co)
-    x = (torch.rand(B, H, W, Ci, generator=g) - 0.3).to(DEV)
-    w = (torch.randn(Co, Ci, 3, 3, generator=g) * (9 * Ci) ** -0.5).to(DEV)
-    bias = torch.randn(Co, generator=g).to(DEV)
-    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous()
-    u = ops.wino_weights(wp)
-    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
-    xn = x.permute(0, 3, 1, 2).double()
-    xp = F.pad(xn, (1, 1, 1, 1), mode="reflect") if pad_mode == "reflect" else F.pad(xn, (pad,) * 4)
-    mask = (torch.rand(B, Ho, Wo, ldc, generator=g) - 0.5).to(DEV)
-    for kw in (dict(bias=bias, relu=True), dict(bias=None, relu=False), dict(bias=bias, relu=False, relu_mask=mask)):
-        outs = []
-        for knob in (0, ws):
-            out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
-            with _lib.tuning(wino_ws=knob):
-                outs.append(ops.conv3x3_wino(x, u, kw["bias"], kw["relu"], pad_mode, pad, out=out,
-                                             relu_mask=kw.get("relu_mask")))
-        y = outs[1]
-        assert bool((y[..., Co:] == 7.0).all())
-        ref = F.conv2d(xp, w.double(), None if kw["bias"] is None else bias.double())
-        ref = torch.relu(ref) if kw["relu"] else ref
-        if "relu_mask" in kw:
-            keep = (mask[..., :Co] > 0).permute(0, 3, 1, 2)
-            ref = torch.where(keep, ref, torch.zeros_like(ref))
-            assert bool((y[..., :Co].permute(0, 3, 1, 2)[~keep] == 0).all())
-        assert rel(y[..., :Co].permute(0, 3, 1, 2), ref) < 2e-6, kw.keys()
-        assert rel(y, outs[0]) < 2e-6
 
 
 def test_conv3x3_wino_routing():
@@ -521,17 +430,12 @@ def _attn_ref(q, kv, fcs, mu, rstd, v_mu):
     return out * f + mm + v_mu.double()[:, None]
 
 
-# bf16 softmax attention variants (attn.hip): the fixed-shift kernels — "fsq" / "fsq1" (LDS-DMA on
-# 16x16x32 MFMAs; fsq1 takes the row sum from an all-ones MFMA; fsp = fsq1 persistent with a
-# continuous tile stream across query blocks), "fsg" (LDS-DMA; the default
-# when Ns % 128 == 0), "fsh" (half-tile pipelined, LDS-DMA), "fsE" (register staging, early loads),
-# "fs" (register staging; the default for ragged Ns) — and the online-max kernel "w8".
-# Variants that need whole 128-key tiles fall back to "fs" on ragged Ns.
-ATTN_VARIANTS = {"fsq": dict(attn_fixed_shift=1, attn_sched=6), "fsq1": dict(attn_fixed_shift=1, attn_sched=7),
-                 "fsp": dict(attn_fixed_shift=1, attn_sched=8),
-                 "fsh": dict(attn_fixed_shift=1, attn_sched=5), "fsg": dict(attn_fixed_shift=1, attn_sched=3),
-                 "fsE": dict(attn_fixed_shift=1, attn_sched=4), "fs": dict(attn_fixed_shift=1, attn_sched=0),
-                 "w8": dict(attn_fixed_shift=0)}
+# bf16 softmax attention kernels (attn.hip), each pinned to its wave count (tuning attn_waves) so the
+# named kernel runs whatever the grid size: "fsq1_8" / "fsq1_4" — the fixed-shift LDS-DMA kernel on
+# 16x16x32 MFMAs at 8 / 4 waves (Ns % 128 == 0; ragged Ns takes the register-staged fixed-shift kernel
+# "fs" at 8 waves and the online-max kernel at 4) — and the online-max kernel "w8" / "w4".
+ATTN_VARIANTS = {"fsq1_8": dict(attn_fixed_shift=1, attn_waves=8), "fsq1_4": dict(attn_fixed_shift=1, attn_waves=4),
+                 "w8": dict(attn_fixed_shift=0, attn_waves=8), "w4": dict(attn_fixed_shift=0, attn_waves=4)}
 
 
 @pytest.mark.parametrize("kernel", list(ATTN_VARIANTS))

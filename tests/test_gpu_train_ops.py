@@ -351,10 +351,11 @@ def test_linear_fn_fused_residual(M, K, N):
         assert rel(a, b_) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,W,C", [(2, 5, 7, 64), (3, 33, 20, 128), (1, 1, 2, 4), (2, 64, 64, 512), (8, 128, 128, 64)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 5, 7, 64), (3, 33, 20, 128), (1, 1, 2, 4), (2, 64, 64, 512), (8, 128, 128, 64),
+                                     (2, 1, 1, 8)])
 def test_feat_stats_vs_fp64(B, H, W, C):
     """mhada_feat_stats (the losses' per-channel mean / unbiased std and mse in one pass) against
-    fp64 torch on channels-last feature maps."""
+    fp64 torch on channels-last feature maps; a 1x1 map gives the unbiased std's NaN, as torch.std."""
     g = torch.Generator().manual_seed(B * H * W + C)
     x = (torch.rand(B, C, H, W, generator=g) * 3).to(DEV).contiguous(memory_format=torch.channels_last)
     t = (torch.rand(B, C, H, W, generator=g) * 3).to(DEV).contiguous(memory_format=torch.channels_last)
@@ -363,9 +364,12 @@ def test_feat_stats_vs_fp64(B, H, W, C):
     torch.testing.assert_close(mu.double(), xd.mean(dim=(2, 3)), rtol=1e-6, atol=1e-6)
     if H * W > 1:
         torch.testing.assert_close(sd.double(), xd.std(dim=(2, 3)), rtol=1e-5, atol=1e-6)
+    else:
+        assert bool(torch.isnan(sd).all()) and bool(torch.isnan(xd.std(dim=(2, 3))).all())
     torch.testing.assert_close(mse.double(), ((xd - td) ** 2).mean(), rtol=1e-6, atol=0)
     mu2, sd2, none = ops.feat_stats(x.permute(0, 2, 3, 1))
-    assert none is None and torch.equal(mu2, mu) and torch.equal(sd2, sd)
+    assert none is None and torch.equal(mu2, mu)
+    assert torch.equal(sd2, sd) if H * W > 1 else bool(torch.isnan(sd2).all())
     _, _, mse2 = ops.feat_stats(x.permute(0, 2, 3, 1), t.permute(0, 2, 3, 1), stats=False)
     assert torch.equal(mse2, mse)
 

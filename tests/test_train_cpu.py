@@ -71,8 +71,10 @@ def _dp_worker(rank, world, port, out_dir):
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = Trainer(*build(), distributed=True, bucket_mb=4)  # several buckets
-    c = seeded_image(1, 64, 64, 200 + rank)
-    s = seeded_image(1, 64, 64, 300 + rank)
+    # a micro-batch of TWO images per rank: the batch-axis ViT attention couples
+    # them inside the rank's forward call, never across ranks
+    c = seeded_image(2, 64, 64, 200 + rank)
+    s = seeded_image(2, 64, 64, 300 + rank)
     tr.backward(c, s)
     if rank == 0:
         grads = {n: p.grad.clone() for n, p in tr.ada.named_parameters()}
@@ -89,22 +91,35 @@ def _dp_worker(rank, world, port, out_dir):
 
 
 def test_data_parallel_allreduce_equals_accumulation(tmp_path):
-    """2 gloo ranks, one image each == single process averaging the two micro-batch gradients."""
+    """2 gloo ranks with 2 images each == one process averaging the gradients of the two B = 2
+    micro-batch calls (train_image.py:103-110,139-144).  Control: splitting each
+    micro-batch into single-image calls (batch-axis attention uncoupled) gives different
+    gradients, so the comparison does see the coupling."""
     world = 2
     mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     dp = torch.load(tmp_path / "dp_grads.pt", weights_only=True)
     torch.set_num_threads(2)  # same intra-op split as the workers: same summation order
     tr = Trainer(*build(), distributed=False)
-    acc = {}
-    for r in range(world):
-        tr.backward(seeded_image(1, 64, 64, 200 + r), seeded_image(1, 64, 64, 300 + r))
-        named = dict(("vit_c." + n, p) for n, p in tr.vit_c.named_parameters())
-        named.update(dict(tr.ada.named_parameters()))
-        for n, p in named.items():
-            acc[n] = acc.get(n, 0) + p.grad / world
+    def accumulate(calls):
+        acc = {}
+        for c, s in calls:
+            tr.backward(c, s)
+            named = dict(("vit_c." + n, p) for n, p in tr.vit_c.named_parameters())
+            named.update(dict(tr.ada.named_parameters()))
+            for n, p in named.items():
+                acc[n] = acc.get(n, 0) + p.grad / len(calls)
+        return acc
+
+    micro = [(seeded_image(2, 64, 64, 200 + r), seeded_image(2, 64, 64, 300 + r)) for r in range(world)]
+    acc = accumulate(micro)
+    single = accumulate([(c[i:i + 1], s[i:i + 1]) for c, s in micro for i in range(2)])
     torch.set_num_threads(8)
     for n, g in acc.items():
         torch.testing.assert_close(dp[n], g, rtol=1e-4, atol=1e-5 * float(g.abs().max()))
+    # the ViT's attention weights see the coupling: per-image calls move their gradient by far more
+    # than the DP tolerance
+    qkv = "vit_c.encoder.0.attention.in_proj_weight"
+    assert float((single[qkv] - acc[qkv]).norm()) > 1e-2 * float(acc[qkv].norm())
     for r in range(world):
         agree = torch.load(tmp_path / f"agree_{r}.pt", weights_only=True)
         assert agree["identical"] and agree["backend"] == "gloo" and agree["world"] == world, agree

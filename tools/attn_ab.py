@@ -17,13 +17,9 @@ SHAPES = [("1024^2 B4", 4, 16384, 16384), ("512^2 B8", 8, 4096, 4096), ("video 1
           ("ragged", 2, 1000, 777)]
 
 
-VARIANTS = {"fs": {"attn_fixed_shift": 1, "attn_tk": 128, "attn_sched": 0, "attn_prio": 1},
-            "fsh": {"attn_fixed_shift": 1, "attn_sched": 5, "attn_prio": 1},
-            "fsq1P0": {"attn_fixed_shift": 1, "attn_sched": 7, "attn_prio": 0},
-            "fsg": {"attn_fixed_shift": 1, "attn_sched": 3},
-            "fsq1": {"attn_fixed_shift": 1, "attn_sched": 7},
-            "fsp": {"attn_fixed_shift": 1, "attn_sched": 8},
-            "w8": {"attn_fixed_shift": 0, "attn_tk": 128, "attn_sched": 0}}
+VARIANTS = {"fsq1P0": {"attn_fixed_shift": 1, "attn_prio": 0},
+            "fsq1": {"attn_fixed_shift": 1, "attn_prio": 1},
+            "w8": {"attn_fixed_shift": 0, "attn_tk": 128}}
 
 
 def run(variant, args):

@@ -22,9 +22,7 @@ import torch
 
 from mhada_hip import _lib, ops
 
-VARIANTS = {"fsg": {"attn_fixed_shift": 1, "attn_sched": 3}, "fsh": {"attn_fixed_shift": 1, "attn_sched": 5},
-            "fsq": {"attn_fixed_shift": 1, "attn_sched": 6}, "fsq1": {"attn_fixed_shift": 1, "attn_sched": 7},
-            "fsp": {"attn_fixed_shift": 1, "attn_sched": 8}}
+VARIANTS = {"fsq1": {"attn_fixed_shift": 1}}
 
 
 def train_dkv(lib):

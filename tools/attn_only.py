@@ -1,15 +1,13 @@
 """Run only the bf16 (or fp32) MHAda attention kernel a few times (for rocprofv3 PMC passes).
 
-    python tools/attn_only.py [bf16|f32] [variant: fsg fsh fsq fsq1 fs w8]"""
+    python tools/attn_only.py [bf16|f32] [variant: fsq1 w8]"""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd")]
 import torch
 from mhada_hip import _lib, ops
 
-VARIANTS = {"fsg": dict(attn_fixed_shift=1, attn_sched=3), "fsh": dict(attn_fixed_shift=1, attn_sched=5),
-            "fsq": dict(attn_fixed_shift=1, attn_sched=6), "fsq1": dict(attn_fixed_shift=1, attn_sched=7), "fsp": dict(attn_fixed_shift=1, attn_sched=8),
-            "fs": dict(attn_fixed_shift=1, attn_sched=0), "w8": dict(attn_fixed_shift=0)}
+VARIANTS = {"fsq1": dict(attn_fixed_shift=1), "w8": dict(attn_fixed_shift=0)}
 if len(sys.argv) > 2:
     for k, v in VARIANTS[sys.argv[2]].items():
         _lib.set_tuning(k, v)

@@ -1,6 +1,6 @@
 """Ablation timing of the Winograd conv kernel: builds of wino.hip with -DWINO_DBG=<bits> (1 no
 MFMA, 2 no global loads, 4 no transform / LDS stores) linked as build_dbg/libwino_<bits>.so,
-timed on one shape, for each value of the tuning knob WINO_KNOB (default wino_ws: 0 and 1).
+timed on one shape, for each value of the tuning knob WINO_KNOB (default xknob: 0 and 1).
 usage: python tools/wino_dbg.py B H Ci Co [bits ...]   (WINO_LIB_DIR: directory of the builds)"""
 import ctypes, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,7 +23,7 @@ for v in bits:
     assert lib.mhada_wino_weights(w.data_ptr(), u.data_ptr(), Co, Ci, st) == 0
     f = lambda: lib.mhada_conv3x3_wino(x.data_ptr(), u.data_ptr(), None, y.data_ptr(), B, H, H, Ci, Co, Co, 0, 1, 1, None, st)  # noqa
     for kv in [int(v) for v in os.environ.get("WINO_KNOB_VALS", "0,1").split(",")]:
-        assert lib.mhada_set_tuning(os.environ.get("WINO_KNOB", "wino_ws").encode(), kv) == 0
+        assert lib.mhada_set_tuning(os.environ.get("WINO_KNOB", "xknob").encode(), kv) == 0
         f(); torch.cuda.synchronize()
         ts = []
         for _ in range(15):

@@ -1,7 +1,7 @@
 """fp32 Winograd conv tuning knobs A/B in one process (interleaved rounds, median), at the 512^2 B8
 decoder / VGG19 / dgrad shapes.
-    python tools/wino_knob_ab.py <knob> [iters]                  (knob = 0 vs 1, e.g. wino_l2pf)
-    python tools/wino_knob_ab.py -c wino_ws=0,xknob=0 -c wino_ws=1 ... [iters]   (any settings)"""
+    python tools/wino_knob_ab.py <knob> [iters]                  (knob = 0 vs 1, e.g. xknob)
+    python tools/wino_knob_ab.py -c xknob=0 -c xknob=1 ... [iters]   (any settings)"""
 import os
 import sys
 

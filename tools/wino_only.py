@@ -1,5 +1,5 @@
 """The fp32 Winograd conv alone on one shape, a few launches (a target for rocprofv3 PMC passes).
-    python tools/wino_only.py <wino_ws: 0|1> [B H Ci Co]   (default 8 128 256 256)"""
+    python tools/wino_only.py [B H Ci Co]   (default 8 128 256 256)"""
 import os
 import sys
 
@@ -9,8 +9,7 @@ import torch
 
 from mhada_hip import _lib, ops
 
-_lib.set_tuning("wino_ws", int(sys.argv[1]))
-B, H, Ci, Co = map(int, sys.argv[2:6]) if len(sys.argv) > 5 else (8, 128, 256, 256)
+B, H, Ci, Co = map(int, sys.argv[1:5]) if len(sys.argv) > 4 else (8, 128, 256, 256)
 x = torch.rand(B, H, H, Ci, device="cuda")
 w = torch.randn(Co, 9 * Ci, device="cuda") / (9 * Ci) ** 0.5
 u = ops.wino_weights(w)
