@@ -115,7 +115,7 @@ def pmc_traffic(cfg_key):
     return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
-def shader_clock(launches: int = 20, iters: int = 300000) -> float:
+def shader_clock(launches: int = 20, iters: int = 150000) -> float:
     """The box's sustained shader clock under dense bf16 MFMA load, in GHz, measured in THIS process
     right after a timed region (mhada_clock_probe, csrc/probe.hip: s_memtime / s_memrealtime around a
     dependent MFMA chain per workgroup, ~10 ms per launch, `launches` back to back; median over the

@@ -57,8 +57,8 @@ const char* mhada_last_error(void);
 int mhada_set_tuning(const char* name, int value);
 int mhada_get_tuning(const char* name, int* value);
 
-/* Sustained shader-clock probe (ABI 13; probe.hip): nblk workgroups of 4 waves each run a dependent
- * v_mfma_f32_16x16x32_bf16 chain of 4 * iters MFMAs per wave on non-trivial operands; workgroup b
+/* Sustained shader-clock probe (ABI 13; probe.hip): nblk workgroups of 8 waves each run 4 * iters
+ * v_mfma_f32_16x16x32_bf16 per wave on pseudo-random operands read from LDS; workgroup b
  * writes stamps[2b] = shader-clock ticks (s_memtime) and stamps[2b + 1] = 100 MHz ticks
  * (s_memrealtime) spent in the chain (device buffer of 2 * nblk).  clock = stamps[2b] /
  * stamps[2b + 1] * 100 MHz.  bench.py runs it after each timed region so a box's clock under dense

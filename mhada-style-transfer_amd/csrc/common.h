@@ -43,6 +43,7 @@ struct Tuning {
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
+  int gemm_f32w = 0;         // fp32 GEMM (ROWS A, N > 128): 4-wave one-wave-per-SIMD 256x256 kernel (0: ping-pong)
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };
@@ -66,6 +67,14 @@ template <> MHADA_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
 template <typename T> struct Vec16;
 template <> struct Vec16<float> { typedef f32x4 type; static constexpr int N = 4; };
 template <> struct Vec16<bf16> { typedef bf16x8 type; static constexpr int N = 8; };
+
+// Bilinear blend in PyTorch's order, h0 * (w0 * x00 + w1 * x01) + h1 * (w0 * x10 + w1 * x11), with the
+// fp32 contraction pinned (explicit fmaf), so every kernel that upsamples — the standalone
+// upsample kernels, the conv tile kernel's fused halo and the implicit GEMM's UP2 gather —
+// produces the same bits.
+MHADA_DEV float bilerp(float ly0, float ly1, float lx0, float lx1, float x00, float x01, float x10, float x11) {
+  return fmaf(ly1, fmaf(lx0, x10, lx1 * x11), ly0 * fmaf(lx0, x00, lx1 * x01));
+}
 
 MHADA_DEV float wave_sum(float v) {
 #pragma unroll

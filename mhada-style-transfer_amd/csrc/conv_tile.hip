@@ -162,8 +162,8 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_c64_kernel(const ConvTileP p) 
               bf16x8 o;
 #pragma unroll
               for (int e = 0; e < 8; ++e)
-                o[e] = (bf16)(ly0 * (lx0 * v[ey][ex][e] + lx1 * v[ey][ex + 1][e]) +
-                              ly1 * (lx0 * v[ey + 1][ex][e] + lx1 * v[ey + 1][ex + 1][e]));
+                o[e] = (bf16)bilerp(ly0, ly1, lx0, lx1, v[ey][ex][e], v[ey][ex + 1][e], v[ey + 1][ex][e],
+                                    v[ey + 1][ex + 1][e]);
               *reinterpret_cast<bf16x8*>(sX + swz(hy * kHW + hx, c)) = o;
             }
           }
@@ -188,8 +188,7 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_c64_kernel(const ConvTileP p) 
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          o[e] = (bf16)(ly0 * (lx0 * (float)a00[e] + lx1 * (float)a01[e]) +
-                        ly1 * (lx0 * (float)a10[e] + lx1 * (float)a11[e]));
+          o[e] = (bf16)bilerp(ly0, ly1, lx0, lx1, (float)a00[e], (float)a01[e], (float)a10[e], (float)a11[e]);
         *reinterpret_cast<bf16x8*>(sX + swz(px, c)) = o;
       }
     } else {

@@ -2,8 +2,8 @@
 // clock it holds differs between boxes (MI355X_MICROARCH.md, DVFS give-back items 5-7), so a bench
 // number alone cannot tell a code change from a box change.  bench.py runs this kernel right after
 // each timed region, in the same process: every workgroup keeps each SIMD's matrix pipe busy with
-// a dependent chain of v_mfma_f32_16x16x32_bf16 on non-trivial operands (zero operands run at a
-// higher clock, item 7) and stamps s_memtime (shader clock) and s_memrealtime (constant 100 MHz)
+// v_mfma_f32_16x16x32_bf16 on pseudo-random operands re-read from LDS every iteration (zero or
+// constant operands run at a higher clock, item 7), two waves per SIMD and stamps s_memtime (shader clock) and s_memrealtime (constant 100 MHz)
 // around the chain; clock = d(memtime) / d(memrealtime) * 100 MHz per workgroup.  The stamps go to
 // their own device buffer with vector stores; no output of any other kernel depends on them.
 // No reference counterpart (the reference has no kernels; its only timer is infer_time.py:64-87).
@@ -12,17 +12,18 @@
 namespace mhada {
 namespace {
 
-__global__ void __launch_bounds__(256) clock_probe_kernel(unsigned long long* __restrict__ stamps, int iters) {
+__global__ void __launch_bounds__(512) clock_probe_kernel(unsigned long long* __restrict__ stamps, int iters) {
+  // 32 KiB of pseudo-random bf16 in [-1, 1) in LDS; every wave re-reads its operands from it each
+  // iteration at a rotating offset, so the MFMA inputs change like a real kernel's (constant
+  // register operands run the matrix pipe at a higher clock than any kernel of this library)
+  __shared__ __attribute__((aligned(16))) bf16 lds[16384];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // pseudo-random bf16 operands in [-1, 1) per lane (a hash of the lane and wave)
-  bf16x8 a, b;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    unsigned h = (unsigned)(lane * 8 + j + 1) * 2654435761u ^ (unsigned)(wave + 1) * 40503u;
+  for (int i = threadIdx.x; i < 16384; i += 512) {
+    unsigned h = (unsigned)(i + 1) * 2654435761u ^ (unsigned)(blockIdx.x + 1) * 40503u;
     h ^= h >> 13;
     h *= 0x5bd1e995u;
-    a[j] = (bf16)((float)(h & 0xffff) / 32768.f - 1.f);
-    b[j] = (bf16)((float)(h >> 16) / 32768.f - 1.f);
+    h ^= h >> 15;
+    lds[i] = (bf16)((float)(h & 0xffff) / 32768.f - 1.f);
   }
   f32x4 acc[4];
 #pragma unroll
@@ -30,9 +31,13 @@ __global__ void __launch_bounds__(256) clock_probe_kernel(unsigned long long* __
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  int off = (wave * 1024 + lane * 8) & 16383;
   for (int it = 0; it < iters; ++it) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + off);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(lds + ((off + 4096) & 16383));
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+    off = (off + 512) & 16383;
   }
   __syncthreads();
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -53,6 +58,6 @@ using namespace mhada;
 
 extern "C" int mhada_clock_probe(unsigned long long* stamps, int nblk, int iters, mhada_stream_t s_) {
   if (!stamps || nblk <= 0 || iters <= 0) return fail("mhada_clock_probe: bad args");
-  hipLaunchKernelGGL(clock_probe_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)s_, stamps, iters);
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(nblk), dim3(512), 0, (hipStream_t)s_, stamps, iters);
   return check_launch("mhada_clock_probe");
 }

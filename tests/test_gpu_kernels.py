@@ -55,26 +55,38 @@ def test_linear(cdt, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(70000, 1024, 64), (70000, 768, 512), (32400, 512, 2048), (57000, 600, 96),
                                    (65536, 2048, 512)])
-def test_gemm_f32_persistent_epilogues(M, N, K):
-    """The fp32 persistent ping-pong GEMM: bias / ReLU / residual (preloaded into the
-    accumulators) / bf16 copy outputs against fp64 on every row tile (last partial), several tiles
-    per CU, 2 to 64 K-tiles, partial column tiles; a second run is bit-identical."""
+@pytest.mark.parametrize("f32w", [0, 1, 2])
+def test_gemm_f32_persistent_epilogues(M, N, K, f32w):
+    """The fp32 persistent GEMMs — the ping-pong kernel (f32w = 0) and the one-wave-per-SIMD kernel
+    (tuning gemm_f32w = 1): bias / ReLU / residual / bf16 copy outputs against fp64 on every row
+    tile (last partial), several tiles per CU, 2 to 64 K-tiles, partial column tiles; a second run
+    is bit-identical, and without a residual the two kernels agree bit for bit (same k order)."""
     x = rnd(M, K, seed=1)
     w = rnd(N, K, scale=K ** -0.5, seed=2)
     b = rnd(N, seed=3)
     r = rnd(M, N, seed=4)
-    outs = []
-    for _ in range(2):
+
+    def run():
         c2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         y0 = torch.empty(M, N, device=DEV)
         ops.gemm(a=x, w=w, c=y0, M=M, N=N, K=K, compute=torch.float32, lda=K, ldw=K, bias=b, ldc=N,
                  c2=c2, ldc2=N)
-        outs.append((ops.linear(x, w, b, torch.float32, residual=r),
-                     ops.linear(x, w, b, torch.float32, relu=True),
-                     ops.linear(x, w, None, torch.float32), y0, c2))
+        out = (ops.linear(x, w, b, torch.float32, residual=r),
+               ops.linear(x, w, b, torch.float32, relu=True),
+               ops.linear(x, w, None, torch.float32), y0, c2)
         torch.cuda.synchronize()
+        return out
+
+    with _lib.tuning(gemm_f32w=f32w):
+        outs = [run(), run()]
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
+    if f32w:
+        with _lib.tuning(gemm_f32w=0):
+            pp = run()
+        for a, c in zip(outs[0][1:], pp[1:]):
+            assert torch.equal(a, c)
+        assert rel(outs[0][0], pp[0]) < 4e-6  # bias + residual after the products vs before them
     res, rl, plain, y0, c2 = outs[0]
     assert rel(c2, y0) < 4e-3
     rows = torch.cat([torch.arange(0, M, 997), torch.arange(M - 300, M)]).to(DEV)
@@ -262,12 +274,19 @@ def test_conv3x3_c64_tile(up, B, H, W):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128)])
+@pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128), (1, 3, 8), (3, 1, 16)])
 def test_upsample2x(dt, H, W, C):
+    """The 2 x 2-block kernel (16-B aligned operands) against fp64 F.interpolate, and bit-identical to
+    the per-pixel kernel (which a misaligned view of the same values takes)."""
     x = rnd(2, H, W, C, seed=H).to(dt)
     y = ops.upsample2x(x)
     ref = F.interpolate(x.permute(0, 3, 1, 2).double(), scale_factor=2, mode="bilinear", align_corners=False)
     assert rel(y.permute(0, 3, 1, 2), ref) < (1e-6 if dt == torch.float32 else 5e-3)
+    buf = torch.empty(x.numel() + 1, device=DEV, dtype=dt)
+    xm = buf[1:].view(x.shape)  # 2 or 4 bytes past a 16-B boundary
+    xm.copy_(x)
+    assert xm.data_ptr() % 16 != 0
+    assert torch.equal(ops.upsample2x(xm), y)
 
 
 @pytest.mark.parametrize("dt,mfma", [(torch.float32, "1"), (torch.float32, "0"), (torch.bfloat16, "1"),

@@ -67,12 +67,8 @@ def gemm_suite(dts=(torch.bfloat16, torch.float32)):
             else:
                 fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
-                fns["f32b"] = lambda: with_env("MHADA_GEMM_F32B", "1", ops.linear, x, w, b, out, residual=r,
+                fns["f32w"] = lambda: with_env("MHADA_GEMM_F32W", "1", ops.linear, x, w, b, out, residual=r,
                                                relu=relu)
-                fns["pp2"] = lambda: with_env("MHADA_GEMM_F32B", "2", ops.linear, x, w, b, out, residual=r,
-                                              relu=relu)
-                fns["pp128"] = lambda: with_env("MHADA_GEMM_F32B", "3", ops.linear, x, w, b, out, residual=r,
-                                                relu=relu)
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
@@ -110,6 +106,25 @@ def gemm_k_suite():
               "no_rinit": M * K * 2 + 2 * M * N * 4}
         print(f"gemmR bf16 M={M} N={N} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {by[k] / v / 1e6:7.1f} GB/s"
                                                              for k, v in t.items()))
+
+
+def gemm_k32_suite():
+    """fp32 main-loop rate vs K for the ping-pong and the one-wave-per-SIMD kernels: the slope
+    separates the K-loop rate from the fixed per-tile prologue / epilogue cost."""
+    dev = "cuda"
+    M = 32768
+    for N in (512, 1536):
+        for K in (512, 1024, 2048, 4096):
+            x = torch.randn(M, K, device=dev)
+            w = torch.randn(N, K, device=dev) / K ** 0.5
+            b = torch.randn(N, device=dev)
+            t = bench({"pp": lambda: ops.linear(x, w, b, torch.float32),
+                       "f32w": lambda: with_env("MHADA_GEMM_F32W", "1", ops.linear, x, w, b, torch.float32),
+                       "f32wr": lambda: with_env("MHADA_GEMM_F32W", "2", ops.linear, x, w, b, torch.float32),
+                       "torch": lambda: torch.addmm(b, x, w.t())})
+            fl = 2 * M * N * K
+            print(f"gemmK f32 M={M} N={N:5d} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF"
+                                                                  for k, v in t.items()))
 
 
 def out3_suite():
@@ -239,6 +254,8 @@ if __name__ == "__main__":
         gemm_suite((torch.float32,))
     if what in ("gemmk",):
         gemm_k_suite()
+    if what == "gemmk32":
+        gemm_k32_suite()
     if what in ("n64",):
         n64_suite()
     if what == "proj":
