@@ -40,7 +40,7 @@ const Knob kKnobs[] = {
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
     {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
     {"tn_skinny_lds", &Tuning::tn_skinny_lds},       {"train_dkv_dma", &Tuning::train_dkv_dma},
-    {"gemm_f32w", &Tuning::gemm_f32w},               {"xknob", &Tuning::xknob},
+    {"loss_q16", &Tuning::loss_q16},                 {"xknob", &Tuning::xknob},
 };
 
 Tuning g_tuning;
@@ -61,7 +61,6 @@ bool valid(const char* name, int v) {
   if (!strcmp(name, "attn_tk")) return v == 64 || v == 128;
   if (!strcmp(name, "gemm_n64")) return v == 128 || v == 256;
   if (!strcmp(name, "xknob")) return v >= 0 && v < 16;
-  if (!strcmp(name, "gemm_f32w")) return v >= 0 && v <= 2;
   return v == 0 || v == 1;
 }
 }  // namespace

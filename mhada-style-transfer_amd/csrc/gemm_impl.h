@@ -1286,205 +1286,6 @@ __global__ void __launch_bounds__(BM * 2) gemm_n64_kernel(const GemmP p) {
   store_tile<float, 1, 2>(p, acc, z1, z2, m0 + 32 * wave + r32, 0, h);
 }
 
-// ------------------------------------------------------------------------------------
-// fp32 GEMM, one wave per SIMD (round 5; tuning gemm_f32w, ROWS A only).  hipBLASLt's fp32 kernel
-// for these shapes is a 4-wave 256x256 tile (profiles/r04_hipblaslt_f32_kernels.txt); the
-// ping-pong kernel above hands the MFMA pipe between its two wave groups 8 times per 32-deep
-// K-tile, and its K-loop measured ~88 % of the fp32 peak against hipBLASLt's ~95 % (MLP2 at
-// 512^2 B8, one tile per CU: 521 vs 471 us).  Here 4 waves each own a 128x128 quarter of the
-// 256x256 tile: 4 x 4 blocks of v_mfma_f32_32x32x2_f32 = 256 accumulator registers (the AGPR
-// half of the 512-register file, launch_bounds(256, 1)), so a wave issues 256 independent MFMAs
-// (16384 matrix cycles) per K-tile against 32 ds_read_b128 and 16 LDS-DMA pieces — ONE barrier
-// per K-tile, no hand-over.  Staging: the ping-pong kernel's 128-B rows with chunk c of row r at
-// slot c ^ ((r >> 1) & 7) (applied on the DMA source: conflict-free ds_read_b128), a 2-slot ring
-// of [A 256 x 32 | W 256 x 32] fp32 (64 KiB per slot), K-tile g+1 staged during K-tile g; the next
-// tile's K-tile 0 is staged during the last K-tile of this one (persistent: tiles w, w + G, ..).
-// The per-accumulator k order is the ping-pong kernel's (chunk q = 0..3 of lane half h, element
-// e); the bias and residual are added in the epilogue (after the products, where the ping-pong
-// kernel's rinit starts from them), so results agree with it to fp32 summation order.
-// ------------------------------------------------------------------------------------
-// REG (tuning gemm_f32w = 2): the next K-tile staged through registers (16 global_load_dwordx4 per
-// wave at the K-tile's start, ds_write_b128 into the free slot after its MFMAs) instead of LDS-DMA,
-// as hipBLASLt's kernel does (its name carries no DirectToLds): same LDS image, same results.
-template <typename TO, bool REG>
-__global__ void __launch_bounds__(256, 1) gemm_f32w_kernel(const GemmP p, int total) {
-  constexpr int BK = 32, ROWS = 256, TILE = 2 * ROWS * BK;  // floats per slot: A rows | W rows
-  constexpr int SCR = 4 * 1024;                              // epilogue scratch: 4 KiB per wave
-  __shared__ __attribute__((aligned(16))) float smem[2 * TILE + SCR];  // 144 KiB, the only LDS object
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int G = gridDim.x;
-  // staging: piece i of this wave covers rows 64 * wave + 8 i + (lane >> 3) of A (and of W), 16-B
-  // chunk slot lane & 7, whose source chunk is (lane & 7) ^ ((row >> 1) & 7)
-  const int srow = 64 * wave + (lane >> 3);
-  // source chunk offset of piece i: odd pieces flip bit 2 of (row >> 1) & 7 (row bit 3)
-  const int sch0 = 4 * ((lane & 7) ^ ((srow >> 1) & 7)), sch1 = sch0 ^ 16;
-  // tile state: wave-uniform scalars only (per-lane staging offsets are recomputed per K-tile)
-  struct St {
-    int m0, n0, z1, z2;
-  };
-  auto setup = [&](int w, St& s) {
-    const int lg = xcd_remap(w, total);
-    const int z = lg / p.ntiles, t = lg - z * p.ntiles;
-    s.z1 = z / p.nb2;
-    s.z2 = z - s.z1 * p.nb2;
-    const int tm = t / p.tiles_n, tn = t - tm * p.tiles_n;
-    s.m0 = tm * 256;
-    s.n0 = tn * 256;
-  };
-  // LDS-DMA piece i (0-7: A rows, 8-15: W rows) of K-tile kt of tile s into slot `slot`
-  auto piece = [&](const St& s, int kt, int slot, int i) __attribute__((always_inline)) {
-    float* dst = smem + slot * TILE + 64 * wave * BK + (i >> 3) * ROWS * BK + 8 * (i & 7) * BK;
-    if (i < 8) {
-      const float* ab = reinterpret_cast<const float*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
-      const int m = min(s.m0 + srow + 8 * i, p.M - 1);
-      glds16(ab + ((unsigned)(m * (unsigned)p.lda) + (i & 1 ? sch1 : sch0)), dst);
-    } else {
-      const float* wb = reinterpret_cast<const float*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
-      const int n = min(s.n0 + srow + 8 * (i & 7), p.N - 1);
-      glds16(wb + ((unsigned)(n * (unsigned)p.ldw) + (i & 1 ? sch1 : sch0)), dst);
-    }
-  };
-  auto stage = [&](const St& s, int kt, int slot) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) piece(s, kt, slot, i);
-  };
-  // register staging (REG): the same pieces as plain 16-B loads and LDS writes
-  auto piece_src = [&](const St& s, int kt, int i) __attribute__((always_inline)) {
-    if (i < 8) {
-      const float* ab = reinterpret_cast<const float*>(p.a) + s.z1 * p.sa1 + s.z2 * p.sa2 + kt * BK;
-      const int m = min(s.m0 + srow + 8 * i, p.M - 1);
-      return ab + ((unsigned)(m * (unsigned)p.lda) + (i & 1 ? sch1 : sch0));
-    }
-    const float* wb = reinterpret_cast<const float*>(p.w) + s.z1 * p.sw1 + s.z2 * p.sw2 + kt * BK;
-    const int n = min(s.n0 + srow + 8 * (i & 7), p.N - 1);
-    return wb + ((unsigned)(n * (unsigned)p.ldw) + (i & 1 ? sch1 : sch0));
-  };
-  auto piece_dst = [&](int slot, int i) __attribute__((always_inline)) {
-    return smem + slot * TILE + 64 * wave * BK + (i >> 3) * ROWS * BK + 8 * (i & 7) * BK + 4 * lane;
-  };
-  const int swz = (r32 >> 1) & 7;
-  int koff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) koff[q] = 4 * ((4 * h + q) ^ swz);
-  f32x16 acc[4][4];
-  // one K-tile from slot `slot`: chunk q of each lane half (k = 16 h + 4 q + e), fragments of chunk
-  // q + 1 read while chunk q's 64 MFMAs run
-  auto compute = [&](int slot, const St& ns, int nkt, auto dma_c) {
-    constexpr bool dma = decltype(dma_c)::value;
-    const float* sA = smem + slot * TILE + (128 * wr + r32) * BK;
-    const float* sW = smem + slot * TILE + ROWS * BK + (128 * wc + r32) * BK;
-    f32x4 af[2][4], wf[2][4];
-    f32x4 stg[REG ? 16 : 1];
-    if constexpr (REG && dma) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) stg[i] = *reinterpret_cast<const f32x4*>(piece_src(ns, nkt, i));
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      af[0][t] = *reinterpret_cast<const f32x4*>(sA + 32 * t * BK + koff[0]);
-      wf[0][t] = *reinterpret_cast<const f32x4*>(sW + 32 * t * BK + koff[0]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = q & 1;
-      // 4 of the 16 LDS-DMA pieces of the next K-tile per chunk step (one wave per SIMD: a burst of
-      // 16 pieces would hold the matrix pipe for their whole issue time)
-      if constexpr (dma && !REG) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) piece(ns, nkt, slot ^ 1, 4 * q + i);
-      }
-      if constexpr (dma && REG) {
-        if (q == 3) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(piece_dst(slot ^ 1, i)) = stg[i];
-        }
-      }
-      if (q < 3) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          af[c ^ 1][t] = *reinterpret_cast<const f32x4*>(sA + 32 * t * BK + koff[q + 1]);
-          wf[c ^ 1][t] = *reinterpret_cast<const f32x4*>(sW + 32 * t * BK + koff[q + 1]);
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[c][nt][e], af[c][mt][e], acc[mt][nt], 0, 0, 0);
-      // interleave: each DMA piece and pair of fragment reads ahead of 16 MFMAs
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (dma && !REG) __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);  // VMEM (LDS-DMA piece)
-        if constexpr (dma && REG) {
-          if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);  // VMEM read (staging loads)
-          if (q == 3) __builtin_amdgcn_sched_group_barrier(0x0200, 4, 0);  // DS write (staging)
-        }
-        if (q < 3) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x0008, 16, 0);           // MFMA
-      }
-    }
-  };
-
-  const int KT = p.K / BK;
-  int w = blockIdx.x;
-  St cur, nxt;
-  setup(w, cur);
-  bool has_nxt = w + G < total;
-  if (has_nxt) setup(w + G, nxt);
-  int slot = 0;
-  if constexpr (REG) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(piece_dst(0, i)) = *reinterpret_cast<const f32x4*>(piece_src(cur, 0, i));
-  } else {
-    stage(cur, 0, 0);
-  }
-  bool first_tile = true;
-  while (true) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-    for (int kt = 0; kt < KT; ++kt) {
-      // this wave's DMA of K-tile kt has landed.  The previous tile's epilogue stores were issued
-      // after it: at most 63 of them may stay in flight (vmcnt counts stores, in issue order)
-      // (REG: the loads were consumed by the LDS writes; the compiler's waits cover them)
-      if constexpr (!REG) {
-        if (kt == 0 && !first_tile) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      PP_LGKM0();
-      PP_BARRIER();  // K-tile kt visible to every wave; every wave is done with the other slot
-      // the next K-tile's DMA (this tile's kt + 1, or the next tile's K-tile 0) inside the MFMAs
-      // (after the last tile: a harmless re-fetch of this tile's K-tile 0 into the free slot)
-      const bool in_tile = kt + 1 < KT;
-      St ns;
-      ns.m0 = in_tile || !has_nxt ? cur.m0 : nxt.m0;
-      ns.n0 = in_tile || !has_nxt ? cur.n0 : nxt.n0;
-      ns.z1 = in_tile || !has_nxt ? cur.z1 : nxt.z1;
-      ns.z2 = in_tile || !has_nxt ? cur.z2 : nxt.z2;
-      compute(slot, ns, in_tile ? kt + 1 : 0, std::true_type{});
-      slot ^= 1;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // epilogue (bias, ReLU, residual, bf16 copy) through this wave's LDS scratch
-    float* scr = smem + 2 * TILE + wave * 1024;
-    store_tile_lds<TO, 4, 4>(p, acc, cur.z1, cur.z2, cur.m0 + 128 * wr, cur.n0 + 128 * wc, lane, scr);
-    if (!has_nxt) break;
-    cur = nxt;
-    w += G;
-    has_nxt = w + G < total;
-    if (has_nxt) setup(w + G, nxt);
-    first_tile = false;
-  }
-}
-
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 static int num_cus() {
@@ -1522,23 +1323,6 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
     return check_launch("mhada_gemm");
   }
   return fail("mhada_gemm: no ping-pong form");
-}
-
-template <typename TO>
-static int launch_gemm_f32w(const GemmP& p0, int nz, hipStream_t stream) {
-  GemmP p = p0;
-  p.tiles_n = (p.N + 255) / 256;
-  p.ntiles = ((p.M + 255) / 256) * p.tiles_n;
-  p.lds_epi = 1;
-  p.rinit = 0;  // the residual is added in the epilogue
-  const long long total = (long long)p.ntiles * nz;
-  if (total >= (1LL << 31)) return fail("mhada_gemm: too many tiles");
-  const int grid = (int)std::min<long long>(total, num_cus());
-  if (tuning().gemm_f32w == 2)
-    hipLaunchKernelGGL((gemm_f32w_kernel<TO, true>), dim3(grid), dim3(256), 0, stream, p, (int)total);
-  else
-    hipLaunchKernelGGL((gemm_f32w_kernel<TO, false>), dim3(grid), dim3(256), 0, stream, p, (int)total);
-  return check_launch("mhada_gemm");
 }
 
 // The ping-pong kernel takes bf16 A (rows or 3x3 taps) with K % 64 == 0, N > 128 and operand
@@ -1631,11 +1415,6 @@ static int dispatch_tile(const GemmP& p, int nz, hipStream_t s) {
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * nz;
       if (p.N > 128 && p.K % 32 == 0 && p.K >= 64 && 8 * t256 >= 7LL * num_cus() && pp_enabled() && persist_enabled() &&
           pp_offsets_fit(p, AMODE)) {
-        if constexpr (AMODE == MHADA_A_ROWS) {
-          if (tuning().gemm_f32w && p.lda % 4 == 0 && p.ldw % 4 == 0 && p.sa1 % 4 == 0 && p.sa2 % 4 == 0 &&
-              p.sw1 % 4 == 0 && p.sw2 % 4 == 0 && aligned16(p.a) && aligned16(p.w))
-            return launch_gemm_f32w<TO>(p, nz, s);
-        }
         return launch_gemm_pp<float, TO, AMODE>(p, nz, s);
       }
       // (the 256x128 form measured 2-4 % slower than the 128x128 kernel in fp32: bf16 only)

@@ -67,8 +67,7 @@ def gemm_suite(dts=(torch.bfloat16, torch.float32)):
             else:
                 fns["tile128"] = lambda: with_env("MHADA_GEMM_PP", "0", ops.linear, x, w, b, out, residual=r,
                                                   relu=relu)
-                fns["f32w"] = lambda: with_env("MHADA_GEMM_F32W", "1", ops.linear, x, w, b, out, residual=r,
-                                               relu=relu)
+
             t = bench(fns)
             fl = 2 * M * N * K
             print(f"gemm {str(dt)[6:]:8s} M={M} N={N:5d} K={K:5d} out={str(out)[6:]:8s} res={res:d}: "
@@ -119,8 +118,6 @@ def gemm_k32_suite():
             w = torch.randn(N, K, device=dev) / K ** 0.5
             b = torch.randn(N, device=dev)
             t = bench({"pp": lambda: ops.linear(x, w, b, torch.float32),
-                       "f32w": lambda: with_env("MHADA_GEMM_F32W", "1", ops.linear, x, w, b, torch.float32),
-                       "f32wr": lambda: with_env("MHADA_GEMM_F32W", "2", ops.linear, x, w, b, torch.float32),
                        "torch": lambda: torch.addmm(b, x, w.t())})
             fl = 2 * M * N * K
             print(f"gemmK f32 M={M} N={N:5d} K={K:5d}: " + "  ".join(f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:7.1f} TF"

@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r05c; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -v --timeout 120 --timeout-method thread -k "attn" > $OUT/tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 1
+timeout -k 10 300 python -u tools/attn_ab.py > $OUT/attn_ab.log 2>&1 || exit 2
+echo done
