@@ -43,7 +43,7 @@ struct Tuning {
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
-  int loss_q16 = 0;          // AdaAttnForLoss, d_v 256 / d_qk <= 448: query-stationary 16x16x4 kernel (round 5; 0: LDS-staged split-d)
+  int wino4 = 1;             // fp32 Winograd conv: 4-wave kernel (round 5; 0: the 8-wave kernel, also the fallback for inputs >= 2 GiB)
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };

@@ -403,207 +403,6 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Query-stationary form for d_qk <= 448, d_v = 256 (round 5; the relu3_1 level, 90 % of the loss
-// attention time).  The LDS kernel above splits each 32-query block's Q K^T reduction over 4
-// waves and sums their partial score tiles through LDS (two barriers and a 4-way exchange per
-// 32-key tile, the softmax evaluated 4x).  Here each wave owns 16 queries outright, on
-// v_mfma_f32_16x16x4_f32: its Q rows (d_qk / 4 registers per lane) stay in registers, a 16-key
-// tile's whole score block S^T (16 keys x 16 queries) comes out of one wave's own MFMAs (4
-// accumulation chains over the d chunks, summed once), and O^T (2 x 256 d_v columns x 16 queries
-// = 32 blocks, 128 accumulator registers) lives in the accumulator half of the 512-register file
-// (one wave per SIMD, 4 waves = 64 queries per workgroup).  Lane layouts (16x16x4 f32: lane l
-// supplies A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15]; D register r = D[4 (l >> 4) + r][l & 15]):
-//   * Q K^T: k-step 4c + e takes d = 16c + 4(l >> 4) + e, so a lane's K operands of 4 steps are
-//     one ds_read_b128 of its key row and its Q operands one register quad; K tiles arrive by
-//     LDS-DMA (16 unpadded 1792-B rows, 16-B chunk c of row r at slot c ^ (r & 15), applied on the
-//     source address: the 16 rows of a ds_read_b128 lane group land on 16 distinct bank groups);
-//   * P V: the score accumulator S^T[4g + r][q] is the B operand of k-step r directly (key 4g + r),
-//     so the V^T operand of lane (dv, g) at step r is V^T[dv][4g + r]: one ds_read_b128 of the
-//     tile's V^T image ([dv][16 keys], transposed by the staging writes) per 16-column block.
-// Per tile and wave: 112 + 128 MFMAs (16x16x4, 32 cycles each), one barrier; the K tile (28 KiB)
-// by LDS-DMA and the V tile (16 KiB, transposed on its way in) through registers, one tile ahead,
-// into a double-buffered LDS image.
-// ---------------------------------------------------------------------------------------
-template <int ACT>
-__global__ void __launch_bounds__(256, 1) loss_attn_q16_kernel(const LossAttnP p) {
-  constexpr int TK = 16, DQ = 448, DV = 256;
-  constexpr int VLD = TK + 4;          // V^T row stride (floats): 20 words, 16 rows x 16 B spread over the banks
-  constexpr int KSZ = TK * DQ, VSZ = DV * VLD;
-  constexpr int KPW = TK * DQ / 4 / 64 / 4;  // 1-KiB LDS-DMA pieces of a K tile per wave (7)
-  constexpr int VPT = TK * DV / 4 / 256;  // 4 per thread
-  __shared__ __attribute__((aligned(16))) float smem[2 * (KSZ + VSZ)];  // 96 KiB
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
-  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int nqb = (p.Nq + 63) / 64;
-  const int b = t0 / nqb, qb = t0 - b * nqb;
-  const int q = qb * 64 + wave * 16 + r16;
-  const int qc = min(q, p.Nq - 1);
-  const int NC = DQ / 16;  // 28 16-d chunks (d_qk == 448 checked on the host)
-  // Q operands: chunk c, element e <-> d = 16c + 4g + e
-  f32x4 qreg[DQ / 16];
-  {
-    const float* qrow = p.q + ((long long)b * p.Nq + qc) * p.Dqk + 4 * g;
-#pragma unroll
-    for (int c = 0; c < DQ / 16; ++c)
-      qreg[c] = c < NC ? *reinterpret_cast<const f32x4*>(qrow + 16 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const float* kb = p.k + (long long)b * p.Ns * p.Dqk;
-  const float* vb = p.v + (long long)b * p.Ns * DV;
-  // K tile: LDS slot s (16 B) of the tile's 16 x 112-slot image = row s / 112, logical chunk
-  // (s % 112) ^ (row & 15); this wave's pieces are slots 64 (KPW wave + i) + lane.  Rows hold
-  // d_qk / 4 chunks of the key row (d_qk == 448 checked on the host, so every slot is a real chunk)
-  int ksrc[KPW];
-#pragma unroll
-  for (int i = 0; i < KPW; ++i) {
-    const int sl = 64 * (KPW * wave + i) + lane, row = sl / 112, ch = (sl % 112) ^ (row & 15);
-    ksrc[i] = row * DQ + 4 * ch;
-  }
-  auto dma_k = [&](int key0, int buf) {
-    float* sk = smem + buf * (KSZ + VSZ) + 256 * KPW * wave;
-    const float* src = kb + (long long)key0 * DQ;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) {
-      // clamp rows past Ns (the tail tile): re-read the last key row
-      const int off = min(ksrc[i], (p.Ns - 1 - key0) * DQ + (ksrc[i] % DQ));
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off),
-                                       (__attribute__((address_space(3))) void*)(sk + 256 * i), 16, 0, 0);
-    }
-  };
-  // V tile (registers, one tile ahead): chunk i = key i / 64, dv 4 (i % 64) .. +3, written transposed
-  f32x4 rv[VPT];
-  auto issue_v = [&](int key0) {
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = tid + 256 * i, row = c >> 6, col = c & 63;
-      rv[i] = *reinterpret_cast<const f32x4*>(vb + (long long)min(key0 + row, p.Ns - 1) * DV + 4 * col);
-    }
-  };
-  auto commit_v = [&](int buf) {
-    float* sv = smem + buf * (KSZ + VSZ) + KSZ;
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = tid + 256 * i, row = c >> 6, col = c & 63;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sv[(4 * col + e) * VLD + row] = rv[i][e];
-    }
-  };
-
-  f32x4 O[2][DV / 16];  // [M | E2][dv block]: O^T[16 blk + 4g + r][query r16]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < DV / 16; ++j) O[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m2 = -INFINITY, l = 0.f;
-
-  const int ntile = (p.Ns + TK - 1) / TK;
-  dma_k(0, 0);
-  issue_v(0);
-  commit_v(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int tt = 0; tt < ntile; ++tt) {
-    const int key0 = tt * TK, buf = tt & 1;
-    // tile tt + 1: K by LDS-DMA into the other buffer (its readers, tile tt - 1, passed the last
-    // barrier), V into registers (committed after this tile's products)
-    const int knext = min(tt + 1, ntile - 1) * TK;
-    dma_k(knext, buf ^ 1);
-    issue_v(knext);
-    const float* sk = smem + buf * (KSZ + VSZ);
-    const float* sv = sk + KSZ;
-    // ---- S^T[key 4g + r][query r16] over d_qk, 4 accumulation chains
-    f32x4 Sc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) Sc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    {
-      const float* kr = sk + r16 * DQ;
-#pragma unroll
-      for (int c = 0; c < DQ / 16; ++c) {
-        if (c < NC) {  // wave-uniform
-          const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + 4 * ((4 * c + g) ^ r16));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) Sc[c & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(k4[e], qreg[c][e], Sc[c & 3], 0, 0, 0);
-        }
-      }
-    }
-    f32x4 S = (Sc[0] + Sc[1]) + (Sc[2] + Sc[3]);
-    if constexpr (ACT == MHADA_ACT_SOFTMAX) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        S[r] *= kLog2e;
-        if (key0 + TK > p.Ns && key0 + 4 * g + r >= p.Ns) S[r] = -INFINITY;  // uniform test first: tail tile only
-        mx = fmaxf(mx, S[r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (mx > m2 + kLossRescaleThr || tt == 0) {
-        const float mn = fmaxf(m2, mx);
-        const float alpha = m2 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
-        l *= alpha;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < DV / 16; ++j) O[i][j] *= alpha;
-        m2 = mn;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        S[r] = __builtin_amdgcn_exp2f(S[r] - m2);
-        l += S[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        S[r] = key0 + 4 * g + r < p.Ns ? S[r] + 1.0f : 0.f;
-        l += S[r];
-      }
-    }
-    // ---- O^T[dv][q] += V^T P^T and (V^2)^T P^T; step r: key 4g + r
-    {
-      const float* vr = sv + r16 * VLD + 4 * g;
-#pragma unroll
-      for (int j = 0; j < DV / 16; ++j) {
-        const f32x4 v4 = *reinterpret_cast<const f32x4*>(vr + 16 * j * VLD);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          O[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v4[r], S[r], O[0][j], 0, 0, 0);
-          O[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v4[r] * v4[r], S[r], O[1][j], 0, 0, 0);
-        }
-      }
-    }
-    commit_v(buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's K pieces of tile tt + 1
-    __syncthreads();
-  }
-
-  float lt = l + __shfl_xor(l, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  if (q >= p.Nq) return;
-  const float inv = 1.f / lt;
-  const float* xr = p.x + ((long long)b * p.Nq + q) * DV;
-  const float* mu = p.x_mu + (long long)b * DV;
-  const float* rs = p.x_rs + (long long)b * DV;
-  float* orow = p.out + ((long long)b * p.Nq + q) * DV;
-#pragma unroll
-  for (int j = 0; j < DV / 16; ++j) {
-    const int dv = 16 * j + 4 * g;
-    const f32x4 xx = *reinterpret_cast<const f32x4*>(xr + dv);
-    const f32x4 mm = *reinterpret_cast<const f32x4*>(mu + dv);
-    const f32x4 rr = *reinterpret_cast<const f32x4*>(rs + dv);
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float m1 = O[0][j][e] * inv;
-      const float e2 = O[1][j][e] * inv;
-      o[e] = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f)) * ((xx[e] - mm[e]) * rr[e]) + m1;
-    }
-    *reinterpret_cast<f32x4*>(orow + dv) = o;
-  }
-}
-
 // InstanceNorm applied to token rows: out[b][n][c] = (x - mu[b][c]) * rs[b][c]; with unit != 0
 // each normalised row is further divided by its L2 norm (the cosine activation's q/|q|, k/|k|:
 // adaDecoder.py:30-32).  One wave per row.
@@ -674,14 +473,6 @@ extern "C" int mhada_loss_attn(const float* q, const float* k, const float* v, c
   const int W = Dv / 64;
   if (W & (W - 1)) return fail("mhada_loss_attn: d_v / 64 must be 1, 2, 4 or 8");
   p.dsl = (Dqk + W * 8 - 1) / (W * 8) * 8;
-  if (W == 4 && Dqk == 448 && tuning().loss_q16) {  // d_v 256: query-stationary 16x16x4 form
-    const long long nb64 = (long long)B * ((Nq + 63) / 64);
-    if (activation == MHADA_ACT_SOFTMAX)
-      hipLaunchKernelGGL(loss_attn_q16_kernel<MHADA_ACT_SOFTMAX>, dim3((unsigned)nb64), dim3(256), 0, s, p);
-    else
-      hipLaunchKernelGGL(loss_attn_q16_kernel<MHADA_ACT_COSINE>, dim3((unsigned)nb64), dim3(256), 0, s, p);
-    return check_launch("mhada_loss_attn");
-  }
   if (W == 4 && p.dsl <= 112) {  // d_v 256, d_qk <= 448: the LDS-staged form, 64 queries per workgroup
     const long long nb64 = (long long)B * ((Nq + 63) / 64);
     if (activation == MHADA_ACT_SOFTMAX)

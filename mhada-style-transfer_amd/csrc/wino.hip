@@ -27,7 +27,9 @@
 //   * one counted vmcnt(0) + workgroup barrier.
 // Earlier forms, measured and replaced: 4 waves x 32 tiles with scalar gathers
 // (L2 bound), and 4 waves x 64 tiles holding all 16 positions in 256 AGPRs (one wave per SIMD:
-// the transform and loads serialised with the MFMAs).
+// the transform and loads serialised with the MFMAs).  Round 5: the default is wino4_kernel
+// below (the same tile and MFMA sequence, bit-identical, 13-15 % faster); this 8-wave kernel
+// remains the fallback for inputs of 2 GiB and more (wino4 addresses x by a buffer resource).
 // LDS operand rows are 32 B (8 channels) with the two 16-B halves swapped on rows with bit 3
 // set (swz), so the ds_read_b128 of 32 consecutive rows is conflict-free; the raw patch's 16-B
 // slots are XOR-swizzled (rswz) so the transform's ds_read_b32 hit distinct banks.
@@ -38,6 +40,9 @@
 
 #ifndef WINO_DBG
 #define WINO_DBG 0  // ablation builds (tools/wino_dbg.py): 1 no MFMA, 2 no loads, 4 no transform
+#endif
+#ifndef WINO4_DBG
+#define WINO4_DBG 0  // 4-wave kernel ablation builds (results invalid): 1 no DMA, 2 no transform, 4 no MFMA, 8 no DMA wait
 #endif
 
 namespace mhada {
@@ -76,6 +81,10 @@ MHADA_DEV int swz(int row, int half) { return row * 8 + ((half ^ ((row >> 3) & 1
 // transform's ds_read_b32 of 4 tiles x 8 channels (slots s0 + 4 tx + {0, 1}) hit 8 distinct
 // 4-bank groups (ds_read_b32 serves 32 lanes over 32 banks; unswizzled, tiles tx and tx + 2 met).
 MHADA_DEV int rswz(int slot) { return slot ^ (((slot >> 3) & 1) << 1); }
+// The 4-wave kernel's raw-patch swizzle: its transform reads 64-bit channel pairs of 8 tiles of one
+// tile row per half-wave (pixels 2 apart = 4 slots): bit 1 of the slot flips with bit 4, so tiles
+// t and t + 4 (16 slots apart) land on different 16-B bank groups.
+MHADA_DEV int rswz4(int slot) { return slot ^ (((slot >> 4) & 1) << 1); }
 MHADA_DEV void glds16(const float* src, float* lds) {  // LDS-DMA: lane l -> lds + 16 l bytes
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -297,6 +306,226 @@ __global__ void __launch_bounds__(512, 1) wino_kernel(const WinoP p) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// 4-wave form (round 5, tuning wino4): the same workgroup tile, LDS images and chunk pipeline as
+// wino_kernel, one wave per SIMD with ALL 16 positions of its 32 tiles x 32 channels in 256
+// accumulator registers (wave w: tiles 32 (w & 1).., channels 32 (w >> 1)..), and the chunk's
+// non-MFMA work cut to the transform arithmetic.  Measured (tools/ubench/f32mfma_fill.hip,
+// profiles/r05_f32mfma_fill.log): v_mfma_f32_32x32x2_f32 holds the SIMD's vector issue for its
+// whole 64 cycles, so every VALU instruction of an fp32 MFMA kernel adds its issue cost to the
+// MFMA time whichever wave issues it — only fewer vector instructions help.  Hence:
+//   * LDS-DMA through buffer resources (buffer_load ... lds): the per-chunk advance is the scalar
+//     soffset, no 64-bit address VALU per piece; zero padding comes from out-of-range offsets
+//     (the buffer returns 0), so the transform has no per-value select;
+//   * the chunk loop unrolled by two, so every LDS address of the transform, the operand reads
+//     and the V writes is a per-lane base plus an immediate;
+//   * a chunk is 16 stages of 4 MFMAs, fenced per stage: operand reads two stages ahead, one
+//     LDS-DMA piece in each of stages 0-10, the transform (one item per thread: a channel pair of
+//     one tile, packed f32 arithmetic) loaded in stage 2 and finished in stages 4-5.
+// Every MFMA (accumulator, operand bits and order) is the 8-wave kernel's and the output transform
+// keeps its association: bit-identical to wino_kernel.
+// ------------------------------------------------------------------------------------
+template <int DBG>
+__global__ void __launch_bounds__(256, 1) wino4_kernel(const WinoP p) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * (kVS + kUS + kRS)];  // 150 KiB
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int th = wave & 1, ch = wave >> 1;
+
+  int id = xcd_remap(blockIdx.x, p.nblk);
+  const int nb = id % p.nbn;
+  id /= p.nbn;
+  const int bx = id % p.nbx;
+  id /= p.nbx;
+  const int by = id % p.nby;
+  const int b = id / p.nby;
+  const int co0 = nb * kCO;
+  const int P = p.zero ? p.pad : 1;
+  const int nck = p.Cin / kCK;
+
+  // buffer resources (sizes < 2^31 bytes, checked on the host): offsets at or past the size read 0
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), 0, (int)((long long)p.B * p.H * p.W * p.Cin * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.u), 0, p.Cin * 16 * p.Cout * 4, 0x00020000);
+  // raw patch DMA: instruction j = wave + 4 t (j < 11), slots as wino_kernel's; byte offsets,
+  // 0x7ff00000 (past the buffer) for zero-padding pixels
+  int rvo[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int slot = rswz4(64 * min(wave + 4 * t, kRDma - 1) + lane);
+    const int px = min(slot >> 1, kRaw - 1);
+    int iy = 2 * by * kT - P + px / kRP, ix = 2 * bx * kT - P + px % kRP;
+    bool inside = true;
+    if (p.zero) {
+      inside = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+    } else {
+      iy = reflect_clamp(iy, p.H);
+      ix = reflect_clamp(ix, p.W);
+    }
+    rvo[t] = inside ? (((b * p.H + iy) * p.W + ix) * p.Cin + 4 * (slot & 1)) * 4 : 0x7ff00000;
+  }
+  const bool raw2 = wave + 8 < kRDma;
+  // U DMA: instructions 8w .. 8w+7 of 32 (byte offsets inside one chunk)
+  int uvo[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int slot = 64 * (8 * wave + t) + lane;
+    const int xi = slot >> 7, row = (slot >> 1) & 63, sh = slot & 1;
+    uvo[t] = ((xi * p.Cout + co0 + row) * kCK + 4 * (sh ^ ((row >> 3) & 1))) * 4;
+  }
+  const int ucb = 16 * p.Cout * kCK * 4;  // bytes per U chunk
+  typedef __attribute__((address_space(3))) void* LdsP;
+  // DMA piece i (0-7: U of chunk cu into U buffer su, 8-10: raw of chunk cr into raw buffer sr)
+  auto dma_piece = [&](int i, int cu, int su, int cr, int sr) {
+    if constexpr ((DBG & 1) != 0) return;
+    if (i < 8) {
+      float* dst = lds + 2 * kVS + su * kUS + (8 * wave + i) * 256;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (LdsP)dst, 16, uvo[i], min(cu, nck - 1) * ucb, 0, 0);
+    } else if (i < 10 || raw2) {
+      float* dst = lds + 2 * (kVS + kUS) + sr * kRS + (wave + 4 * (i - 8)) * 256;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LdsP)dst, 16, rvo[i - 8], min(cr, nck - 1) * kCK * 4, 0, 0);
+    }
+  };
+  // transform item: channels 2 tp, 2 tp + 1 of tile tt (one item per thread, both channels in one
+  // 64-bit LDS word: ds_read_b64 / v_pk_add_f32 / ds_write2st64_b64, half the instructions of
+  // one channel per item)
+  const int tp = tid & 3, tt = tid >> 2;
+  // LDS float offsets of the item's 16 raw pairs (raw buffer 0; buffer 1 is + kRS); & 0xffff: the
+  // sign bit is known zero, so hipcc folds the buffer constant into the ds_read immediate
+  int roffs[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pix = (2 * (tt >> 3) + i) * kRP + 2 * (tt & 7) + j;
+      roffs[4 * i + j] = (2 * (kVS + kUS) + rswz4(2 * pix + (tp >> 1)) * 4 + 2 * (tp & 1)) & 0xffff;
+    }
+  const int vdst = (swz(tt, tp >> 1) + 2 * (tp & 1)) & 0x7fff;
+  f32x2 d[16], tv[16];
+  auto tload = [&](int rbuf) {
+    if constexpr ((DBG & 2) != 0) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = *reinterpret_cast<const f32x2*>(lds + roffs[q] + rbuf * kRS);
+  };
+  auto tcols = [&]() {
+    if constexpr ((DBG & 2) != 0) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tv[0 * 4 + j] = d[0 * 4 + j] - d[2 * 4 + j];
+      tv[1 * 4 + j] = d[1 * 4 + j] + d[2 * 4 + j];
+      tv[2 * 4 + j] = d[2 * 4 + j] - d[1 * 4 + j];
+      tv[3 * 4 + j] = d[1 * 4 + j] - d[3 * 4 + j];
+    }
+  };
+  auto trows = [&](int vbuf, int i0) {  // rows i0, i0 + 1 of V = t B
+    if constexpr ((DBG & 2) != 0) return;
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i) {
+      float* o = lds + vbuf * kVS + vdst;
+      *reinterpret_cast<f32x2*>(o + (4 * i + 0) * kTT * kCK) = tv[4 * i + 0] - tv[4 * i + 2];
+      *reinterpret_cast<f32x2*>(o + (4 * i + 1) * kTT * kCK) = tv[4 * i + 1] + tv[4 * i + 2];
+      *reinterpret_cast<f32x2*>(o + (4 * i + 2) * kTT * kCK) = tv[4 * i + 2] - tv[4 * i + 1];
+      *reinterpret_cast<f32x2*>(o + (4 * i + 3) * kTT * kCK) = tv[4 * i + 1] - tv[4 * i + 3];
+    }
+  };
+
+  f32x16 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[x][q] = 0.f;
+  const int arow = swz(32 * th + r32, h) & 0x7fff, brow = (2 * kVS + swz(32 * ch + r32, h)) & 0xffff;
+  f32x4 oa[3], ob[3];
+  auto rdop = [&](int xi, int buf, f32x4& a, f32x4& bb) {
+    a = *reinterpret_cast<const f32x4*>(lds + buf * kVS + xi * (kTT * kCK) + arow);
+    bb = *reinterpret_cast<const f32x4*>(lds + buf * kUS + xi * (kCO * kCK) + brow);
+  };
+  auto publish = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((DBG & 8) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  // prologue: U(0), raw(0), raw(1); transform raw(0) into V[0]
+#pragma unroll
+  for (int i = 0; i < 11; ++i) dma_piece(i, 0, 0, 0, 0);
+#pragma unroll
+  for (int i = 8; i < 11; ++i) dma_piece(i, 0, 0, 1, 1);
+  publish();
+  tload(0);
+  tcols();
+  trows(0, 0);
+  trows(0, 2);
+  __syncthreads();
+  // chunk k (buffer parity C = k & 1, a compile-time constant in each unrolled copy)
+  auto chunk = [&](int k, auto cc) {
+    constexpr int C = decltype(cc)::value, N = C ^ 1;
+    rdop(0, C, oa[0], ob[0]);
+    rdop(1, C, oa[1], ob[1]);
+    fence();
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      if (xi + 2 < 16) rdop(xi + 2, C, oa[(xi + 2) % 3], ob[(xi + 2) % 3]);
+      if constexpr ((DBG & 4) == 0) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(oa[xi % 3][s], ob[xi % 3][s], acc[xi], 0, 0, 0);
+      }
+      if (xi < 11) dma_piece(xi, k + 1, N, k + 2, C);
+      if (xi == 2) tload(N);
+      if (xi == 4) { tcols(); trows(N, 0); }
+      if (xi == 5) trows(N, 2);
+      fence();
+    }
+    publish();
+  };
+  int k = 0;
+  for (; k + 1 < nck; k += 2) {
+    chunk(k, std::integral_constant<int, 0>());
+    chunk(k + 1, std::integral_constant<int, 1>());
+  }
+  if (k < nck) chunk(k, std::integral_constant<int, 0>());
+
+  // output transform Y = A^T M A, every position in this wave; the association of wino_kernel's
+  // two-wave form (row partials P_i; Y0 = (P0 + P1) + P2, Y1 = P1 + (-P2 - P3))
+  const int co = co0 + 32 * ch + r32;
+  const float bias = p.bias ? p.bias[co] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int tile = 32 * th + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float m[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float m0 = acc[4 * i][r], m1 = acc[4 * i + 1][r], m2 = acc[4 * i + 2][r], m3 = acc[4 * i + 3][r];
+      m[i][0] = m0 + m1 + m2;
+      m[i][1] = m1 - m2 - m3;
+    }
+    const int oy0 = 2 * (by * kT + (tile >> 3)), ox0 = 2 * (bx * kT + (tile & 7));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float e1 = -m[2][q] - m[3][q];
+      float y0 = m[0][q] + m[1][q] + m[2][q] + bias;
+      float y1 = m[1][q] + e1 + bias;
+      if (p.relu) {
+        y0 = fmaxf(y0, 0.f);
+        y1 = fmaxf(y1, 0.f);
+      }
+      const int ox = ox0 + q;
+      if (ox < p.Wo) {
+        const long long i0 = ((long long)(b * p.Ho + oy0) * p.Wo + ox) * p.ldc + co;
+        const long long i1 = i0 + (long long)p.Wo * p.ldc;
+        if (p.mask) {
+          if (oy0 < p.Ho && !(p.mask[i0] > 0.f)) y0 = 0.f;
+          if (oy0 + 1 < p.Ho && !(p.mask[i1] > 0.f)) y1 = 0.f;
+        }
+        if (oy0 < p.Ho) p.y[i0] = y0;
+        if (oy0 + 1 < p.Ho) p.y[i1] = y1;
+      }
+    }
+  }
+}
 
 // U = G g G^T per (co, ci); w [Cout][3][3][Cin] -> u [Cin/8][16][Cout][8]
 __global__ void wino_weights_kernel(const float* __restrict__ w, float* __restrict__ u, int Cout, int Cin) {
@@ -677,6 +906,10 @@ extern "C" int mhada_conv3x3_wino(const float* x, const float* u, const float* b
   if (nblk > (1LL << 31) - 1 || (long long)B * H * W * Cin > (1LL << 31) - 1)
     return fail("mhada_conv3x3_wino: problem too large for 32-bit indexing");
   p.nblk = (int)nblk;
-  hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
+  // the 4-wave form addresses x through a buffer resource: byte size below the out-of-range offset
+  if (tuning().wino4 && (long long)B * H * W * Cin * 4 < 0x7ff00000LL) {
+    hipLaunchKernelGGL(wino4_kernel<WINO4_DBG>, dim3(p.nblk), dim3(256), 0, (hipStream_t)s_, p);
+  } else
+    hipLaunchKernelGGL(wino_kernel, dim3(p.nblk), dim3(512), 0, (hipStream_t)s_, p);
   return check_launch("mhada_conv3x3_wino");
 }

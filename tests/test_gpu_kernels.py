@@ -231,6 +231,30 @@ def test_conv3x3_wino(pad_mode, pad, B, H, W, Ci, Co, ldc):
         assert rel(y[..., :Co], yd) < 2e-6
 
 
+@pytest.mark.parametrize("pad_mode,pad", [("reflect", 1), ("zero", 1), ("zero", 2)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldc", [(2, 8, 8, 8, 64, 64), (1, 9, 13, 32, 128, 128), (2, 33, 20, 64, 64, 68),
+                                              (1, 3, 2, 16, 64, 64), (1, 16, 16, 512, 256, 256), (2, 2, 5, 24, 192, 196),
+                                              (2, 40, 36, 96, 128, 128)])
+def test_conv3x3_wino4_bit_identical(pad_mode, pad, B, H, W, Ci, Co, ldc):
+    """The 4-wave Winograd kernel (tuning wino4 = 1) runs every MFMA of the 8-wave kernel in the
+    same order and keeps its output-transform association: the outputs are bit-identical, with
+    and without bias / ReLU / the folded ReLU mask, partial tiles and channel-padded outputs."""
+    from mhada_hip import _lib
+    x = torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(H * W + Ci)).to(DEV) - 0.3
+    wp = rnd(Co, 9 * Ci, scale=(9 * Ci) ** -0.5, seed=2)
+    b = rnd(Co, seed=3)
+    Ho, Wo = (H, W) if pad_mode == "reflect" else (H + 2 * (pad - 1), W + 2 * (pad - 1))
+    mask = (torch.rand(B, Ho, Wo, ldc, generator=torch.Generator().manual_seed(Ci)) - 0.5).to(DEV)
+    u = ops.wino_weights(wp)
+    for bias, relu, m in ((b, True, None), (None, False, None), (b, False, mask)):
+        outs = []
+        for knob in (0, 1):
+            with _lib.tuning(wino4=knob):
+                out = torch.full((B, Ho, Wo, ldc), 7.0, device=DEV)
+                outs.append(ops.conv3x3_wino(x, u, bias, relu, pad_mode, pad, out=out, relu_mask=m))
+        assert torch.equal(outs[0], outs[1])
+
+
 def test_conv3x3_wino_routing():
     """ops.conv3x3 takes the Winograd kernel for eligible fp32 shapes (same result as the explicit
     call) and the implicit GEMM otherwise (Cout % 64 != 0)."""

@@ -1,43 +1,44 @@
-"""fp32 3x3 conv: Winograd F(2x2,3x3) (wino.hip) vs the direct implicit GEMM, median HIP-event
-time per shape.  usage: python tools/wino_ab.py [iters]"""
-import os, sys
+"""A/B timing of the fp32 Winograd conv kernels (tuning wino4 0 / 1) on the decoder / VGG shapes
+of the 512^2 batch-8 step and the training step, interleaved rounds in one process.
+
+    python tools/wino_ab.py
+
+Ablations of the 4-wave kernel (profiles/r05_wino4_ablate.log) come from builds with
+-DWINO4_DBG=<mask> (1 no DMA, 2 no transform, 4 no MFMA, 8 no DMA wait; results invalid).
+"""
+import os
+import sys
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd")]
+sys.path[:0] = [REPO, os.path.join(REPO, "mhada-style-transfer_amd"), os.path.dirname(os.path.abspath(__file__))]
+
 import torch
-from mhada_hip import ops
 
-ITERS = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-# (name, B, H, Ci, Co, pad_mode, pad): 512^2 B8 decoder layers, VGG19 at 512^2 B8, a dgrad shape
-SHAPES = [("dec1 512->256 @64", 8, 64, 512, 256, "reflect", 1), ("dec2 256->256 @128", 8, 128, 256, 256, "reflect", 1),
-          ("dec5 256->128 @128", 8, 128, 256, 128, "reflect", 1), ("dec6 128->128 @256", 8, 256, 128, 128, "reflect", 1),
-          ("dec7 128->64 @256", 8, 256, 128, 64, "reflect", 1), ("dec8 64->64 @512", 8, 512, 64, 64, "reflect", 1),
-          ("vgg1_2 64->64 @512", 8, 512, 64, 64, "zero", 1), ("vgg2_2 128->128 @256", 8, 256, 128, 128, "zero", 1),
-          ("vgg3 256->256 @128", 8, 128, 256, 256, "zero", 1), ("vgg4 512->512 @64", 8, 64, 512, 512, "zero", 1),
-          ("dgrad 256->256 @128 pad2", 8, 128, 256, 256, "zero", 2)]
+from mhada_hip import _lib, ops
+from opbench import bench
 
 
-def med(f):
-    f()
-    ts = []
-    for _ in range(ITERS):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(); f(); e.record(); torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e) * 1e3)
-    return sorted(ts)[len(ts) // 2]
+def main():
+    dev = "cuda"
+    torch.manual_seed(0)
+    for (B, H, Ci, Co, pad_mode) in [(8, 64, 512, 256, "reflect"), (8, 128, 256, 256, "reflect"),
+                                     (8, 128, 256, 128, "reflect"), (8, 256, 128, 128, "reflect"),
+                                     (8, 256, 128, 64, "reflect"), (8, 512, 64, 64, "reflect"),
+                                     (8, 256, 64, 128, "zero"), (8, 128, 128, 256, "zero"), (8, 64, 256, 512, "zero")]:
+        x = torch.randn(B, H, H, Ci, device=dev)
+        w = torch.randn(Co, 9 * Ci, device=dev) / (9 * Ci) ** 0.5
+        b = torch.randn(Co, device=dev)
+        u = ops.wino_weights(w)
+        out = torch.empty(B, H, H, Co, device=dev)
+
+        def run(k):
+            with _lib.tuning(wino4=k):
+                ops.conv3x3_wino(x, u, b, True, pad_mode, 1, out=out)
+        t = bench({"w8": lambda: run(0), "w4": lambda: run(1)})
+        fl = 2 * B * H * H * Co * 9 * Ci / 2.25  # Winograd products
+        print(f"wino {pad_mode:7s} B={B} {H:3d}^2 {Ci:3d}->{Co:3d}: " + "  ".join(
+            f"{k} {v * 1e3:7.1f} us {fl / v / 1e9:6.1f} TF(wino)" for k, v in t.items()), flush=True)
 
 
-for name, B, H, Ci, Co, pm, pad in SHAPES:
-    x = torch.rand(B, H, H, Ci, device="cuda")
-    w = torch.randn(Co, 9 * Ci, device="cuda") / (9 * Ci) ** 0.5
-    b = torch.randn(Co, device="cuda")
-    u = ops.wino_weights(w)
-    Ho = H + 2 * (pad - 1)
-    flop = 2.0 * 9 * Ci * Co * B * Ho * Ho
-    tw = med(lambda: ops.conv3x3_wino(x, u, b, True, pm, pad))
-    ops.WINO = False
-    td = med(lambda: ops.conv3x3(x, w, b, torch.float32, upsample=False, relu=True, pad_mode=pm, pad=pad))
-    ops.WINO = True
-    err = (ops.conv3x3_wino(x, u, b, True, pm, pad) - ops.conv3x3(x, w, b, torch.float32, upsample=False,
-                                                                 pad_mode=pm, pad=pad)).abs().max().item()
-    print(f"{name:26s} wino {tw:8.1f} us ({flop / tw / 1e6:6.1f} direct-equiv TF/s, {flop / 2.25 / tw / 1e6:6.1f} TF/s "
-          f"MFMA)  direct {td:8.1f} us ({flop / td / 1e6:6.1f} TF/s)  x{td / tw:.2f}  max|d|={err:.2e}", flush=True)
+if __name__ == "__main__":
+    main()
