@@ -23,6 +23,8 @@
 // (accumulator-as-operand), so no score or probability ever moves between lanes.
 #include "common.h"
 
+#include <type_traits>
+
 #include <stdlib.h>
 
 namespace mhada {
@@ -397,6 +399,7 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   // dS rows of this (b, h): offsets past num_records (rows >= Nc, or a key >= Ns, whose lanes
   // add (Nc + 32) rows) are dropped; unsigned offsets < 2 (Nc + 32) Ns * 4 < 2^32 (entry check)
   const unsigned dkey = kv ? key * 4u : (unsigned)(p.Nc + TT) * p.Ns * 4;
+  const unsigned dvo = 4u * h * p.Ns * 4 + dkey;  // + the row's soffset: past the spill for key >= Ns
   const __amdgpu_buffer_rsrc_t dsr =
       __builtin_amdgcn_make_buffer_rsrc(SPILL ? p.ds + bh * p.Nc * p.Ns : nullptr, 0,
                                         SPILL ? p.Nc * p.Ns * 4 : 0, 0x00020000);
@@ -526,21 +529,37 @@ __global__ void __launch_bounds__(256, 1) attn_train_dkv_dma_kernel(const TrainP
   const float* lb = p.lse + bh * p.Nc;
   const float* db = p.dd + bh * p.Nc;
   // DMA pieces (1 KiB = 64 lanes x 16 B) of this wave: Q rows 4 per piece (pieces 2w, 2w+1), dO
-  // rows 2 per piece (pieces 4w .. 4w+3); each lane fetches the global chunk its LDS slot holds
-  auto stage = [&](int q0, int sl) {  // tile q0 .. q0+31 into ring slot sl (rows clamped to Nc - 1)
+  // rows 2 per piece (pieces 4w .. 4w+3); each lane fetches the global chunk its LDS slot holds.
+  // Q and dO go through buffer resources built per tile (scalar work) over the rows q0 .. Nc - 1,
+  // so each lane's offset is a constant and a piece costs no vector address arithmetic (an fp32
+  // MFMA holds the SIMD's vector issue for its whole 64 cycles, profiles/r05_f32mfma_fill.log:
+  // every VALU instruction adds to the loop).  Rows past Nc read 0 (out of range); with their
+  // lse = +inf (padding piece below) P = 0 there, as with the clamped rows of the other kernel.
+  typedef __attribute__((address_space(3))) void* LdsP;
+  int qvo[2], ovo[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 4 * (2 * wave + i) + (lane >> 4);
+    qvo[i] = (row * 64 + 4 * ((lane & 15) ^ (row & 15))) * 4;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 2 * (4 * wave + i) + (lane >> 5);
+    ovo[i] = (row * 128 + 4 * (((lane >> 4) & 1) * 16 + ((lane & 15) ^ (row & 15)))) * 4;
+  }
+  auto stage = [&](int q0, int sl) {  // tile q0 .. q0+31 into ring slot sl
     float* d = smem + sl * SLOT;
+    const int left = max(p.Nc - q0, 0);
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(qb + (long long)min(q0, p.Nc) * 64), 0, left * 64 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(ob + (long long)min(q0, p.Nc) * 128), 0, left * 128 * 4, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 4 * (2 * wave + i) + (lane >> 4);
-      train_glds(qb + (long long)min(q0 + row, p.Nc - 1) * 64 + 4 * ((lane & 15) ^ (row & 15)),
-                 d + (2 * wave + i) * 256, 16);
-    }
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LdsP)(d + (2 * wave + i) * 256), 16, qvo[i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 2 * (4 * wave + i) + (lane >> 5);
-      train_glds(ob + (long long)min(q0 + row, p.Nc - 1) * 128 + 4 * (((lane >> 4) & 1) * 16 + ((lane & 15) ^ (row & 15))),
-                 d + QF + (4 * wave + i) * 256, 16);
-    }
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ors, (LdsP)(d + QF + (4 * wave + i) * 256), 16, ovo[i], 0, 0, 0);
     // lse | D: lanes 0-31 / 32-63; padding queries read +inf / 0 (every wave issues the same
     // piece, so every wave's wait counts are equal)
     const int qi = q0 + r32;
@@ -554,25 +573,35 @@ __global__ void __launch_bounds__(256, 1) attn_train_dkv_dma_kernel(const TrainP
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int lo = 4 * ((r32 >> 2) ^ (j | (4 * h))) + (r32 & 3);
-    xo[j] = 4 * h * 128 + lo;
-    xq[j] = 4 * h * 64 + lo;
+    xo[j] = (QF + 4 * h * 128 + lo) & 0xffff;  // the O rows' base QF folded in: immediates stay < 64 KiB
+    xq[j] = (4 * h * 64 + lo) & 0xffff;
   }
   const int sw1 = r32 & 15;
   f32x16 G1[2] = {f32x16{}, f32x16{}}, G2[2] = {f32x16{}, f32x16{}}, dK[2] = {f32x16{}, f32x16{}};
-  const unsigned dkey = kv ? key * 4u : (unsigned)(p.Nc + TT) * p.Ns * 4;
-  const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(p.ds + bh * p.Nc * p.Ns, 0, p.Nc * p.Ns * 4,
-                                                                      0x00020000);
+  // dS spill offsets of the lane's 16 accumulator rows relative to the tile's first row (past the
+  // resource for keys >= Ns)
+  unsigned dvo[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dvo[r] = kv ? (unsigned)acc_row(r, h) * p.Ns * 4 + key * 4u : 0x7ff00000u;
   // phase 1 of the tile in ring slot sl: S (queries x keys) = Q . K^T, dA = [dM' | dE2'] . [V' | V'^2]^T
+  // Every LDS address below is a per-lane register plus an immediate: the ring slot is a
+  // compile-time constant in each unrolled step (the loop runs six steps per iteration, two
+  // register sets x three slots), and the per-lane parts are masked so their sign bit is known
+  // zero (hipcc folds constants into a ds_read immediate only then).
+  int qoff[8], ooff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = 4 * ((8 * h + i) ^ sw1);
+    qoff[i] = (r32 * 64 + c) & 0xffff;
+    ooff[i] = (QF + r32 * 128 + c) & 0xffff;
+  }
   auto phase1 = [&](int sl, f32x16& S, f32x16& dA) {
     const float* sQ = smem + sl * SLOT;
-    const float* qrw = sQ + r32 * 64;
-    const float* orw = sQ + QF + r32 * 128;
     S = f32x16{};
     dA = f32x16{};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = 4 * ((8 * h + i) ^ sw1);
-      const f32x4 qq = ld4(qrw + c), o1 = ld4(orw + c), o2 = ld4(orw + 64 + c);
+      const f32x4 qq = ld4(sQ + qoff[i]), o1 = ld4(sQ + ooff[i]), o2 = ld4(sQ + ooff[i] + 64);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int s2 = 4 * i + e;
@@ -591,20 +620,21 @@ __global__ void __launch_bounds__(256, 1) attn_train_dkv_dma_kernel(const TrainP
       S[r] = __builtin_amdgcn_exp2f(S[r] - sLD[qi]);
       dA[r] = S[r] * (dA[r] - sLD[TT + qi]);
     }
-    const unsigned base = (unsigned)(q0 + 4 * h) * p.Ns * 4 + dkey;  // dS [q][key]: 32 lanes write 128 B
+    // dS [q][key]: 32 lanes write 128 B, through a resource over rows q0 .. Nc - 1 (rows past Nc
+    // and keys past Ns are out of range: dropped) and per-lane offsets precomputed for the 16 rows
+    const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
+        p.ds + bh * p.Nc * p.Ns + (long long)min(q0, p.Nc) * p.Ns, 0, max(p.Nc - q0, 0) * p.Ns * 4, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dA[r]), dsr,
-                                            (int)(base + ((r & 3) + 8 * (r >> 2)) * p.Ns * 4u), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dA[r]), dsr, (int)dvo[r], 0, 0);
   };
   // phase 2: G1^T, G2^T (c x keys) += [dM' | dE2']^T (c x queries) . P;  dK^T += Q^T . dS
   auto phase2 = [&](int sl, const f32x16& P, const f32x16& dS) {
     const float* sQ = smem + sl * SLOT;
-    const float* sO = sQ + QF;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = r & 3, rowb = (r & 3) + 8 * (r >> 2), b3 = (r >> 2) & 1;
-      const float* o = sO + xo[j] + rowb * 128;
+      const float* o = sQ + xo[j] + rowb * 128;
       const float* qq = sQ + xq[j] + rowb * 64;
       G1[0] = mfma(o[32 * b3], P[r], G1[0]);
       G1[1] = mfma(o[32 * (1 - b3)], P[r], G1[1]);
@@ -623,28 +653,38 @@ __global__ void __launch_bounds__(256, 1) attn_train_dkv_dma_kernel(const TrainP
   TRAIN_STAMP(0);
   f32x16 Sa, dAa, Sb, dAb;
   phase1(0, Sa, dAa);
-  int sl = 0;
   // iteration t: publish tile t + 1; DMA tile t + 2 into the slot tile t - 1 used; tile t + 1's
   // phase 1 beside tile t's softmax and stores; tile t's phase 2.  Two register sets, A / B,
-  // alternate by unrolling the loop by two.
-  auto step = [&](int t, f32x16& S, f32x16& dA, f32x16& Sn, f32x16& dAn) __attribute__((always_inline)) {
+  // alternate and the ring slot cycles 0, 1, 2: six steps per loop iteration, each with its slot
+  // a compile-time constant.
+  auto step = [&](int t, auto slc, f32x16& S, f32x16& dA, f32x16& Sn, f32x16& dAn) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slc)::value, SN = (SL + 1) % 3, S2 = (SL + 2) % 3;
     // tile t + 1 landed (younger: tile t's dS stores... issued after it in iteration t - 1: 16)
     if (t == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     lds_barrier();
-    const int sn = sl == 2 ? 0 : sl + 1, s2 = sl == 0 ? 2 : sl - 1;
-    stage((t + 2) * TT, s2);  // past the end: clamped rows, never read
-    softmax(sl, t * TT, S, dA);
-    phase1(sn, Sn, dAn);  // tile t + 1 (past the end: clamped rows, result unused)
-    phase2(sl, S, dA);
-    sl = sn;
+    stage((t + 2) * TT, S2);  // past the end: rows read 0, never used
+    softmax(SL, t * TT, S, dA);
+    phase1(SN, Sn, dAn);  // tile t + 1 (past the end: result unused)
+    phase2(SL, S, dA);
   };
+  typedef std::integral_constant<int, 0> L0;
+  typedef std::integral_constant<int, 1> L1;
+  typedef std::integral_constant<int, 2> L2;
   int t = 0;
-  for (; t + 1 < nt; t += 2) {
-    step(t, Sa, dAa, Sb, dAb);
-    step(t + 1, Sb, dAb, Sa, dAa);
+  for (; t + 5 < nt; t += 6) {
+    step(t, L0(), Sa, dAa, Sb, dAb);
+    step(t + 1, L1(), Sb, dAb, Sa, dAa);
+    step(t + 2, L2(), Sa, dAa, Sb, dAb);
+    step(t + 3, L0(), Sb, dAb, Sa, dAa);
+    step(t + 4, L1(), Sa, dAa, Sb, dAb);
+    step(t + 5, L2(), Sb, dAb, Sa, dAa);
   }
-  if (t < nt) step(t, Sa, dAa, Sb, dAb);
+  if (t < nt) step(t, L0(), Sa, dAa, Sb, dAb);
+  if (t + 1 < nt) step(t + 1, L1(), Sb, dAb, Sa, dAa);
+  if (t + 2 < nt) step(t + 2, L2(), Sa, dAa, Sb, dAb);
+  if (t + 3 < nt) step(t + 3, L0(), Sb, dAb, Sa, dAa);
+  if (t + 4 < nt) step(t + 4, L1(), Sa, dAa, Sb, dAb);
   TRAIN_STAMP(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMA past the end has landed
   if (!kv) return;

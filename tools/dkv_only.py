@@ -22,9 +22,23 @@ dd = (dmo * mo).sum(-1).contiguous()
 ds = torch.empty(BH, n, n, device="cuda")
 dk, dv = torch.empty_like(k), torch.empty_like(v)
 lib = _lib.load()
-for _ in range(int(os.environ.get("ITERS", "3"))):
+
+
+def launch():
     assert lib.mhada_attn_train_dkv(q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
                                     dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, n, n,
                                     torch.cuda.current_stream().cuda_stream) == 0
+
+
+launch()
 torch.cuda.synchronize()
-print("done")
+iters = int(os.environ.get("ITERS", "3"))
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+for _ in range(iters):
+    launch()
+e.record()
+torch.cuda.synchronize()
+t = s.elapsed_time(e) / iters
+fl = 2 * BH * n * n * 64 * 6  # S, dA (2 x 64 + 64 ... the six 64-deep products per (q, key))
+print(f"dK/dV' BH={BH} N={n}: {t:.3f} ms per launch ({fl / t / 1e9:.1f} TF/s at 6 x 2 x 64 FLOP per pair)", flush=True)
