@@ -253,28 +253,37 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
   }
   const float* kb = p.k + (long long)b * p.Ns * p.Dqk;
   const float* vb = p.v + (long long)b * p.Ns * p.Dv;
-  // tile staging: K tile = 32 rows x Dqk/4 16-B chunks, V tile = 32 x 64 chunks (clamped rows)
+  // tile staging: K tile = 32 rows x Dqk/4 16-B chunks, V tile = 32 x 64 chunks.  Loads through
+  // buffer resources built per tile over the key rows key0 .. Ns - 1 (scalar work): every lane's
+  // offset (and LDS destination) is a loop constant, so a tile's 11 loads cost no vector address
+  // arithmetic (an fp32 MFMA holds the SIMD's vector issue for its whole 64 cycles,
+  // profiles/r05_f32mfma_fill.log).  Rows past Ns read 0: their scores are masked, their P is 0.
   const int kcr = p.Dqk / 4, kch = 32 * kcr;
   constexpr int KR = (32 * 112 + 511) / 512;  // <= 7 chunks per thread (d_qk <= 448)
   f32x4 rk[KR], rv[4];
+  int kvo[KR], klo[KR];
+#pragma unroll
+  for (int i = 0; i < KR; ++i) {
+    const int c = min(tid + 512 * i, kch - 1), row = c / kcr, col = c - row * kcr;
+    kvo[i] = (row * p.Dqk + 4 * col) * 4;
+    klo[i] = (row * KLD + 4 * col) & 0xffff;
+  }
   auto issue = [&](int key0) {
+    const int left = max(p.Ns - key0, 0);
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(kb + (long long)min(key0, p.Ns) * p.Dqk), 0, left * p.Dqk * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(vb + (long long)min(key0, p.Ns) * p.Dv), 0, left * p.Dv * 4, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < KR; ++i) {
-      const int c = min(tid + 512 * i, kch - 1), row = c / kcr, col = c - row * kcr;
-      rk[i] = *reinterpret_cast<const f32x4*>(kb + (long long)min(key0 + row, p.Ns - 1) * p.Dqk + 4 * col);
-    }
+    for (int i = 0; i < KR; ++i)
+      rk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(kr, kvo[i], 0, 0));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 512 * i, row = c >> 6, col = c & 63;
-      rv[i] = *reinterpret_cast<const f32x4*>(vb + (long long)min(key0 + row, p.Ns - 1) * p.Dv + 4 * col);
-    }
+    for (int i = 0; i < 4; ++i)
+      rv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, (tid + 512 * i) * 16, 0, 0));
   };
   auto commit_k = [&]() {
 #pragma unroll
-    for (int i = 0; i < KR; ++i) {
-      const int c = min(tid + 512 * i, kch - 1), row = c / kcr, col = c - row * kcr;
-      *reinterpret_cast<f32x4*>(sK + row * KLD + 4 * col) = rk[i];
-    }
+    for (int i = 0; i < KR; ++i) *reinterpret_cast<f32x4*>(sK + klo[i]) = rk[i];
   };
   auto commit_v = [&]() {
 #pragma unroll
@@ -325,15 +334,17 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
       S[r] = a;
     }
     if constexpr (ACT == MHADA_ACT_SOFTMAX) {
+      // the tile max on the raw scores, then P = exp2(s log2 e - m2) as one fma per score (the
+      // scale is monotonic, so the max commutes with it)
+      if (key0 + 32 > p.Ns) {  // uniform: tail tile only
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + (r & 3) + 8 * (r >> 2) + 4 * h >= p.Ns) S[r] = -INFINITY;
+      }
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        S[r] *= kLog2e;
-        if (key0 + 32 > p.Ns && key >= p.Ns) S[r] = -INFINITY;  // uniform test first: tail tile only
-        mx = fmaxf(mx, S[r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * kLog2e;
       if (mx > m2 + kLossRescaleThr || tt == 0) {
         const float mn = fmaxf(m2, mx);
         const float alpha = m2 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
@@ -347,7 +358,7 @@ __global__ void __launch_bounds__(512) loss_attn_lds_kernel(const LossAttnP p) {
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        S[r] = __builtin_amdgcn_exp2f(S[r] - m2);  // bare v_exp_f32 (no denormal range fix-up)
+        S[r] = __builtin_amdgcn_exp2f(fmaf(S[r], kLog2e, -m2));  // bare v_exp_f32 (no denormal range fix-up)
         sum += S[r];
       }
       l += sum;
