@@ -708,83 +708,48 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ x
   }
 }
 
-// Round 5: one thread per (source pixel, 8-channel group) writes the 2 x 2 output block above it.
-// Output rows 2i, 2i + 1 only ever read source rows i - 1 .. i + 1 (columns likewise), so the 3 x 3
-// source window is loaded once (9 vector loads for 4 outputs instead of 16 scalar-indexed ones) and
-// each output takes its taps from the window by the SAME coordinate / weight computation and blend
-// expression as upsample2x_kernel (bit-identical; tests/test_gpu_kernels.py::test_upsample2x).
+// 16-B vector form (round 5) for 16-B aligned tensors: the same thread mapping, coordinates,
+// weights and blend expression as upsample2x_kernel (bit-identical), with each tap's 8 channels
+// read and the output written as whole 16-B vectors.  (A 2 x 2-output-block form that loaded the
+// 3 x 3 source window once measured 1.1-1.6x SLOWER: its window indexing cost more vector
+// instructions than the loads it saved, profiles/r05_prof_bench_per_config.txt.)
 template <typename T>
-__global__ void __launch_bounds__(256) upsample2x_blk_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
+__global__ void __launch_bounds__(256) upsample2x_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
                                                              int W, int C) {
   typedef typename Vec16<T>::type V;
-  constexpr int NV = 8 / Vec16<T>::N;  // 16-B vectors per 8-channel group
+  constexpr int N = Vec16<T>::N, NV = 8 / N;  // 16-B vectors per 8-channel group
   const int G = C / 8;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)B * H * W * G;
+  const long long total = (long long)B * 4 * H * W * G;
   if (idx >= total) return;
   const int g = (int)(idx % G);
   long long pix = idx / G;
-  const int j = (int)(pix % W);
-  pix /= W;
-  const int i = (int)(pix % H);
-  const int b = (int)(pix / H);
-  const T* base = x + (long long)b * H * W * C + g * 8;
-  float win[3][3][8];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const int yy = min(max(i - 1 + r, 0), H - 1);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const int xx = min(max(j - 1 + c, 0), W - 1);
-      const V* src = reinterpret_cast<const V*>(base + ((long long)yy * W + xx) * C);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const V q = src[v];
-#pragma unroll
-        for (int e = 0; e < Vec16<T>::N; ++e) win[r][c][v * Vec16<T>::N + e] = to_f32<T>(q[e]);
-      }
-    }
-  }
   const int Wo = 2 * W, Ho = 2 * H;
+  const int X = (int)(pix % Wo);
+  pix /= Wo;
+  const int Y = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
+  const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.f);
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const T* base = x + (long long)b * H * W * C + g * 8;
+  const V* p00 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x0) * C);
+  const V* p01 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x1) * C);
+  const V* p10 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x0) * C);
+  const V* p11 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x1) * C);
+  V* out = reinterpret_cast<V*>(y + (((long long)b * Ho + Y) * Wo + X) * C + g * 8);
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int Y = 2 * i + a;
-    const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
-    const int y0 = (int)sy;
-    const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
-    const float ly1 = sy - (float)y0;
-    const float ly0 = 1.f - ly1;
-    const int r0 = y0 - i + 1, r1 = y1 - i + 1;  // window rows (0 .. 2)
+  for (int v = 0; v < NV; ++v) {
+    const V a00 = p00[v], a01 = p01[v], a10 = p10[v], a11 = p11[v];
+    V o;
 #pragma unroll
-    for (int bb = 0; bb < 2; ++bb) {
-      const int X = 2 * j + bb;
-      const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.f);
-      const int x0 = (int)sx;
-      const int x1 = x0 + (x0 < W - 1 ? 1 : 0);
-      const float lx1 = sx - (float)x0;
-      const float lx0 = 1.f - lx1;
-      const int c0 = x0 - j + 1, c1 = x1 - j + 1;
-      V out[NV];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float p00 = 0.f, p01 = 0.f, p10 = 0.f, p11 = 0.f;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const float w = win[r][c][e];
-            p00 = (r == r0 && c == c0) ? w : p00;
-            p01 = (r == r0 && c == c1) ? w : p01;
-            p10 = (r == r1 && c == c0) ? w : p10;
-            p11 = (r == r1 && c == c1) ? w : p11;
-          }
-        const float v = bilerp(ly0, ly1, lx0, lx1, p00, p01, p10, p11);
-        out[e / Vec16<T>::N][e % Vec16<T>::N] = from_f32<T>(v);
-      }
-      V* dst = reinterpret_cast<V*>(y + (((long long)b * Ho + Y) * Wo + X) * C + g * 8);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) dst[v] = out[v];
-    }
+    for (int e = 0; e < N; ++e)
+      o[e] = from_f32<T>(bilerp(ly0, ly1, lx0, lx1, to_f32<T>(a00[e]), to_f32<T>(a01[e]), to_f32<T>(a10[e]),
+                                to_f32<T>(a11[e])));
+    out[v] = o;
   }
 }
 
@@ -998,14 +963,14 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
 
 extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int C, mhada_stream_t s_) {
   if (!x || !y || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return fail("mhada_upsample2x: bad args");
-  if (aligned16(x) && aligned16(y)) {  // 2 x 2 output blocks (round 5); unaligned views: per-pixel kernel
-    const long long total = (long long)B * H * W * (C / 8);
+  if (aligned16(x) && aligned16(y)) {  // 16-B vector loads / stores (round 5); unaligned views: element form
+    const long long total = (long long)B * 4 * H * W * (C / 8);
     const dim3 grid((unsigned)((total + 255) / 256));
     if (dtype == MHADA_F32)
-      hipLaunchKernelGGL((upsample2x_blk_kernel<float>), grid, dim3(256), 0, (hipStream_t)s_, (const float*)x,
+      hipLaunchKernelGGL((upsample2x_vec_kernel<float>), grid, dim3(256), 0, (hipStream_t)s_, (const float*)x,
                          (float*)y, B, H, W, C);
     else
-      hipLaunchKernelGGL((upsample2x_blk_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)x,
+      hipLaunchKernelGGL((upsample2x_vec_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)x,
                          (bf16*)y, B, H, W, C);
     return check_launch("mhada_upsample2x");
   }

@@ -55,9 +55,6 @@ def gemm_suite(dts=(torch.bfloat16, torch.float32)):
                    "torch": lambda: torch.addmm(b.to(dt), x, w.t())}
             fns["epi_direct"] = lambda: with_env("MHADA_GEMM_LDSEPI", "0", ops.linear, x, w, b, out, residual=r,
                                                  relu=relu)
-            if out == torch.bfloat16:
-                fns["epi8"] = lambda: with_env("MHADA_XKNOB", "1", ops.linear, x, w, b, out, residual=r, relu=relu)
-            fns["epi_nt"] = lambda: with_env("MHADA_XKNOB", "4", ops.linear, x, w, b, out, residual=r, relu=relu)
             if res:
                 fns["no_rinit"] = lambda: with_env("MHADA_GEMM_RINIT", "0", ops.linear, x, w, b, out, residual=r,
                                                    relu=relu)
@@ -168,9 +165,6 @@ def conv_suite():
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
-            if Co <= 64 and dt == torch.bfloat16:
-                fns["n64_pp"] = lambda: with_env("MHADA_GEMM_N64_PP", "1", ops.conv3x3, ops.upsample2x(x) if up else x,
-                                                 w, bias, dt, upsample=False)
             if Co <= 64:
                 fns["n64_256"] = lambda: with_env("MHADA_GEMM_N64", "256", ops.conv3x3, ops.upsample2x(x) if up else x, w,
                                                   bias, dt, upsample=False)
@@ -186,7 +180,7 @@ def conv_suite():
 def n64_suite():
     """fp32 N = 64 GEMMs of the training step: the attention backward's dQ = dS K (24 images x 8
     heads at 64^2 tokens) and the grouped per-head 1x1 convs (K = 64): the LDS-DMA ring kernel vs
-    the register-staged tile (xknob 8) vs torch.bmm."""
+    torch.bmm."""
     dev = "cuda"
     for nz, M, K, lda in ((192, 4096, 4096, 4096), (8, 98304, 64, 512), (8, 98304, 64, 64)):
         a = torch.randn(nz, M, lda, device=dev) if lda == K else torch.randn(M, lda, device=dev)
@@ -195,11 +189,7 @@ def n64_suite():
         sa = (M * K, 0) if lda == K else (64, 0)
         args = dict(a=a, w=w, c=c, M=M, N=64, K=K, compute=torch.float32, lda=lda, sa=sa, nb=(nz, 1), ldw=K,
                     sw=(64 * K, 0), ldc=64, sc=(M * 64, 0))
-        fns = {"default": lambda: ops.gemm(**args), "tile": lambda: with_env("MHADA_XKNOB", "8", ops.gemm, **args),
-               "r128x3": lambda: with_env("MHADA_XKNOB", "1", ops.gemm, **args),
-               "r64x3": lambda: with_env("MHADA_XKNOB", "2", ops.gemm, **args),
-               "r64x2": lambda: with_env("MHADA_XKNOB", "4", ops.gemm, **args),
-               "no_xcdz": lambda: with_env("MHADA_XKNOB", "3", ops.gemm, **args)}
+        fns = {"default": lambda: ops.gemm(**args)}
         if lda == K:
             fns["torch"] = lambda: torch.bmm(a, w.transpose(1, 2))
         t = bench(fns, rounds=5, iters=3)
@@ -233,7 +223,6 @@ def proj_suite():
                   sc=(H * N * 128, N * 128), vt=vt, ldt=N, svt=(H * 128 * N, 128 * N))
         fns = {"q": lambda: ops.gemm(a_mu=mu, smu=(C, 64), **qa),
                "q_n64_256": lambda: with_env("MHADA_GEMM_N64", "256", ops.gemm, a_mu=mu, smu=(C, 64), **qa),
-               "q_ring": lambda: with_env("MHADA_GEMM_N64_CEN", "1", ops.gemm, a_mu=mu, smu=(C, 64), **qa),
                "q_uncentred": lambda: ops.gemm(**qa),
                "kv_vt": lambda: ops.gemm(**ka)}
         t = bench(fns)
