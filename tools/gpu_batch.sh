@@ -7,7 +7,7 @@
 #   bench      the default bench line
 #   trainclock in-kernel clock of the training dK/dV' kernel (diagnostic build)
 #   vit        the ViT / batched-training tests (LinearFn residual, batched ViT / AdaFormer, goldens)
-#   winotests / winoab  the Winograd conv tests / knob A/B (WINO_KNOB, default wino_ws)
+#   winotests / winoab  the Winograd conv tests / knob A/B (WINO_KNOB, default wino4)
 #   train / trainprof  the training step bench line / its rocprofv3 kernel trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -22,9 +22,9 @@ for s in "$@"; do
           timeout -k 10 120 python -u tools/attn_clock.py f32 > $OUT/attn_clock_f32.log 2>&1 || exit 1 ;;
     c64) timeout -k 10 120 python -u tools/c64_ab.py > $OUT/c64_ab.log 2>&1 || exit 2 ;;
     trainclock) timeout -k 10 180 python -u tools/attn_clock.py dkv > $OUT/train_clock.log 2>&1 || exit 6 ;;
-    winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py ${WINO_KNOB:-wino_ws} > $OUT/wino_${WINO_KNOB:-wino_ws}_ab.log 2>&1 || exit 9 ;;
+    winoab) timeout -k 10 300 python -u tools/wino_knob_ab.py ${WINO_KNOB:-wino4} > $OUT/wino_${WINO_KNOB:-wino4}_ab.log 2>&1 || exit 9 ;;
     vit) timeout -k 10 600 $PYT tests/test_gpu_train_ops.py tests/test_gpu_train.py -k "linear_fn or vit_training or batch_axis or batched or bit_identical or golden or 256_b2 or rccl" > $OUT/vit_tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 15 ;;
-    winoab2) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino_ws=0 -c wino_ws=1 -c wino_ws=2 > $OUT/wino_ab2.log 2>&1 || exit 9 ;;
+    winoab2) timeout -k 10 400 python -u tools/wino_knob_ab.py -c wino4=0 -c wino4=1 > $OUT/wino_ab2.log 2>&1 || exit 9 ;;
     winopk) timeout -k 10 300 $PYT tests/test_gpu_kernels.py -k "wino_persistent" > $OUT/wino_pk_tests.log 2>&1 || exit 14 ;;
     winotests) timeout -k 10 300 $PYT tests/test_gpu_kernels.py tests/test_gpu_train_ops.py -k "wino or chain" > $OUT/wino_tests.log 2>&1; rc=$?; [ $rc -le 1 ] || exit 11 ;;
     winodbg) for shp in ${WINO_DBG_SHAPES:-"8 128 256 256" "8 256 128 128" "8 64 512 512"}; do
