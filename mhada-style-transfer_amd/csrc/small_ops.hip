@@ -961,8 +961,98 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
   return check_launch("mhada_conv3x3_out3");
 }
 
+// 2 x 2 output blocks for 16-B aligned tensors (round 5): one thread per (source pixel, 8-channel
+// group) writes the four outputs above source pixel (i, j).  Interior pixels (1 <= i <= H-2,
+// 1 <= j <= W-2) take their taps from the 3 x 3 source window with compile-time indices and the
+// weights the formula gives there exactly (1/4, 3/4: the coordinates are exact in fp32), so each
+// output is the same bilerp expression on the same operands as upsample2x_kernel (bit-identical);
+// border pixels evaluate the formula per output.  9 vector loads per 4 outputs instead of 16.
+template <typename T>
+__global__ void __launch_bounds__(256) upsample2x_quad_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
+                                                              int W, int C) {
+  typedef typename Vec16<T>::type V;
+  constexpr int N = Vec16<T>::N, NV = 8 / N;
+  const int G = C / 8;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)B * H * W * G;
+  if (idx >= total) return;
+  const int g = (int)(idx % G);
+  long long pix = idx / G;
+  const int j = (int)(pix % W);
+  pix /= W;
+  const int i = (int)(pix % H);
+  const int b = (int)(pix / H);
+  const T* base = x + (long long)b * H * W * C + g * 8;
+  const int Wo = 2 * W, Ho = 2 * H;
+  T* obase = y + (long long)b * Ho * Wo * C + g * 8;
+  if (i >= 1 && i <= H - 2 && j >= 1 && j <= W - 2) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      V w[3][3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          w[r][c] = reinterpret_cast<const V*>(base + ((long long)(i - 1 + r) * W + (j - 1 + c)) * C)[v];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const float ly0 = a ? 0.75f : 0.25f, ly1 = a ? 0.25f : 0.75f;  // rows (i-1+a, i+a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const float lx0 = bb ? 0.75f : 0.25f, lx1 = bb ? 0.25f : 0.75f;  // cols (j-1+bb, j+bb)
+          V o;
+#pragma unroll
+          for (int e = 0; e < N; ++e)
+            o[e] = from_f32<T>(bilerp(ly0, ly1, lx0, lx1, to_f32<T>(w[a][bb][e]), to_f32<T>(w[a][bb + 1][e]),
+                                      to_f32<T>(w[a + 1][bb][e]), to_f32<T>(w[a + 1][bb + 1][e])));
+          reinterpret_cast<V*>(obase + ((long long)(2 * i + a) * Wo + (2 * j + bb)) * C)[v] = o;
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int Y = 2 * i + a;
+    const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
+    const int y0 = (int)sy, y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      const int X = 2 * j + bb;
+      const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.f);
+      const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+      const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+      const V* p00 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x0) * C);
+      const V* p01 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x1) * C);
+      const V* p10 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x0) * C);
+      const V* p11 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x1) * C);
+      V* out = reinterpret_cast<V*>(obase + ((long long)Y * Wo + X) * C);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const V a00 = p00[v], a01 = p01[v], a10 = p10[v], a11 = p11[v];
+        V o;
+#pragma unroll
+        for (int e = 0; e < N; ++e)
+          o[e] = from_f32<T>(bilerp(ly0, ly1, lx0, lx1, to_f32<T>(a00[e]), to_f32<T>(a01[e]), to_f32<T>(a10[e]),
+                                    to_f32<T>(a11[e])));
+        out[v] = o;
+      }
+    }
+  }
+}
+
 extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int C, mhada_stream_t s_) {
   if (!x || !y || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return fail("mhada_upsample2x: bad args");
+  // bf16: 2 x 2 output blocks (34 / 88 us vs 53 / 105 us for the 16-B per-pixel form at the
+  // 1024^2 B4 decoder shapes, profiles/r05_opbench_conv_upsample.log); fp32 (two vectors per
+  // 8-channel group): equal or slower, per-pixel.  tuning xknob = 1 forces the per-pixel form (A/B)
+  if (dtype != MHADA_F32 && aligned16(x) && aligned16(y) && H >= 3 && W >= 3 && tuning().xknob != 1) {
+    const long long total = (long long)B * H * W * (C / 8);
+    hipLaunchKernelGGL((upsample2x_quad_kernel<bf16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)s_, (const bf16*)x, (bf16*)y, B, H, W, C);
+    return check_launch("mhada_upsample2x");
+  }
   if (aligned16(x) && aligned16(y)) {  // 16-B vector loads / stores (round 5); unaligned views: element form
     const long long total = (long long)B * 4 * H * W * (C / 8);
     const dim3 grid((unsigned)((total + 255) / 256));

@@ -289,14 +289,19 @@ def test_conv3x3_c64_tile(up, B, H, W):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128), (1, 3, 8), (3, 1, 16)])
+@pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128), (1, 3, 8), (3, 1, 16), (3, 3, 8),
+                                   (4, 9, 24)])
 def test_upsample2x(dt, H, W, C):
-    """The 2 x 2-block kernel (16-B aligned operands) against fp64 F.interpolate, and bit-identical to
-    the per-pixel kernel (which a misaligned view of the same values takes)."""
+    """The default kernel (bf16: 2 x 2 output blocks when H, W >= 3; fp32 and small maps: 16-B per
+    pixel) against fp64 F.interpolate, bit-identical to the 16-B per-pixel kernel (tuning xknob 1
+    forces it) and to the element-wise per-pixel kernel (which a misaligned view takes)."""
+    from mhada_hip import _lib
     x = rnd(2, H, W, C, seed=H).to(dt)
     y = ops.upsample2x(x)
     ref = F.interpolate(x.permute(0, 3, 1, 2).double(), scale_factor=2, mode="bilinear", align_corners=False)
     assert rel(y.permute(0, 3, 1, 2), ref) < (1e-6 if dt == torch.float32 else 5e-3)
+    with _lib.tuning(xknob=1):
+        assert torch.equal(ops.upsample2x(x), y)
     buf = torch.empty(x.numel() + 1, device=DEV, dtype=dt)
     xm = buf[1:].view(x.shape)  # 2 or 4 bytes past a 16-B boundary
     xm.copy_(x)

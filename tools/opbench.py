@@ -171,6 +171,7 @@ def conv_suite():
             if up:
                 fns["sep"] = lambda: ops.conv3x3(ops.upsample2x(x), w, bias, dt, upsample=False)
                 fns["upsample_only"] = lambda: ops.upsample2x(x)
+                fns["upsample_pp"] = lambda: with_env("MHADA_XKNOB", "1", ops.upsample2x, x)
             t = bench(fns)
             fl = 2 * B * H * H * Co * 9 * Ci
             print(f"conv {str(dt)[6:]:8s} {Ci:3d}->{Co:3d} @{H:4d} up={up:d}: "
