@@ -477,10 +477,11 @@ __global__ void __launch_bounds__(256) conv_out3_kernel(const T* __restrict__ x,
 // (The per-pixel VALU kernel above re-reads each input pixel 9x from L1/L2 and spends 1728
 // FMAs + 576 conversions per pixel: ~8x slower at 1024^2.)
 // ---------------------------------------------------------------------------------------
-constexpr int kOut3Rows = 8;  // row tiles per workgroup strip
+constexpr int kOut3Rows = 8;    // row tiles per workgroup strip (fp32 kernel)
+constexpr int kOut3RowsM = 16;  // bf16 MFMA kernel: longer strips amortise its weight-fragment prologue
 
 template <int CIN, int CC>
-__global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+__global__ void __launch_bounds__(256, 2) conv_out3_mfma_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, float* __restrict__ y,
                                                              int H, int W, int tiles_x, int strips_y, int clamp255) {
   // the halo is staged in CC-channel chunks (CC = 32: 31 KiB per buffer, two workgroups per CU;
@@ -491,24 +492,35 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
   __shared__ __attribute__((aligned(16))) bf16 tile[2][HR * HC * LP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bt = blockIdx.x, tx = bt % tiles_x, sy = (bt / tiles_x) % strips_y, b = bt / (tiles_x * strips_y);
-  const int x0 = tx * TC, ys = sy * TR * kOut3Rows;
+  const int x0 = tx * TC, ys = sy * TR * kOut3RowsM;
   const bf16* xb = x + (long long)b * H * W * CIN;
-  // A = W^T fragments (loaded once per block, amortised over the strip's kOut3Rows tiles):
+  // A = W^T fragments (loaded once per block, amortised over the strip's kOut3RowsM tiles):
   // row n = lane & 15 (out channel; rows 3..15 zero), k = 32*hc + 8*(lane >> 4) + j
+  // the 9 x CIN x 3 weights pass through LDS (coalesced loads into the second halo buffer, free
+  // until step 0's commit): per lane 144 scattered 4-B loads with 13 of 16 lanes idle were a
+  // measurable share of each strip
   bf16x8 wa[9][NH];
   const int n = lane & 15, kg = lane >> 4;
+  {
+    static_assert(9 * CIN * 3 * 4 <= (int)sizeof(tile[1]), "weights fit the halo buffer");
+    float* sw = reinterpret_cast<float*>(tile[1]);
+    for (int i = tid; i < 9 * CIN * 3; i += 256) sw[i] = w[i];
+    __syncthreads();
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int hc = 0; hc < NH; ++hc)
+      for (int hc = 0; hc < NH; ++hc)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        wa[tap][hc][j] = (bf16)(n < 3 ? w[(tap * CIN + 32 * hc + 8 * kg + j) * 3 + n] : 0.f);
+        for (int j = 0; j < 8; ++j)
+          wa[tap][hc][j] = (bf16)(n < 3 ? sw[(tap * CIN + 32 * hc + 8 * kg + j) * 3 + n] : 0.f);
+  }
   const float bo[3] = {bias[0], bias[1], bias[2]};
   // halo chunk (rows y0-1 .. y0+4, channels ck*CC ..; reflect-padded, clamped past the image
   // edge) into registers; written to LDS after the current chunk's MFMAs
-  bf16x8 st[PER];
-  auto fetch = [&](int y0, int ck) {
+  // two register sets: the loads of step s + 2 are issued at step s (set s & 1), so every chunk has
+  // two steps of MFMA work to arrive in (one step did not cover the load latency: 2.7 TB/s)
+  bf16x8 sts[2][PER];
+  auto fetch = [&](bf16x8 (&st)[PER], int y0, int ck) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = min(tid + 256 * i, NCH - 1);
@@ -522,7 +534,7 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
       st[i] = *reinterpret_cast<const bf16x8*>(xb + ((long long)Y * W + X) * CIN + ck * CC + ch * 8);
     }
   };
-  auto commit = [&](bf16* t) {
+  auto commit = [&](const bf16x8 (&st)[PER], bf16* t) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + 256 * i;
@@ -532,9 +544,15 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
       }
     }
   };
-  const int nt = min(kOut3Rows, (H - ys + TR - 1) / TR);
-  fetch(ys, 0);
-  commit(tile[0]);
+  const int nt = min(kOut3RowsM, (H - ys + TR - 1) / TR);
+  // step s = (tile r, chunk ck), s = NCK r + ck; rows of step s: ys + (s / NCK) TR, clamped past
+  // the strip.  NCK == 2: the register set alternates with the chunk index (compile-time); NCK == 1
+  // (CIN = 32): one set, loaded one step ahead
+  constexpr bool TWO = NCK == 2;
+  auto step_y = [&](int s2) { return ys + min(s2 / NCK, nt - 1) * TR; };
+  fetch(sts[0], ys, 0);
+  commit(sts[0], tile[0]);
+  if constexpr (TWO) fetch(sts[1], step_y(1), 1);
   __syncthreads();
   int buf = 0;
   for (int r = 0; r < nt; ++r) {
@@ -545,8 +563,13 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
 #pragma unroll
     for (int ck = 0; ck < NCK; ++ck) {
       const bf16* t = tile[buf];
-      const bool more = ck + 1 < NCK || r + 1 < nt;
-      if (more) fetch(ck + 1 < NCK ? ys + r * TR : ys + (r + 1) * TR, (ck + 1) % NCK);
+      const int s2 = r * NCK + ck;
+      const bool more = s2 + 1 < nt * NCK;
+      if constexpr (TWO) {
+        if (s2 + 2 < nt * NCK) fetch(sts[ck], step_y(s2 + 2), ck);  // step s + 2 has this step's chunk index
+      } else {
+        if (more) fetch(sts[0], step_y(s2 + 1), 0);
+      }
 #pragma unroll
       for (int g = 0; g < TC / 16; ++g) {
 #pragma unroll
@@ -573,7 +596,7 @@ __global__ void __launch_bounds__(256) conv_out3_mfma_kernel(const bf16* __restr
           }
         }
       }
-      if (more) commit(tile[buf ^ 1]);
+      if (more) commit(sts[TWO ? ck ^ 1 : 0], tile[buf ^ 1]);
       __syncthreads();
       buf ^= 1;
     }
@@ -917,7 +940,7 @@ extern "C" int mhada_conv3x3_out3(const void* x, int dtype, const float* w, cons
   hipStream_t s = (hipStream_t)s_;
   // bf16, Cin 32/64: the MFMA tile kernel (tuning out3_mfma = 0 selects the per-pixel VALU kernel)
   if (dtype == MHADA_BF16 && tuning().out3_mfma && (Cin == 32 || Cin == 64)) {
-    const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3Rows - 1) / (4 * kOut3Rows);
+    const int tiles_x = (W + 63) / 64, strips_y = (H + 4 * kOut3RowsM - 1) / (4 * kOut3RowsM);
     const long long nb = (long long)B * strips_y * tiles_x;
     if (nb >= (1LL << 31)) return fail("mhada_conv3x3_out3: grid too large");
     const dim3 g((unsigned)nb);
