@@ -36,6 +36,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace mhada {
 
@@ -51,6 +52,7 @@ struct TnP {
   float* cslab;                           // [splits][M] column sums of A (null: none)
   int kchunk, tiles_n;
   int nb; long long sza, szb;             // batch (blockIdx.z): A / B element strides; slabs [S][nb][M][N]
+  int rsrc;                               // ROWS, 16-B A rows: loads through per-stage buffer resources
 };
 
 constexpr int kTnBN = 128, kTnBK = 32;
@@ -63,8 +65,9 @@ MHADA_DEV int tn_reflect(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2
 // VEC_A: A rows are 16-B aligned with M % 4 == 0 (else element loads, e.g. the 3-channel layer).
 // BM = 128 (M >= 128) or 64 (the 64-channel layers: no half-empty M tiles); waves 2 x 2, each
 // (BM/2) x 64 of the output.
-template <int BMODE, bool VEC_A, int BM>
+template <int BMODE, bool VEC_A, int BM, bool RS = false>
 __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
+  static_assert(!RS || (BMODE == MHADA_A_ROWS && VEC_A), "buffer-resource loads: ROWS, 16-B A rows");
   constexpr int TMW = BM / 64;   // 32-row MFMA blocks per wave
   constexpr int ACH = BM / 32;   // A chunks (16 B) staged per thread per K-stage
   __shared__ __attribute__((aligned(16))) float sA[2][kTnBK][BM];
@@ -112,7 +115,38 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       cxx[i] = rem - cyy[i] * p.out_w;
     }
   }
+  // ROWS with 16-B A rows (p.rsrc, the linears' weight gradients): A and B through buffer resources
+  // rebuilt per K-stage in scalar registers over the stage's rows; every lane's offset is a loop
+  // constant (columns past M / N at an out-of-range offset read 0), so a stage's loads cost no
+  // vector address arithmetic and no per-lane branch — an fp32 MFMA holds its SIMD's vector issue
+  // for its whole 64 cycles (profiles/r05_f32mfma_fill.log), every VALU instruction adds to the loop
+  int avo[ACH], bvo[4];
+  if constexpr (RS) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + 256 * i, m = m0 + 4 * (c % (BM / 4));
+      avo[i] = m < p.M ? (int)(((long long)(c / (BM / 4)) * p.lda + m) * 4) : 0x7ff00000;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bvo[i] = bcol_ok ? (int)(((long long)(row0 + 8 * i) * p.ldb + n0 + col) * 4) : 0x7ff00000;
+  }
   auto issue = [&](int k0) {
+    if constexpr (RS) {
+      {
+        const int rows = min(kend - k0, kTnBK);
+        const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(pa + (long long)k0 * p.lda), 0, (int)(rows * p.lda * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(pb + (long long)k0 * p.ldb), 0, (int)(rows * p.ldb * 4), 0x00020000);
+#pragma unroll
+        for (int i = 0; i < ACH; ++i)
+          ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, avo[i], 0, 0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(br, bvo[i], 0, 0));
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {  // A: chunk c = tid + 256 i -> row c / (BM/4), 4 columns at 4 (c % (BM/4))
       const int c = tid + 256 * i;
@@ -204,8 +238,10 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
     commit(0);
   }
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
+  // one K-stage on LDS buffer BUF (a compile-time constant: the loop runs two stages per
+  // iteration, so every LDS address is a per-lane base plus an immediate)
+  auto stage = [&](int st, auto bufc) __attribute__((always_inline)) {
+    constexpr int buf = decltype(bufc)::value;
     const bool more = st + 1 < nst;
     if (more) issue(kbeg + (st + 1) * kTnBK);
 #pragma unroll
@@ -227,7 +263,13 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(const TnP p) {
       commit(buf ^ 1);
     }
     __syncthreads();
+  };
+  int st = 0;
+  for (; st + 1 < nst; st += 2) {
+    stage(st, std::integral_constant<int, 0>());
+    stage(st + 1, std::integral_constant<int, 1>());
   }
+  if (st < nst) stage(st, std::integral_constant<int, 0>());
 
   if (csum) {  // the 256 / (BM/4) threads of one column quad, summed in thread order through LDS
     f32x4* part = reinterpret_cast<f32x4*>(&sA[0][0][0]);
@@ -1066,6 +1108,9 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
     return fail("mhada_gemm_tn: batched form needs ROWS mode, M > 4, ldc == N, 16-B batch strides");
   if (p.nb > 65535) return fail("mhada_gemm_tn: batch too large");
   const bool vec_a = al16(a->a) && a->lda % 4 == 0 && a->M % 4 == 0;
+  // per-stage buffer resources: 32 rows of A / B and the out-of-range offset must stay below 2^31 bytes
+  p.rsrc = vec_a && a->b_mode == MHADA_A_ROWS && (long long)kTnBK * std::max(a->lda, a->ldb) * 4 < 0x7ff00000LL &&
+           (long long)kTnBK * std::max(a->lda, a->ldb) * 4 <= 0x7fffffffLL;
   switch (a->b_mode) {
     case MHADA_A_ROWS:
       if (a->ldb % 4) return fail("mhada_gemm_tn: ldb must be a multiple of 4");
@@ -1130,6 +1175,10 @@ extern "C" int mhada_gemm_tn(const mhada_gemm_tn_args* a, float* work, long long
 #define TN_LAUNCH(MODE)                                                                             \
   do {                                                                                              \
     if (p.M <= 4) hipLaunchKernelGGL((tn_skinny_kernel<MODE>), gsk, dim3(256), 0, s, p);           \
+    else if (MODE == MHADA_A_ROWS && p.rsrc && bm == 64)                                            \
+      hipLaunchKernelGGL((gemm_tn_kernel<MHADA_A_ROWS, true, 64, true>), grid, dim3(256), 0, s, p); \
+    else if (MODE == MHADA_A_ROWS && p.rsrc)                                                        \
+      hipLaunchKernelGGL((gemm_tn_kernel<MHADA_A_ROWS, true, 128, true>), grid, dim3(256), 0, s, p); \
     else if (bm == 64 && vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true, 64>), grid, dim3(256), 0, s, p); \
     else if (bm == 64) hipLaunchKernelGGL((gemm_tn_kernel<MODE, false, 64>), grid, dim3(256), 0, s, p); \
     else if (vec_a) hipLaunchKernelGGL((gemm_tn_kernel<MODE, true, 128>), grid, dim3(256), 0, s, p); \
