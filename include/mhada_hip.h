@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 13 (mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 14 (mhada_cosine_moments / mhada_cosine_attn; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -175,6 +175,23 @@ int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns
 int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
                const float* fcs_mu, const float* fcs_rstd, const float* v_mu, void* out,
                int dtype, int B, int H, int Nc, int Ns, int activation, mhada_stream_t stream);
+
+/* The cosine activation (CosineSimilarity, adaDecoder.py:20-34) in its linear form (ABI 14):
+ * A[i][j] = (q^_i.k^_j + 1) / l_i with l_i = q^_i.sum_j k^_j + Ns, so A V' and A V'^2 need only the
+ * style-side moments — O(N d^2) instead of mhada_attn's Nc x Ns loop.  After mhada_cosine_prep:
+ * mhada_cosine_moments reduces the normalised K half of kv [B][H][Ns][128] and vt
+ * [B][H][128][ceil64(Ns)] (mhada_transpose_v layout) over the keys into mom [B][H][65][132] fp32:
+ *   mom[d][o] = sum_n k^[n][d] vt[o][n] (d < 64, o < 128), mom[d][128] = sum_n k^[n][d],
+ *   mom[64][o] = sum_n vt[o][n], mom[64][128] = Ns, other entries 0;
+ * splits > 1 splits the keys over that many workgroups per (b, h) with a fixed-order sum
+ * (work: splits*B*H*65*132 floats; splits == 1 may pass work = NULL).  Once per style.
+ * mhada_cosine_attn: per query, M' = (q^.mom[:, o<64] + mom[64][o]) / l, E2' likewise with o + 64,
+ * out = sqrt(max(E2' - M'^2, 1e-6)) * IN(fcs) + M' + v_mu — mhada_attn's arguments and output. */
+int mhada_cosine_moments(const void* kv, const void* vt, int dtype, int B, int H, int Ns, float* mom,
+                         float* work, int splits, mhada_stream_t stream);
+int mhada_cosine_attn(const void* q, const float* mom, const float* fcs, const float* fcs_mu,
+                      const float* fcs_rstd, const float* v_mu, void* out, int dtype, int B, int H,
+                      int Nc, mhada_stream_t stream);
 
 /* MHAda attention for training (adaDecoder.py:186-198 under train_image.py:139 autograd), fp32,
  * one (batch, head) per leading index, all rows of 64 (or 128) contiguous floats:

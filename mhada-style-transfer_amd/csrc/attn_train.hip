@@ -399,7 +399,6 @@ __global__ void __launch_bounds__(64 * NW, OCC) attn_train_dkv_kernel(const Trai
   // dS rows of this (b, h): offsets past num_records (rows >= Nc, or a key >= Ns, whose lanes
   // add (Nc + 32) rows) are dropped; unsigned offsets < 2 (Nc + 32) Ns * 4 < 2^32 (entry check)
   const unsigned dkey = kv ? key * 4u : (unsigned)(p.Nc + TT) * p.Ns * 4;
-  const unsigned dvo = 4u * h * p.Ns * 4 + dkey;  // + the row's soffset: past the spill for key >= Ns
   const __amdgpu_buffer_rsrc_t dsr =
       __builtin_amdgcn_make_buffer_rsrc(SPILL ? p.ds + bh * p.Nc * p.Ns : nullptr, 0,
                                         SPILL ? p.Nc * p.Ns * 4 : 0, 0x00020000);

@@ -67,6 +67,8 @@ SIGNATURES = {
     "mhada_fold_block": (_I, [_vp] * 12 + [_F, _I, _I, _I, _vp]),
     "mhada_transpose_v": (_I, [_vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_cosine_prep": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_cosine_moments": (_I, [_vp, _vp, _I, _I, _I, _I, _vp, _vp, _I, _vp]),
+    "mhada_cosine_attn": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
@@ -137,7 +139,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 def get_tuning(name: str) -> int:

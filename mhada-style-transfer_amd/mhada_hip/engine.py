@@ -243,8 +243,9 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
     C = H * HEAD_DIM
     B, Nc, Cc = fc.t.shape
     cached = bool(side)
+    mom = None
     if cached:
-        mu_s, rstd_s, kv, vt = side["mu_s"], side["rstd_s"], side["kv"], side["vt"]
+        mu_s, rstd_s, kv, vt, mom = side["mu_s"], side["rstd_s"], side["kv"], side["vt"], side.get("mom")
         if kv.shape[0] != B:
             raise ValueError(f"cached style batch {kv.shape[0]} != content batch {B}")
     else:
@@ -276,13 +277,18 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
                  ldc=2 * HEAD_DIM, sc=(H * Ns * 2 * HEAD_DIM, Ns * 2 * HEAD_DIM),
                  vt=vt, ldt=ldt, svt=(H * 2 * HEAD_DIM * ldt, 2 * HEAD_DIM * ldt))
         if act == ACT_COSINE:
+            # the cosine activation's linear form: the style-side moments replace the Nc x Ns loop
             ops.cosine_prep(None, kv)
+            mom = ops.cosine_moments(kv, vt)
         if side is not None:
-            side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt)
+            side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt, mom=mom)
     if act == ACT_COSINE:
         ops.cosine_prep(q, None)
-    with _timed("mhada_attn"):
-        att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
+        with _timed("mhada_attn"):
+            att = ops.cosine_attn(q, mom, fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] dt
+    else:
+        with _timed("mhada_attn"):
+            att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
     out = torch.empty(B * Nc, C, device=dev, dtype=torch.float32)
     t16 = torch.empty(B * Nc, C, device=dev, dtype=torch.bfloat16) if want_bf16 else None
     ops.gemm(a=att.view(B * Nc, C), w=prep["w_out"], c=out, M=B * Nc, N=C, K=C, compute=dt, lda=C, ldw=C,

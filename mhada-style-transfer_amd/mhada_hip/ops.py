@@ -441,6 +441,35 @@ def cosine_prep(q: Optional[torch.Tensor], kv: Optional[torch.Tensor]) -> None:
     _call("mhada_cosine_prep", ref, _ptr(q), _ptr(kv), dt_code(ref.dtype), B, H, Nc, Ns)
 
 
+def cosine_moments(kv: torch.Tensor, vt: torch.Tensor) -> torch.Tensor:
+    """``mhada_cosine_moments``: the style-side moments [B][H][65][132] fp32 of the linear cosine
+    activation from the normalised K half of kv and the V'^T | V'^2^T image vt.  The keys are split
+    so that about 512 workgroups run (fixed-order sum of the splits: deterministic)."""
+    _need_gpu(kv, vt)
+    B, H, Ns, _ = kv.shape
+    if vt.shape != (B, H, 128, (Ns + 63) // 64 * 64) or vt.dtype != kv.dtype:
+        raise ValueError(f"cosine_moments: vt {tuple(vt.shape)} does not match kv {tuple(kv.shape)}")
+    splits = max(1, min((Ns + 63) // 64, -(-512 // (B * H))))
+    mom = torch.empty(B, H, 65, 132, device=kv.device, dtype=torch.float32)
+    work = torch.empty(splits, B * H * 65 * 132, device=kv.device, dtype=torch.float32) if splits > 1 else None
+    _call("mhada_cosine_moments", kv, kv.data_ptr(), vt.data_ptr(), dt_code(kv.dtype), B, H, Ns, mom.data_ptr(),
+          _ptr(work), splits)
+    return mom
+
+
+def cosine_attn(q, mom, fcs, fcs_mu, fcs_rstd, v_mu) -> torch.Tensor:
+    """``mhada_cosine_attn``: mhada_attn's output for the cosine activation from normalised q and
+    the style moments of cosine_moments."""
+    _need_gpu(q, mom, fcs, fcs_mu, fcs_rstd, v_mu)
+    B, H, Nc, _ = q.shape
+    if mom.shape != (B, H, 65, 132) or mom.dtype != torch.float32:
+        raise ValueError(f"cosine_attn: mom {tuple(mom.shape)} does not match q {tuple(q.shape)}")
+    out = torch.empty(B, Nc, H * 64, device=q.device, dtype=q.dtype)
+    _call("mhada_cosine_attn", q, q.data_ptr(), mom.data_ptr(), fcs.data_ptr(), fcs_mu.data_ptr(),
+          fcs_rstd.data_ptr(), v_mu.data_ptr(), out.data_ptr(), dt_code(q.dtype), B, H, Nc)
+    return out
+
+
 def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch.Tensor:
     _need_gpu(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu)
     B, H, Nc, _ = q.shape

@@ -405,6 +405,46 @@ def test_mhada_block(dt, act, B, hc, wc, hs, ws):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,Nc,Ns", [(1, 1, 5, 3), (2, 3, 100, 97), (1, 2, 130, 5000), (2, 8, 4096, 4096)])
+def test_cosine_linear_form(dt, B, H, Nc, Ns):
+    """mhada_cosine_moments + mhada_cosine_attn (the cosine activation's O(N d^2) form,
+    adaDecoder.py:20-34) against an fp64 evaluation of the reference's quadratic expression on the
+    same normalised operands, and against the flash kernel (mhada_attn ACT_COSINE).  Ragged Ns
+    (97, 5000: a partial last 64-key tile, several key splits), the bf16 key permutation of vt,
+    Nc not a multiple of 64.  Tolerance: fp32 2e-5 (summation order only); bf16 1e-2 (bf16 q, k,
+    V', V'^2 operands and output)."""
+    C = 64 * H
+    q = rnd(B, H, Nc, 64, seed=1, dtype=dt)
+    kv = rnd(B, H, Ns, 128, seed=2, dtype=dt)
+    vt = ops.transpose_v(kv)
+    ops.cosine_prep(q, kv)
+    fcs = rnd(B, Nc, C, seed=3)
+    mu = rnd(B, C, seed=4, scale=0.1)
+    rs = rnd(B, C, seed=5).abs() + 0.5
+    vmu = rnd(B, C, seed=6)
+    mom = ops.cosine_moments(kv, vt)
+    out = ops.cosine_attn(q, mom, fcs, mu, rs, vmu)
+    flash = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, _lib.ACT_COSINE)
+    torch.cuda.synchronize()
+    # fp64 reference: A = (q^ k^T + 1) / rowsum, M = A V', E2 = A V'^2 (the operands as the kernels see them)
+    qd, kd, vd = q.double(), kv[..., :64].double(), kv[..., 64:].double()
+    a = torch.matmul(qd, kd.transpose(-1, -2)) + 1
+    a = a / a.sum(-1, keepdim=True)
+    m = torch.matmul(a, vd)
+    e2 = torch.matmul(a, vd * vd)
+    s = torch.sqrt((e2 - m * m).clamp(min=1e-6))
+    x = (fcs.double().view(B, Nc, H, 64).permute(0, 2, 1, 3) - mu.double().view(B, H, 1, 64)) * \
+        rs.double().view(B, H, 1, 64)
+    ref = (s * x + m + vmu.double().view(B, H, 1, 64)).permute(0, 2, 1, 3).reshape(B, Nc, C)
+    assert torch.isfinite(out.float()).all()
+    assert rel(out, ref) < TOL[dt]
+    assert rel(out, flash) < 2 * TOL[dt]
+    # the style-side image: row 64 column 128 carries Ns, the padding columns are zero
+    assert torch.all(mom[..., 64, 128] == Ns)
+    assert torch.all(mom[..., :, 129:] == 0) and torch.all(mom[..., 64, :128].isfinite())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_mhada_online_softmax_rescale_branch(dt):
     """Force the running max to jump in a LATE key tile (cdna_hip_programming.md rule 26):
     one style token far out along the content direction dominates every query."""

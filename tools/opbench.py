@@ -1,6 +1,6 @@
 """Per-op microbenchmarks on the GPU (interleaved rounds in one process, median of rounds).
 
-    python tools/opbench.py [gemm|conv|attn|all]     (attn: tools/attn_ab.py)
+    python tools/opbench.py [gemm|conv|attn|cosine|all]     (attn: tools/attn_ab.py)
 
 GEMM shapes are the forward path's (1024^2 batch 4 -> M = 65536 tokens); hipBLASLt via
 torch.matmul is timed beside ours on the same operands as a calibration point.
@@ -232,6 +232,27 @@ def proj_suite():
             f"{k} {v * 1e3:6.1f} us {(kb if k.startswith('kv') else qb) / v / 1e6:6.0f} GB/s" for k, v in t.items()))
 
 
+def cosine_suite():
+    """The cosine activation: the flash loop (mhada_attn ACT_COSINE) vs the linear form
+    (mhada_cosine_moments once per style + mhada_cosine_attn per call) at the bench shapes."""
+    from mhada_hip import _lib
+    dev = "cuda"
+    for B, N, dt in ((8, 4096, torch.float32), (4, 16384, torch.bfloat16)):
+        H, C = 8, 512
+        q = torch.randn(B, H, N, 64, device=dev).to(dt)
+        kv = torch.randn(B, H, N, 128, device=dev).to(dt)
+        vt = ops.transpose_v(kv)
+        ops.cosine_prep(q, kv)
+        fcs = torch.randn(B, N, C, device=dev)
+        mu, rs, vmu = torch.zeros(B, C, device=dev), torch.ones(B, C, device=dev), torch.zeros(B, C, device=dev)
+        mom = ops.cosine_moments(kv, vt)
+        fns = {"flash": lambda: ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, _lib.ACT_COSINE),
+               "moments": lambda: ops.cosine_moments(kv, vt),
+               "apply": lambda: ops.cosine_attn(q, mom, fcs, mu, rs, vmu)}
+        t = bench(fns, rounds=5, iters=3)
+        print(f"cosine {str(dt)[6:]:8s} B{B} N{N}: " + "  ".join(f"{k} {v * 1e3:8.1f} us" for k, v in t.items()))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     torch.manual_seed(0)
@@ -247,6 +268,8 @@ if __name__ == "__main__":
         n64_suite()
     if what == "proj":
         proj_suite()
+    if what == "cosine":
+        cosine_suite()
     if what in ("conv", "all"):
         conv_suite()
     if what in ("out3", "conv", "all"):
