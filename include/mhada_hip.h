@@ -40,7 +40,7 @@ enum {
                               the input gradient of a padded 3x3 conv)                   */
 };
 
-int mhada_abi_version(void);  /* 14 (mhada_cosine_moments / mhada_cosine_attn; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 14 (mhada_cosine_moments / mhada_cosine_attn, mhada_warp_bwd; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -244,6 +244,13 @@ int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H, int W, int
  * displacement, pixels); padding 0 = "zeros", 1 = "border". */
 int mhada_warp(const float* x, const float* flow, float* y, int B, int C, int H, int W,
                int padding, mhada_stream_t stream);
+
+/* Adjoint of mhada_warp w.r.t. x (ABI 14; train_video.py:147-151 temporal losses under
+ * autograd): gx += W^T gy, i.e. each output pixel's gradient scattered to its four bilinear taps
+ * with the forward's weights (fp32 atomics, as ATen's grid_sampler_2d_backward).  gx must be
+ * initialised by the caller (zeros); the flow receives no gradient.  Shapes as mhada_warp. */
+int mhada_warp_bwd(const float* gy, const float* flow, float* gx, int B, int C, int H, int W,
+                   int padding, mhada_stream_t stream);
 
 /* flow_warp_mask (utilities.py:121-151): mask [H][W] = 1 where the forward flow flo01 warped
  * back by flo10 returns within `threshold` (L1, pixels) of the start, else 0.  flo01, flo10

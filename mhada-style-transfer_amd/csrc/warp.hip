@@ -6,6 +6,7 @@
 // fp32 operation order as the reference's tensor ops and ATen's grid_sampler (unnormalise,
 // floor, the four corner weights, taps accumulated nw, ne, sw, se; zero padding skips
 // out-of-range taps, border padding clamps the coordinate first).
+// warp_bwd: the adjoint w.r.t. the warped image, for the temporal losses of train_video.py.
 // flow_warp_mask (utilities.py:121-151): forward-backward consistency of two flows.
 // warp_l1 (exps_sintel.py:101-109): sum(mask * |cs2 - warp(cs1, flow)|) per image, the
 // warping-error metric, fused so the warped frame never reaches HBM; fixed-order fp64
@@ -78,6 +79,34 @@ __global__ void __launch_bounds__(256) warp_kernel(const float* __restrict__ x, 
   const float* xb = x + (long long)b * C * HW;
   float* yb = y + (long long)b * C * HW;
   for (int c = 0; c < C; ++c) yb[c * HW + pix] = sample(xb + c * HW, t, W);
+}
+
+// Adjoint of warp w.r.t. x (the temporal losses of train_video.py:147-151 under autograd):
+// gx[tap] += w_tap * gy[pix] over the four taps of every output pixel — the scatter of ATen's
+// grid_sampler_2d_backward (hardware fp32 atomics there too, so the summation order at a tap hit
+// by several pixels is not fixed, in the reference either).  The flow is data in train_video.py
+// and gets no gradient.  Grid (pixel blocks, channel groups of cpg, B); zero gradients skipped.
+__global__ void __launch_bounds__(256) warp_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ flow,
+                                                       float* __restrict__ gx, int C, int H, int W, int padding,
+                                                       int cpg) {
+  const int b = blockIdx.z;
+  const long long HW = (long long)H * W;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= HW) return;
+  const int py = (int)(pix / W), px = (int)(pix - (long long)py * W);
+  const float* fl = flow + (long long)b * 2 * HW;
+  const Tap t = warp_tap(px, py, fl[pix], fl[HW + pix], H, W, padding);
+  const long long o = (long long)t.y0 * W + t.x0;
+  const int c0 = blockIdx.y * cpg, c1 = min(C, c0 + cpg);
+  for (int c = c0; c < c1; ++c) {
+    const float g = gy[((long long)b * C + c) * HW + pix];
+    if (g == 0.f) continue;
+    float* plane = gx + ((long long)b * C + c) * HW;
+    if (t.inw) unsafeAtomicAdd(plane + o, t.wnw * g);
+    if (t.ine) unsafeAtomicAdd(plane + o + 1, t.wne * g);
+    if (t.isw) unsafeAtomicAdd(plane + o + W, t.wsw * g);
+    if (t.ise) unsafeAtomicAdd(plane + o + W + 1, t.wse * g);
+  }
 }
 
 // grid + flo01 sampled at grid + flo10 (zero padding), L1 distance to the grid < threshold.
@@ -157,6 +186,18 @@ extern "C" int mhada_warp(const float* x, const float* flow, float* y, int B, in
   hipLaunchKernelGGL(warp_kernel, dim3((unsigned)((HW + 255) / 256), B), dim3(256), 0, (hipStream_t)s_, x, flow, y, C,
                      H, W, padding);
   return check_launch("mhada_warp");
+}
+
+extern "C" int mhada_warp_bwd(const float* gy, const float* flow, float* gx, int B, int C, int H, int W, int padding,
+                              mhada_stream_t s_) {
+  if (!gy || !flow || !gx || B <= 0 || C <= 0 || H <= 0 || W <= 0 || B > 65535)
+    return fail("mhada_warp_bwd: bad args");
+  if (padding != 0 && padding != 1) return fail("mhada_warp_bwd: padding must be 0 (zeros) or 1 (border)");
+  const long long HW = (long long)H * W;
+  constexpr int kCpg = 16;
+  const dim3 grid((unsigned)((HW + 255) / 256), (unsigned)((C + kCpg - 1) / kCpg), B);
+  hipLaunchKernelGGL(warp_bwd_kernel, grid, dim3(256), 0, (hipStream_t)s_, gy, flow, gx, C, H, W, padding, kCpg);
+  return check_launch("mhada_warp_bwd");
 }
 
 extern "C" int mhada_flow_warp_mask(const float* flo01, const float* flo10, float* mask, int H, int W, float threshold,

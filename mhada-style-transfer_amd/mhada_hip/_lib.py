@@ -78,6 +78,7 @@ SIGNATURES = {
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_upsample2x": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_warp": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
+    "mhada_warp_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_flow_warp_mask": (_I, [_vp, _vp, _vp, _I, _I, _F, _I, _vp]),
     "mhada_warp_l1": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_frame_ingest": (_I, [_vp, _I, _I, _I, _c_ll, _I, _vp, _I, _I, _vp]),

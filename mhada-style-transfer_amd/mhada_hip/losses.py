@@ -62,12 +62,21 @@ def warp(x: torch.Tensor, flo: torch.Tensor, padding_mode: str = "zeros") -> tor
                          align_corners=False)
 
 
+def _warp(x: torch.Tensor, flo: torch.Tensor) -> torch.Tensor:
+    """warp as the temporal losses call it: on a ROCm device the HIP kernel and its HIP adjoint
+    (video.warp), on the CPU the reference expression above."""
+    if x.is_cuda:
+        from .video import warp as device_warp
+        return device_warp(x, flo)
+    return warp(x, flo)
+
+
 def output_level_temporal_loss(c1, c2, cs1, cs2, flow, mask, loss_matrix):
     """lossfn.py:50-66"""
-    input_term = c2 - warp(c1, flow)
+    input_term = c2 - _warp(c1, flow)
     input_term = 0.2126 * input_term[:, 0] + 0.7152 * input_term[:, 1] + 0.0722 * input_term[:, 2]
     input_term = input_term.unsqueeze(1).expand(-1, c2.shape[1], -1, -1)
-    output_term = cs2 - warp(cs1, flow)
+    output_term = cs2 - _warp(cs1, flow)
     m = mask.unsqueeze(1).expand(-1, c2.shape[1], -1, -1)
     loss = torch.sum(m * loss_matrix(output_term, input_term))
     return loss * (1 / torch.nonzero(m).shape[0])
@@ -78,7 +87,7 @@ def feature_level_temporal_loss(f1, f2, flow, mask, loss_matrix):
     feature_flow = F.interpolate(flow, size=f1.shape[2:], mode="bilinear")
     feature_flow[:, 0] *= float(f1.shape[3]) / flow.shape[3]
     feature_flow[:, 1] *= float(f1.shape[2]) / flow.shape[2]
-    warped = warp(f1, feature_flow)
+    warped = _warp(f1, feature_flow)
     fm = F.interpolate(mask.unsqueeze(1), size=f1.shape[2:], mode="bilinear").squeeze(1)
     fm = (fm > 0).float().unsqueeze(1).expand(-1, f1.shape[1], -1, -1)
     loss = torch.sum(fm * loss_matrix(f2, warped))

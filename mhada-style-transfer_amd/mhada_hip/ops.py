@@ -618,6 +618,18 @@ def warp(x: torch.Tensor, flow: torch.Tensor, padding_mode: str = "zeros") -> to
     return y
 
 
+def warp_bwd(gy: torch.Tensor, flow: torch.Tensor, padding_mode: str = "zeros") -> torch.Tensor:
+    """``mhada_warp_bwd``: the gradient of warp(x, flow) w.r.t. x for the output gradient gy."""
+    _need_gpu(gy, flow)
+    gy, flow = _f32c(gy, "gy"), _f32c(flow, "flow")
+    B, C, H, W = gy.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"flow must be [B,2,H,W] = {[B, 2, H, W]}, got {list(flow.shape)}")
+    gx = torch.zeros_like(gy)
+    _call("mhada_warp_bwd", gy, gy.data_ptr(), flow.data_ptr(), gx.data_ptr(), B, C, H, W, _padding_code(padding_mode))
+    return gx
+
+
 def flow_warp_mask(flo01: torch.Tensor, flo10: torch.Tensor, padding_mode: str = "zeros",
                    threshold: float = 2) -> torch.Tensor:
     """``mhada_flow_warp_mask``: flo01, flo10 [2][H][W] -> mask [H][W] (utilities.py:121-151)."""

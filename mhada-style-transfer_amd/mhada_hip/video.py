@@ -9,9 +9,8 @@
 * ``VideoStylizer`` — the infer_video.py:58-92 loop: the style is encoded once and, through the
   AdaFormer's per-style cache (engine.style_cache), its K/V projections are reused per frame.
 
-The inference forms run the HIP kernels (csrc/warp.hip).  When autograd needs a gradient
-through the warp (train_video.py temporal losses) ``warp`` evaluates the same expression with
-differentiable device ops (mhada_hip.losses.warp).
+The inference forms run the HIP kernels (csrc/warp.hip); the gradient through the warp w.r.t. the
+image (train_video.py temporal losses) runs its HIP adjoint (WarpFn / mhada_warp_bwd).
 """
 from __future__ import annotations
 
@@ -22,10 +21,31 @@ import torch
 from . import losses, ops
 
 
+class WarpFn(torch.autograd.Function):
+    """utilities.warp under autograd w.r.t. the image (train_video.py:147-151): forward mhada_warp,
+    backward its adjoint mhada_warp_bwd.  The flow is data there (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, flo, padding_mode):
+        ctx.save_for_backward(flo)
+        ctx.padding_mode = padding_mode
+        return ops.warp(x, flo, padding_mode)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (flo,) = ctx.saved_tensors
+        return ops.warp_bwd(gy, flo, ctx.padding_mode), None, None
+
+
 def warp(x: torch.Tensor, flo: torch.Tensor, padding_mode: str = "zeros") -> torch.Tensor:
-    """utilities.warp: bilinear backward warp of x [B,C,H,W] by flow flo [B,2,H,W]."""
-    if torch.is_grad_enabled() and (x.requires_grad or flo.requires_grad):
+    """utilities.warp: bilinear backward warp of x [B,C,H,W] by flow flo [B,2,H,W].  On the device:
+    the HIP kernel, with its HIP adjoint when x takes a gradient.  A flow that takes a gradient
+    (no reference script differentiates through the flow) evaluates the reference expression with
+    differentiable device ops (mhada_hip.losses.warp)."""
+    if torch.is_grad_enabled() and flo.requires_grad:
         return losses.warp(x, flo, padding_mode)
+    if torch.is_grad_enabled() and x.requires_grad:
+        return WarpFn.apply(x, flo, padding_mode)
     return ops.warp(x, flo, padding_mode)
 
 

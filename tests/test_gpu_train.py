@@ -7,12 +7,18 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from mhada_hip.recipe import seeded_image
-from mhada_hip.train import Trainer
-from test_train_cpu import build, check_against_golden
+from mhada_hip.train import Trainer, VideoTrainer
+from test_train_cpu import build, check_against_golden, check_video_against_golden
 
 
 def test_train_step_matches_reference_golden_gpu():
     check_against_golden(Trainer(*build("cuda")), "cuda")
+
+
+def test_video_train_step_matches_reference_golden_gpu():
+    """One train_video.py step (5 AdaFormer calls, temporal losses with the warp and its adjoint on
+    HIP) against the reference's own composition of it (tests/golden/make_video_train_goldens.py)."""
+    check_video_against_golden(VideoTrainer(*build("cuda")), "cuda")
 
 
 def test_train_step_256_b2_losses_match_oracle_and_grads_match_cpu():

@@ -157,6 +157,38 @@ def test_warp_autograd_and_errors():
         video.warp(x.detach().cpu(), flow.cpu())
 
 
+@pytest.mark.parametrize("B,C,H,W,amp", [(2, 3, 37, 53, 6.0), (2, 512, 32, 32, 3.0), (1, 64, 135, 240, 12.0)])
+@pytest.mark.parametrize("pad", ["zeros", "border"])
+def test_warp_adjoint_matches_grid_sample_backward(B, C, H, W, amp, pad):
+    """mhada_warp_bwd (the image gradient of utilities.warp, train_video.py temporal losses) against
+    ATen's grid_sample backward of the reference expression in fp64, directly (ops.warp_bwd) and
+    through autograd (video.warp -> WarpFn), with zero output gradients on some rows (skipped
+    taps) and flows reaching out of the image (zero / border padding).  Tolerance: 1e-5 relative,
+    or 1.5x ATen's own fp32 backward error where fp32 sample coordinates (W = 240, 12 px flows)
+    alone put it above that."""
+    from mhada_hip import ops
+    gen = torch.Generator(device="cpu").manual_seed(B * C + H)
+    x = torch.rand(B, C, H, W, generator=gen).to(DEV)
+    flow = ((torch.rand(B, 2, H, W, generator=gen) - 0.5) * 2 * amp).to(DEV)
+    gy = torch.randn(B, C, H, W, generator=gen).to(DEV)
+    gy[:, :, ::5] = 0
+    xr = x.double().requires_grad_(True)
+    (L.warp(xr, flow.double(), pad) * gy.double()).sum().backward()
+    ref = xr.grad
+    x32 = x.clone().requires_grad_(True)
+    (L.warp(x32, flow, pad) * gy).sum().backward()
+    tol = max(1e-5, 1.5 * float((x32.grad.double() - ref).norm() / ref.norm()))
+    got = ops.warp_bwd(gy, flow, pad)
+    assert float((got.double() - ref).norm() / ref.norm()) < tol
+    xa = x.clone().requires_grad_(True)
+    y = video.warp(xa, flow, pad)
+    assert y.grad_fn is not None and type(y.grad_fn).__name__.startswith("WarpFn")
+    with torch.no_grad():
+        assert torch.equal(y, video.warp(x, flow, pad))
+    (y * gy).sum().backward()
+    assert float((xa.grad.double() - ref).norm() / ref.norm()) < tol
+
+
 def test_video_stylizer_loop():
     vc, vs, ada = models("softmax", torch.bfloat16)
     st = video.VideoStylizer(vc, vs, ada)

@@ -12,7 +12,7 @@ import torch.multiprocessing as mp
 import network
 from conftest import load_golden
 from mhada_hip.recipe import load_recipe, seeded_image
-from mhada_hip.train import Trainer
+from mhada_hip.train import Trainer, VideoTrainer
 
 
 def build(device="cpu"):
@@ -46,6 +46,29 @@ def check_against_golden(tr, device):
 def test_train_step_matches_reference_golden():
     torch.set_num_threads(8)
     check_against_golden(Trainer(*build()), "cpu")
+
+
+def check_video_against_golden(tr, device):
+    """One train_video.py:110-166 step against the reference's own composition of it
+    (tests/golden/make_video_train_goldens.py): the seven losses and every gradient norm."""
+    g = load_golden("train_video_64_b2")
+    style, c1, c2 = (seeded_image(2, 64, 64, int(x)).to(device) for x in g["seeds"])
+    flow = torch.from_numpy(g["flow"]).to(device)
+    mask = torch.from_numpy(g["mask"]).to(device)
+    out = tr.backward(style, c1, c2, flow, mask)
+    keys = ("loss_gs", "loss_lf", "loss_ot", "loss_ft", "loss_id1", "loss_id2", "loss")
+    got = np.array([float(out[k].detach()) for k in keys])
+    np.testing.assert_allclose(got, g["losses"], rtol=2e-4)
+    for name, m in (("vit_c", tr.vit_c), ("vit_s", tr.vit_s), ("ada", tr.ada)):
+        ref = g[f"grad_{name}"]
+        np.testing.assert_allclose(grad_summary(m), ref, rtol=2e-3, atol=1e-5 * ref.max())
+    np.testing.assert_allclose(tr.ada.decoder.conv3[1].conv.conv.weight.grad.cpu().numpy(),
+                               g["grad_ada_last_conv_w"], rtol=2e-3, atol=1e-3)
+
+
+def test_video_train_step_matches_reference_golden():
+    torch.set_num_threads(8)
+    check_video_against_golden(VideoTrainer(*build()), "cpu")
 
 
 def test_checkpoint_dict_roundtrip(tmp_path):
