@@ -50,7 +50,7 @@ const char* mhada_last_error(void);
  * Knobs (value range): attn_fixed_shift (0|1), attn_waves (0|4|8; 0 = auto: 8, or 4 when the
  * 8-wave grid has fewer blocks than CUs), attn_tk (64|128), attn_prio (0|1), vit_attn_vec (0|1),
  * out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1), gemm_persist (0|1), gemm_pp128 (0|1),
- * gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1), gemm_rinit (0|1), tn_skinny_lds (0|1),
+ * gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1), conv_dir (0|1), gemm_rinit (0|1), tn_skinny_lds (0|1),
  * train_dkv_dma (0|1), wino4 (0|1), xknob (0..15, read by no shipped dispatch).
  * Returns MHADA_ERR_ARG for an unknown knob or an out-of-range value.  No reference
  * counterpart (the reference has no kernels). */

@@ -38,7 +38,7 @@ const Knob kKnobs[] = {
     {"out3_tile", &Tuning::out3_tile},               {"gemm_pp", &Tuning::gemm_pp},
     {"gemm_persist", &Tuning::gemm_persist},         {"gemm_pp128", &Tuning::gemm_pp128},
     {"gemm_ldsepi", &Tuning::gemm_ldsepi},           {"gemm_n64", &Tuning::gemm_n64},
-    {"conv_c64", &Tuning::conv_c64},                 {"gemm_rinit", &Tuning::gemm_rinit},
+    {"conv_c64", &Tuning::conv_c64},                 {"conv_dir", &Tuning::conv_dir},                 {"gemm_rinit", &Tuning::gemm_rinit},
     {"tn_skinny_lds", &Tuning::tn_skinny_lds},       {"train_dkv_dma", &Tuning::train_dkv_dma},
     {"wino4", &Tuning::wino4},
     {"xknob", &Tuning::xknob},

@@ -21,6 +21,9 @@
 // before the current tile's MFMAs.
 #include "common.h"
 
+#include <type_traits>
+#include <utility>
+
 namespace mhada {
 
 namespace {
@@ -290,6 +293,255 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_c64_kernel(const ConvTileP p) 
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Direct 3x3 convolution for the decoder's 128-input-channel layers (conv.py:75-100: conv2.0
+// 128 -> 128 and conv2.1 128 -> 64 at half the output resolution), bf16 MFMA, fp32 accumulation,
+// reflect pad 1, bias + ReLU, NHWC.  The implicit GEMM ran them at 14-16 % of the bf16 peak
+// (K = 1152, N <= 128: per-tile prologue / epilogue, every input pixel gathered 9 times).  Here:
+//   * the output tile of 8 x 32 pixels stages its 10 x 34 x 128-channel halo ONCE in LDS
+//     (85 KiB; 256-B pixel rows, chunk c at c ^ (row & 15): conflict-free ds_read_b128 over 16
+//     consecutive pixels), prefetched into registers during the previous tile's MFMAs;
+//   * the weights (147 / 295 KiB: too large to stay resident next to the halo) stream through a
+//     3-slot LDS-DMA ring of 16-KiB stages — one tap (Cout = 64) or half a tap (Cout = 128) — by
+//     buffer loads with per-lane constant offsets; the stage sequence repeats per tile, so the
+//     ring runs on across tiles.  ONE barrier per stage, placed before the stage's last k-step:
+//     it proves every wave has read the stage's slot (the last k-step's fragments are already
+//     in registers) and publishes the next stage, whose first fragments are then read beside
+//     that last k-step's MFMAs;
+//   * 4 waves (one per SIMD), wave w = output rows 2w, 2w+1 x all Cout: per 16-channel k-step
+//     Cout/32 + 2 ds_read_b128 per 2 Cout/32 MFMAs (v_mfma_f32_32x32x16_bf16), within the LDS
+//     budget of one read per MFMA; output rows staged in LDS (aliasing the halo after a barrier)
+//     and stored as 16-B chunks through a buffer descriptor, as conv3x3_c64_kernel.
+// ---------------------------------------------------------------------------------------------
+namespace {
+template <typename F, int... I>
+MHADA_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// f(std::integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <int N, typename F>
+MHADA_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+constexpr int kDCin = 128, kDCch = kDCin / 8;                // 16 chunks per halo pixel
+constexpr int kDHalo = kHPIX * kDCin;                         // bf16 elements (85 KiB)
+constexpr int kDXJ = (kHPIX * kDCch + kNT - 1) / kNT;         // halo chunks per thread (22)
+constexpr int kDStage = 8192;                                 // bf16 elements per weight stage (16 KiB)
+constexpr int kDSlots = 3;
+MHADA_DEV int hswz(int row, int chunk) { return row * kDCin + ((chunk ^ (row & 15)) << 3); }
+}  // namespace
+
+template <int COUT>
+__global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) {
+  constexpr int KS = kDStage / COUT;        // input channels per stage: 128 (a tap) or 64 (half a tap)
+  constexpr int SPT = kDCin / KS;           // stages per tap
+  constexpr int NST = 9 * SPT;              // stages per tile
+  constexpr int WCH = KS / 8;               // 16-B chunks per weight row (16 or 8)
+  constexpr int KSTEP = KS / 16;            // k-steps per stage
+  constexpr int CB = COUT / 32;             // 32-channel output blocks
+  constexpr int RPI = 64 / WCH;             // weight rows per DMA instruction (1 KiB)
+  constexpr int DPW = kDStage * 2 / 1024 / 4;  // DMA instructions per wave per stage (4)
+  constexpr int ST = 2 * (COUT / 16);          // output stores per lane and tile
+  static_assert(KS * COUT == kDStage && (WCH == 16 || WCH == 8), "stage shape");
+  // NST is a multiple of the ring depth, so every tile's stage s sits in slot s % kDSlots: the
+  // slots are compile-time constants (with runtime slots hipcc cannot prove the DMA's LDS writes
+  // disjoint from the fragment reads and drains every DMA with vmcnt(0) before the next read)
+  static_assert(NST % kDSlots == 0, "ring depth must divide the stage count");
+  __shared__ __attribute__((aligned(16))) bf16 sX[kDHalo];
+  // the ring slots are three separate LDS objects: hipcc's wait insertion tells an LDS-DMA write
+  // and a later ds_read apart only by the object they address (within one array it drains the DMA
+  // with vmcnt(0) before every fragment read)
+  __shared__ __attribute__((aligned(16))) bf16 sW0[kDStage];
+  __shared__ __attribute__((aligned(16))) bf16 sW1[kDStage];
+  __shared__ __attribute__((aligned(16))) bf16 sW2[kDStage];
+  static_assert(kDSlots == 3, "three ring objects");
+  auto slot = [&](auto S_) -> bf16* {
+    constexpr int k = decltype(S_)::value % kDSlots;
+    if constexpr (k == 0) return sW0;
+    else if constexpr (k == 1) return sW1;
+    else return sW2;
+  };
+  __shared__ __attribute__((aligned(16))) float sB[COUT];  // bias (the epilogue reads LDS, not HBM: a
+                                                          // global load there would wait on the DMA ahead)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  typedef __attribute__((address_space(3))) void* LdsP;
+  // weight rows: 128-B rows (KS = 64) use conv3x3_c64's swizzle, 256-B rows the halo's
+  auto wswz = [](int row, int chunk) {
+    return WCH == 8 ? swz(row, chunk) : row * 128 + ((chunk ^ (row & 15)) << 3);
+  };
+  // DMA: instruction j = DPW * wave + i covers weight rows RPI j .. + RPI; lane -> row RPI j + lane / WCH,
+  // LDS slot lane % WCH, which holds chunk (slot ^ swizzle(row)) of the row.  Offsets in bytes into w
+  // (row co of the packed [Cout][9 * 128] weights); the stage adds tap * 128 + part * KS channels.
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w), 0, COUT * 9 * kDCin * 2, 0x00020000);
+  unsigned wvo[DPW];
+#pragma unroll
+  for (int i = 0; i < DPW; ++i) {
+    const int row = RPI * (DPW * wave + i) + lane / WCH, slot = lane % WCH;
+    const int chunk = WCH == 8 ? slot ^ ((row >> 1) & 7) : slot ^ (row & 15);
+    wvo[i] = (unsigned)(row * 9 * kDCin + chunk * 8) * 2u;
+  }
+  auto dma = [&](auto G_) {  // stage G (mod NST) into slot G % kDSlots
+    constexpr int gs = decltype(G_)::value % NST, tap = gs / SPT, part = gs - tap * SPT;
+    bf16* dst = slot(G_);
+#pragma unroll
+    for (int i = 0; i < DPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (LdsP)(dst + 512 * (DPW * wave + i)), 16, wvo[i],
+                                               (tap * kDCin + part * KS) * 2, 0, 0);
+  };
+
+  bf16x8 stage[kDXJ];
+  auto tile_origin = [&](int t, int& b, int& Y0, int& X0) {
+    const int per = p.tiles_x * p.tiles_y;
+    b = t / per;
+    const int r = t - b * per, ty = r / p.tiles_x;
+    Y0 = ty * kTH;
+    X0 = (r - ty * p.tiles_x) * kTW;
+  };
+  auto fetch = [&](int t) {
+    int b, Y0, X0;
+    tile_origin(t, b, Y0, X0);
+    const bf16* xb = p.x + (long long)b * p.H * p.W * kDCin;
+#pragma unroll
+    for (int j = 0; j < kDXJ; ++j) {
+      const int i = min(tid + kNT * j, kHPIX * kDCch - 1), px = i >> 4, hy = px / kHW, hx = px - hy * kHW;
+      const int gy = reflect_clamp(Y0 - 1 + hy, p.H), gx = reflect_clamp(X0 - 1 + hx, p.W);
+      stage[j] = *reinterpret_cast<const bf16x8*>(xb + ((long long)gy * p.W + gx) * kDCin + (i & 15) * 8);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int j = 0; j < kDXJ; ++j) {
+      const int i = min(tid + kNT * j, kHPIX * kDCch - 1);
+      *reinterpret_cast<bf16x8*>(sX + hswz(i >> 4, i & 15)) = stage[j];
+    }
+  };
+
+  // fragments of k-step ks of stage s (slot sl): weights co = cb*32 + r32, the lane half's 8 channels;
+  // pixels of output rows 2 wave + pb, column r32, shifted by the stage's tap
+  auto frag = [&](auto S_, const int ks, bf16x8 (&wa)[CB], bf16x8 (&xb)[2]) __attribute__((always_inline)) {
+    constexpr int s = decltype(S_)::value, tap = s / SPT, part = s - tap * SPT, dy = tap / 3, dx = tap - 3 * dy;
+    const bf16* ws = slot(S_);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) wa[cb] = *reinterpret_cast<const bf16x8*>(ws + wswz(cb * 32 + r32, 2 * ks + h));
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb)
+      xb[pb] = *reinterpret_cast<const bf16x8*>(
+          sX + hswz((2 * wave + pb + dy) * kHW + r32 + dx, part * (KS / 8) + 2 * ks + h));
+  };
+
+  int t = blockIdx.x;
+  const int first = t;
+  if (t >= p.ntiles) return;
+  for (int i = tid; i < COUT; i += kNT) sB[i] = p.bias[i];
+  dma(std::integral_constant<int, 0>{});
+  dma(std::integral_constant<int, 1>{});
+  dma(std::integral_constant<int, 2>{});
+  fetch(t);
+  for (; t < p.ntiles; t += gridDim.x) {
+    if (t != first) lds_barrier();  // every wave is done with the previous tile's output staging (halo alias)
+    commit();
+    // the first tile: the halo loads are waited for above (the newest loads), so stages 0..2 have landed
+    lds_barrier();
+    fetch(min(t + (int)gridDim.x, p.ntiles - 1));
+
+    f32x16 acc[CB][2];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[cb][pb][e] = 0.f;
+    bf16x8 wa[2][CB], xb[2][2];
+    frag(std::integral_constant<int, 0>{}, 0, wa[0], xb[0]);
+    // NST stages x KSTEP k-steps, fully unrolled: every ring slot, buffer and wait count is a constant
+    auto step = [&](auto S_, auto K_) __attribute__((always_inline)) {
+      constexpr int s = decltype(S_)::value, ks = decltype(K_)::value, q = (s * KSTEP + ks) & 1;
+      if constexpr (ks + 1 < KSTEP) {
+        frag(S_, ks + 1, wa[q ^ 1], xb[q ^ 1]);
+      } else {
+        // this stage's slot is fully read by this wave: wait for our DMA of stage s + 1, barrier
+        // (publishes it; every wave is past stage s's reads), refill the slot of stage s with s + 3
+        // (stages 0 and 1: the ops issued since that DMA include the previous tile's ST output
+        // stores and this tile's kDXJ halo loads; vmcnt counts both, in issue order)
+        if constexpr (s < 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW + ST + kDXJ) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // bare: a __syncthreads() would drain the DMA ahead (vmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+        dma(std::integral_constant<int, s + 3>{});
+        __builtin_amdgcn_sched_barrier(0);  // issue the DMA here, two stages ahead (not sunk to the next wait)
+        if constexpr (s + 1 < NST) frag(std::integral_constant<int, s + 1>{}, 0, wa[q ^ 1], xb[q ^ 1]);
+      }
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb)
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[q][cb], xb[q][pb], acc[cb][pb], 0, 0, 0);
+    };
+    static_for<NST>([&](auto S_) { static_for<KSTEP>([&](auto K_) { step(S_, K_); }); });
+    // the next tile's halo loads complete here, before this tile's stores (see conv3x3_c64_kernel)
+#pragma unroll
+    for (int j = 0; j < kDXJ; ++j) asm volatile("" ::"v"(stage[j]));
+    lds_barrier();  // every wave's last halo reads are done: the output staging may alias the halo
+    int b, Y0, X0;
+    tile_origin(t, b, Y0, X0);
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        p.y + (long long)b * p.H * p.W * COUT, 0, p.H * p.W * COUT * 2, 0x00020000);
+    bf16* so = sX + wave * (32 * COUT);
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      // row r32 (pixel) of the staging slab, COUT channels = COUT / 8 chunks (swizzled by pixel)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          // bias from LDS per tile: 4 x CB registers of bias would not fit beside the halo
+          // prefetch and the accumulators at Cout = 128
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(sB + cb * 32 + 8 * gq + 4 * h);
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[cb][pb][4 * gq + e] + bb[e];
+            if (p.relu) v = fmaxf(v, 0.f);
+            o[e] = (bf16)v;
+          }
+          const int ch = cb * 4 + gq;  // 16-B chunk of the pixel's COUT channels
+          *reinterpret_cast<bf16x4*>(so + r32 * COUT + ((ch ^ (r32 & (COUT / 8 - 1))) << 3) + 4 * h) = o;
+        }
+      const int oy = Y0 + 2 * wave + pb;
+#pragma unroll
+      for (int i = 0; i < ST / 2; ++i) {
+        const int qd = lane + 64 * i, px = qd / (COUT / 8), c = qd % (COUT / 8), ox = X0 + px;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(so + px * COUT + ((c ^ (px & (COUT / 8 - 1))) << 3));
+        const int off = (oy < p.H && ox < p.W) ? ((oy * p.W + ox) * COUT + c * 8) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yr, off, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA left in flight at exit
+}
+
+// Host side, called from mhada_gemm for a bf16 CONV3X3 GEMM with Cin = 128, Cout in {64, 128}.
+int conv3x3_dir(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int cout, int relu,
+                hipStream_t s) {
+  ConvTileP p;
+  p.x = (const bf16*)x; p.w = (const bf16*)w; p.bias = bias; p.y = (bf16*)y;
+  p.B = B; p.H = H; p.W = W; p.relu = relu;
+  p.Hs = H; p.Ws = W;
+  p.tiles_x = (W + kTW - 1) / kTW;
+  p.tiles_y = (H + kTH - 1) / kTH;
+  const long long nt = (long long)B * p.tiles_x * p.tiles_y;
+  if (nt >= (1LL << 31)) return fail("conv3x3_dir: too many tiles");
+  if ((long long)H * W * 128 * 2 >= 0x7ff00000LL) return fail("conv3x3_dir: image too large for 32-bit offsets");
+  p.ntiles = (int)nt;
+  const int grid = (int)std::min<long long>(nt, 256);
+  if (cout == 64) hipLaunchKernelGGL(conv3x3_dir_kernel<64>, dim3(grid), dim3(kNT), 0, s, p);
+  else if (cout == 128) hipLaunchKernelGGL(conv3x3_dir_kernel<128>, dim3(grid), dim3(kNT), 0, s, p);
+  else return fail("conv3x3_dir: Cout must be 64 or 128");
+  return check_launch("conv3x3_dir");
 }
 
 // Host side, called from mhada_gemm for a bf16 CONV3X3 / CONV3X3_UP2 GEMM with Cin = Cout = 64

@@ -288,6 +288,48 @@ def test_conv3x3_c64_tile(up, B, H, W):
     assert rel(y, y0) < 5e-3
 
 
+@pytest.mark.parametrize("Co", [64, 128])
+@pytest.mark.parametrize("B,H,W", [(2, 8, 32), (1, 9, 13), (2, 33, 20), (1, 64, 128), (1, 2, 2), (3, 17, 70),
+                                   (1, 40, 100)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv3x3_dir_tile(Co, B, H, W, relu):
+    """The decoder's 128-input-channel layers on the direct tile kernel with the streamed weight
+    ring (conv_tile.hip conv3x3_dir_kernel, bf16 in / out, reflect pad): against fp64 on the same
+    bf16 input and close to the implicit-GEMM path (tuning conv_dir = 0); partial tiles in both
+    directions, several tiles per workgroup (the ring running on across tiles), 2 x 2 images;
+    a second run is bit-identical."""
+    x = (torch.rand(B, H, W, 128, generator=torch.Generator().manual_seed(H * W + Co)).to(DEV) - 0.3).bfloat16()
+    w = rnd(Co, 128, 3, 3, scale=(9 * 128) ** -0.5, seed=2)
+    b = rnd(Co, seed=3)
+    wp = w.permute(0, 2, 3, 1).reshape(Co, -1).bfloat16().contiguous()
+    y = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False, relu=relu)
+    assert torch.equal(y, ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False, relu=relu))
+    ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
+                   wp.double().view(Co, 3, 3, 128).permute(0, 3, 1, 2), b.double())
+    ref = torch.relu(ref) if relu else ref
+    assert rel(y.permute(0, 3, 1, 2), ref) < 5e-3
+    with _lib.tuning(conv_dir=0):
+        y0 = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False, relu=relu)
+    assert rel(y, y0) < 5e-3
+
+
+def test_conv3x3_dir_full_size():
+    """conv2.1 (128 -> 64) and conv2.0 (128 -> 128) at the 1024^2 batch-4 decoder size (512 x 512):
+    16 tiles per workgroup; against the implicit GEMM and fp64 on a row band."""
+    x = (torch.rand(4, 512, 512, 128, generator=torch.Generator().manual_seed(7)).to(DEV) - 0.3).bfloat16()
+    for Co in (64, 128):
+        wp = rnd(Co, 9 * 128, scale=(9 * 128) ** -0.5, seed=Co).bfloat16()
+        b = rnd(Co, seed=3)
+        y = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False)
+        with _lib.tuning(conv_dir=0):
+            y0 = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False)
+        assert rel(y, y0) < 5e-3
+        band = x[:, 200:240].permute(0, 3, 1, 2).double()  # rows 201..238 of the output, full width
+        ref = torch.relu(F.conv2d(F.pad(band, (1, 1, 0, 0), mode="reflect"),
+                                  wp.double().view(Co, 3, 3, 128).permute(0, 3, 1, 2), b.double()))
+        assert rel(y[:, 201:239].permute(0, 3, 1, 2), ref) < 5e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H,W,C", [(8, 8, 256), (5, 7, 64), (64, 32, 128), (1, 3, 8), (3, 1, 16), (3, 3, 8),
                                    (4, 9, 24)])
