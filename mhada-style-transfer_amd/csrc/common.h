@@ -41,7 +41,7 @@ struct Tuning {
   int gemm_ldsepi = 1;       // ping-pong epilogue staged through LDS
   int gemm_n64 = 128;        // N <= 64 tile rows (128 | 256)
   int conv_c64 = 1;          // bf16 64->64 3x3 conv (+ fused upsample): direct tile kernel
-  int conv_dir = 1;          // bf16 128->64 / 128->128 3x3 conv: direct tile kernel with a streamed weight ring (round 5)
+  int conv_dir = 1;          // bf16 128->64 / 128->128 / 256->128 3x3 conv: direct tile kernel with a streamed weight ring (round 5)
   int gemm_rinit = 1;        // persistent ping-pong GEMM: residual + bias loaded into the accumulators
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
   int wino4 = 1;             // fp32 Winograd conv: 4-wave kernel (round 5; 0: the 8-wave kernel, also the fallback for inputs >= 2 GiB)
@@ -54,9 +54,9 @@ const Tuning& tuning();
 // upsample of the input; H, W = output size.  Dispatched from mhada_gemm.
 int conv3x3_c64(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, bool up, int relu,
                 hipStream_t s);
-// conv_tile.hip: bf16 3x3 conv, Cin = 128, Cout in {64, 128}, reflect pad, no upsample.
-int conv3x3_dir(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int cout, int relu,
-                hipStream_t s);
+// conv_tile.hip: bf16 3x3 conv, (Cin, Cout) in {(128, 64), (128, 128), (256, 128)}, reflect pad, no upsample.
+int conv3x3_dir(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int cin, int cout,
+                int relu, hipStream_t s);
 
 // ---- scalar conversions -----------------------------------------------------------------
 template <typename T> MHADA_DEV float to_f32(T x);

@@ -325,31 +325,37 @@ template <int N, typename F>
 MHADA_DEV void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
-constexpr int kDCin = 128, kDCch = kDCin / 8;                // 16 chunks per halo pixel
-constexpr int kDHalo = kHPIX * kDCin;                         // bf16 elements (85 KiB)
-constexpr int kDXJ = (kHPIX * kDCch + kNT - 1) / kNT;         // halo chunks per thread (22)
 constexpr int kDStage = 8192;                                 // bf16 elements per weight stage (16 KiB)
 constexpr int kDSlots = 3;
-MHADA_DEV int hswz(int row, int chunk) { return row * kDCin + ((chunk ^ (row & 15)) << 3); }
 }  // namespace
 
-template <int COUT>
+// CIN = 128: 8 x 32-pixel tiles (10 x 34 halo, 85 KiB), wave w = output rows 2w, 2w+1;
+// CIN = 256: 4 x 32-pixel tiles (6 x 34 halo, 102 KiB), wave w = output row w.
+template <int CIN, int COUT>
 __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) {
+  constexpr int TH = CIN == 128 ? 8 : 4, PB = TH / 4;   // tile rows, output rows per wave
+  constexpr int HPIX = (TH + 2) * kHW;                  // halo pixels
+  constexpr int CCH = CIN / 8;                          // 16-B chunks per halo pixel
+  constexpr int XJ = (HPIX * CCH + kNT - 1) / kNT;      // halo chunks per thread (22 / 26)
+  static_assert(CIN == 128 || CIN == 256, "Cin");
+  // halo pixel rows of CIN channels, chunk c at c ^ (row & 15): 16 consecutive pixels hit 16
+  // distinct 16-B bank groups (the row stride is a multiple of the 256-B bank width)
+  auto hswz = [](int row, int chunk) { return row * CIN + ((chunk ^ (row & 15)) << 3); };
   constexpr int KS = kDStage / COUT;        // input channels per stage: 128 (a tap) or 64 (half a tap)
-  constexpr int SPT = kDCin / KS;           // stages per tap
+  constexpr int SPT = CIN / KS;             // stages per tap
   constexpr int NST = 9 * SPT;              // stages per tile
   constexpr int WCH = KS / 8;               // 16-B chunks per weight row (16 or 8)
   constexpr int KSTEP = KS / 16;            // k-steps per stage
   constexpr int CB = COUT / 32;             // 32-channel output blocks
   constexpr int RPI = 64 / WCH;             // weight rows per DMA instruction (1 KiB)
   constexpr int DPW = kDStage * 2 / 1024 / 4;  // DMA instructions per wave per stage (4)
-  constexpr int ST = 2 * (COUT / 16);          // output stores per lane and tile
+  constexpr int ST = PB * (COUT / 16);         // output stores per lane and tile
   static_assert(KS * COUT == kDStage && (WCH == 16 || WCH == 8), "stage shape");
   // NST is a multiple of the ring depth, so every tile's stage s sits in slot s % kDSlots: the
   // slots are compile-time constants (with runtime slots hipcc cannot prove the DMA's LDS writes
   // disjoint from the fragment reads and drains every DMA with vmcnt(0) before the next read)
   static_assert(NST % kDSlots == 0, "ring depth must divide the stage count");
-  __shared__ __attribute__((aligned(16))) bf16 sX[kDHalo];
+  __shared__ __attribute__((aligned(16))) bf16 sX[HPIX * CIN];
   // the ring slots are three separate LDS objects: hipcc's wait insertion tells an LDS-DMA write
   // and a later ds_read apart only by the object they address (within one array it drains the DMA
   // with vmcnt(0) before every fragment read)
@@ -375,13 +381,13 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
   // LDS slot lane % WCH, which holds chunk (slot ^ swizzle(row)) of the row.  Offsets in bytes into w
   // (row co of the packed [Cout][9 * 128] weights); the stage adds tap * 128 + part * KS channels.
   const __amdgpu_buffer_rsrc_t wr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w), 0, COUT * 9 * kDCin * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w), 0, COUT * 9 * CIN * 2, 0x00020000);
   unsigned wvo[DPW];
 #pragma unroll
   for (int i = 0; i < DPW; ++i) {
     const int row = RPI * (DPW * wave + i) + lane / WCH, slot = lane % WCH;
     const int chunk = WCH == 8 ? slot ^ ((row >> 1) & 7) : slot ^ (row & 15);
-    wvo[i] = (unsigned)(row * 9 * kDCin + chunk * 8) * 2u;
+    wvo[i] = (unsigned)(row * 9 * CIN + chunk * 8) * 2u;
   }
   auto dma = [&](auto G_) {  // stage G (mod NST) into slot G % kDSlots
     constexpr int gs = decltype(G_)::value % NST, tap = gs / SPT, part = gs - tap * SPT;
@@ -389,47 +395,47 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
 #pragma unroll
     for (int i = 0; i < DPW; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (LdsP)(dst + 512 * (DPW * wave + i)), 16, wvo[i],
-                                               (tap * kDCin + part * KS) * 2, 0, 0);
+                                               (tap * CIN + part * KS) * 2, 0, 0);
   };
 
-  bf16x8 stage[kDXJ];
+  bf16x8 stage[XJ];
   auto tile_origin = [&](int t, int& b, int& Y0, int& X0) {
     const int per = p.tiles_x * p.tiles_y;
     b = t / per;
     const int r = t - b * per, ty = r / p.tiles_x;
-    Y0 = ty * kTH;
+    Y0 = ty * TH;
     X0 = (r - ty * p.tiles_x) * kTW;
   };
   auto fetch = [&](int t) {
     int b, Y0, X0;
     tile_origin(t, b, Y0, X0);
-    const bf16* xb = p.x + (long long)b * p.H * p.W * kDCin;
+    const bf16* xb = p.x + (long long)b * p.H * p.W * CIN;
 #pragma unroll
-    for (int j = 0; j < kDXJ; ++j) {
-      const int i = min(tid + kNT * j, kHPIX * kDCch - 1), px = i >> 4, hy = px / kHW, hx = px - hy * kHW;
+    for (int j = 0; j < XJ; ++j) {
+      const int i = min(tid + kNT * j, HPIX * CCH - 1), px = i / CCH, hy = px / kHW, hx = px - hy * kHW;
       const int gy = reflect_clamp(Y0 - 1 + hy, p.H), gx = reflect_clamp(X0 - 1 + hx, p.W);
-      stage[j] = *reinterpret_cast<const bf16x8*>(xb + ((long long)gy * p.W + gx) * kDCin + (i & 15) * 8);
+      stage[j] = *reinterpret_cast<const bf16x8*>(xb + ((long long)gy * p.W + gx) * CIN + (i % CCH) * 8);
     }
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int j = 0; j < kDXJ; ++j) {
-      const int i = min(tid + kNT * j, kHPIX * kDCch - 1);
-      *reinterpret_cast<bf16x8*>(sX + hswz(i >> 4, i & 15)) = stage[j];
+    for (int j = 0; j < XJ; ++j) {
+      const int i = min(tid + kNT * j, HPIX * CCH - 1);
+      *reinterpret_cast<bf16x8*>(sX + hswz(i / CCH, i % CCH)) = stage[j];
     }
   };
 
   // fragments of k-step ks of stage s (slot sl): weights co = cb*32 + r32, the lane half's 8 channels;
   // pixels of output rows 2 wave + pb, column r32, shifted by the stage's tap
-  auto frag = [&](auto S_, const int ks, bf16x8 (&wa)[CB], bf16x8 (&xb)[2]) __attribute__((always_inline)) {
+  auto frag = [&](auto S_, const int ks, bf16x8 (&wa)[CB], bf16x8 (&xb)[PB]) __attribute__((always_inline)) {
     constexpr int s = decltype(S_)::value, tap = s / SPT, part = s - tap * SPT, dy = tap / 3, dx = tap - 3 * dy;
     const bf16* ws = slot(S_);
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) wa[cb] = *reinterpret_cast<const bf16x8*>(ws + wswz(cb * 32 + r32, 2 * ks + h));
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb)
+    for (int pb = 0; pb < PB; ++pb)
       xb[pb] = *reinterpret_cast<const bf16x8*>(
-          sX + hswz((2 * wave + pb + dy) * kHW + r32 + dx, part * (KS / 8) + 2 * ks + h));
+          sX + hswz((PB * wave + pb + dy) * kHW + r32 + dx, part * (KS / 8) + 2 * ks + h));
   };
 
   int t = blockIdx.x;
@@ -447,14 +453,14 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
     lds_barrier();
     fetch(min(t + (int)gridDim.x, p.ntiles - 1));
 
-    f32x16 acc[CB][2];
+    f32x16 acc[CB][PB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-      for (int pb = 0; pb < 2; ++pb)
+      for (int pb = 0; pb < PB; ++pb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[cb][pb][e] = 0.f;
-    bf16x8 wa[2][CB], xb[2][2];
+    bf16x8 wa[2][CB], xb[2][PB];
     frag(std::integral_constant<int, 0>{}, 0, wa[0], xb[0]);
     // NST stages x KSTEP k-steps, fully unrolled: every ring slot, buffer and wait count is a constant
     auto step = [&](auto S_, auto K_) __attribute__((always_inline)) {
@@ -466,7 +472,7 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
         // (publishes it; every wave is past stage s's reads), refill the slot of stage s with s + 3
         // (stages 0 and 1: the ops issued since that DMA include the previous tile's ST output
         // stores and this tile's kDXJ halo loads; vmcnt counts both, in issue order)
-        if constexpr (s < 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW + ST + kDXJ) : "memory");
+        if constexpr (s < 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW + ST + XJ) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();  // bare: a __syncthreads() would drain the DMA ahead (vmcnt(0))
@@ -478,13 +484,13 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-        for (int pb = 0; pb < 2; ++pb)
+        for (int pb = 0; pb < PB; ++pb)
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[q][cb], xb[q][pb], acc[cb][pb], 0, 0, 0);
     };
     static_for<NST>([&](auto S_) { static_for<KSTEP>([&](auto K_) { step(S_, K_); }); });
     // the next tile's halo loads complete here, before this tile's stores (see conv3x3_c64_kernel)
 #pragma unroll
-    for (int j = 0; j < kDXJ; ++j) asm volatile("" ::"v"(stage[j]));
+    for (int j = 0; j < XJ; ++j) asm volatile("" ::"v"(stage[j]));
     lds_barrier();  // every wave's last halo reads are done: the output staging may alias the halo
     int b, Y0, X0;
     tile_origin(t, b, Y0, X0);
@@ -492,7 +498,7 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
         p.y + (long long)b * p.H * p.W * COUT, 0, p.H * p.W * COUT * 2, 0x00020000);
     bf16* so = sX + wave * (32 * COUT);
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
+    for (int pb = 0; pb < PB; ++pb) {
       // row r32 (pixel) of the staging slab, COUT channels = COUT / 8 chunks (swizzled by pixel)
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb)
@@ -511,9 +517,9 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
           const int ch = cb * 4 + gq;  // 16-B chunk of the pixel's COUT channels
           *reinterpret_cast<bf16x4*>(so + r32 * COUT + ((ch ^ (r32 & (COUT / 8 - 1))) << 3) + 4 * h) = o;
         }
-      const int oy = Y0 + 2 * wave + pb;
+      const int oy = Y0 + PB * wave + pb;
 #pragma unroll
-      for (int i = 0; i < ST / 2; ++i) {
+      for (int i = 0; i < COUT / 16; ++i) {  // one output row: 32 pixels x COUT channels in 16-B chunks
         const int qd = lane + 64 * i, px = qd / (COUT / 8), c = qd % (COUT / 8), ox = X0 + px;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(so + px * COUT + ((c ^ (px & (COUT / 8 - 1))) << 3));
         const int off = (oy < p.H && ox < p.W) ? ((oy * p.W + ox) * COUT + c * 8) * 2 : 0x7ffffff0;
@@ -524,23 +530,26 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_dir_kernel(const ConvTileP p) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA left in flight at exit
 }
 
-// Host side, called from mhada_gemm for a bf16 CONV3X3 GEMM with Cin = 128, Cout in {64, 128}.
-int conv3x3_dir(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int cout, int relu,
-                hipStream_t s) {
+// Host side, called from mhada_gemm for a bf16 CONV3X3 GEMM with (Cin, Cout) in {(128, 64), (128, 128),
+// (256, 128)}.
+int conv3x3_dir(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int cin, int cout,
+                int relu, hipStream_t s) {
   ConvTileP p;
   p.x = (const bf16*)x; p.w = (const bf16*)w; p.bias = bias; p.y = (bf16*)y;
   p.B = B; p.H = H; p.W = W; p.relu = relu;
   p.Hs = H; p.Ws = W;
+  const int th = cin == 128 ? 8 : 4;
   p.tiles_x = (W + kTW - 1) / kTW;
-  p.tiles_y = (H + kTH - 1) / kTH;
+  p.tiles_y = (H + th - 1) / th;
   const long long nt = (long long)B * p.tiles_x * p.tiles_y;
   if (nt >= (1LL << 31)) return fail("conv3x3_dir: too many tiles");
-  if ((long long)H * W * 128 * 2 >= 0x7ff00000LL) return fail("conv3x3_dir: image too large for 32-bit offsets");
+  if ((long long)H * W * cin * 2 >= 0x7ff00000LL) return fail("conv3x3_dir: image too large for 32-bit offsets");
   p.ntiles = (int)nt;
   const int grid = (int)std::min<long long>(nt, 256);
-  if (cout == 64) hipLaunchKernelGGL(conv3x3_dir_kernel<64>, dim3(grid), dim3(kNT), 0, s, p);
-  else if (cout == 128) hipLaunchKernelGGL(conv3x3_dir_kernel<128>, dim3(grid), dim3(kNT), 0, s, p);
-  else return fail("conv3x3_dir: Cout must be 64 or 128");
+  if (cin == 128 && cout == 64) hipLaunchKernelGGL((conv3x3_dir_kernel<128, 64>), dim3(grid), dim3(kNT), 0, s, p);
+  else if (cin == 128 && cout == 128) hipLaunchKernelGGL((conv3x3_dir_kernel<128, 128>), dim3(grid), dim3(kNT), 0, s, p);
+  else if (cin == 256 && cout == 128) hipLaunchKernelGGL((conv3x3_dir_kernel<256, 128>), dim3(grid), dim3(kNT), 0, s, p);
+  else return fail("conv3x3_dir: (Cin, Cout) must be (128, 64), (128, 128) or (256, 128)");
   return check_launch("conv3x3_dir");
 }
 

@@ -104,10 +104,12 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
                        a->a_mode == MHADA_A_CONV3X3_UP2, a->relu, stream);
   // the decoder's 128-input-channel layers: direct tile kernel with a streamed weight ring
   if (!a->c2 && !a->vt && tuning().conv_dir && a->compute == MHADA_BF16 && a->a_dtype == MHADA_BF16 &&
-      a->c_dtype == MHADA_BF16 && a->a_mode == MHADA_A_CONV3X3 && a->img_c == 128 && (a->N == 64 || a->N == 128) &&
-      a->ldc == a->N && a->ldw == 9 * 128 && a->bias && !a->r &&
-      (long long)p.out_h * p.out_w * 128 * 2 < 0x7ff00000LL)
-    return conv3x3_dir(a->a, a->w, a->bias, a->c, a->M / (p.out_h * p.out_w), p.out_h, p.out_w, a->N, a->relu, stream);
+      a->c_dtype == MHADA_BF16 && a->a_mode == MHADA_A_CONV3X3 &&
+      ((a->img_c == 128 && (a->N == 64 || a->N == 128)) || (a->img_c == 256 && a->N == 128)) &&
+      a->ldc == a->N && a->ldw == 9 * a->img_c && a->bias && !a->r &&
+      (long long)p.out_h * p.out_w * a->img_c * 2 < 0x7ff00000LL)
+    return conv3x3_dir(a->a, a->w, a->bias, a->c, a->M / (p.out_h * p.out_w), p.out_h, p.out_w, a->img_c, a->N,
+                       a->relu, stream);
   if (a->compute == MHADA_F32) return gemm_dispatch_f32(a->a_mode, p, nz, stream);
   if (a->a_dtype == MHADA_F32) {
     if (a->c_dtype == MHADA_F32) return gemm_dispatch_bf16_a32_o32(a->a_mode, p, nz, stream);

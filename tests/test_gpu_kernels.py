@@ -288,24 +288,24 @@ def test_conv3x3_c64_tile(up, B, H, W):
     assert rel(y, y0) < 5e-3
 
 
-@pytest.mark.parametrize("Co", [64, 128])
+@pytest.mark.parametrize("Ci,Co", [(128, 64), (128, 128), (256, 128)])
 @pytest.mark.parametrize("B,H,W", [(2, 8, 32), (1, 9, 13), (2, 33, 20), (1, 64, 128), (1, 2, 2), (3, 17, 70),
                                    (1, 40, 100)])
 @pytest.mark.parametrize("relu", [True, False])
-def test_conv3x3_dir_tile(Co, B, H, W, relu):
-    """The decoder's 128-input-channel layers on the direct tile kernel with the streamed weight
-    ring (conv_tile.hip conv3x3_dir_kernel, bf16 in / out, reflect pad): against fp64 on the same
-    bf16 input and close to the implicit-GEMM path (tuning conv_dir = 0); partial tiles in both
-    directions, several tiles per workgroup (the ring running on across tiles), 2 x 2 images;
+def test_conv3x3_dir_tile(Ci, Co, B, H, W, relu):
+    """The decoder's 128 / 256-input-channel layers on the direct tile kernel with the streamed
+    weight ring (conv_tile.hip conv3x3_dir_kernel, bf16 in / out, reflect pad): against fp64 on
+    the same bf16 input and close to the implicit-GEMM path (tuning conv_dir = 0); partial tiles in
+    both directions, several tiles per workgroup (the ring running on across tiles), 2 x 2 images;
     a second run is bit-identical."""
-    x = (torch.rand(B, H, W, 128, generator=torch.Generator().manual_seed(H * W + Co)).to(DEV) - 0.3).bfloat16()
-    w = rnd(Co, 128, 3, 3, scale=(9 * 128) ** -0.5, seed=2)
+    x = (torch.rand(B, H, W, Ci, generator=torch.Generator().manual_seed(H * W + Co)).to(DEV) - 0.3).bfloat16()
+    w = rnd(Co, Ci, 3, 3, scale=(9 * Ci) ** -0.5, seed=2)
     b = rnd(Co, seed=3)
     wp = w.permute(0, 2, 3, 1).reshape(Co, -1).bfloat16().contiguous()
     y = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False, relu=relu)
     assert torch.equal(y, ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False, relu=relu))
     ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2).double(), (1, 1, 1, 1), mode="reflect"),
-                   wp.double().view(Co, 3, 3, 128).permute(0, 3, 1, 2), b.double())
+                   wp.double().view(Co, 3, 3, Ci).permute(0, 3, 1, 2), b.double())
     ref = torch.relu(ref) if relu else ref
     assert rel(y.permute(0, 3, 1, 2), ref) < 5e-3
     with _lib.tuning(conv_dir=0):
@@ -314,11 +314,12 @@ def test_conv3x3_dir_tile(Co, B, H, W, relu):
 
 
 def test_conv3x3_dir_full_size():
-    """conv2.1 (128 -> 64) and conv2.0 (128 -> 128) at the 1024^2 batch-4 decoder size (512 x 512):
-    16 tiles per workgroup; against the implicit GEMM and fp64 on a row band."""
-    x = (torch.rand(4, 512, 512, 128, generator=torch.Generator().manual_seed(7)).to(DEV) - 0.3).bfloat16()
-    for Co in (64, 128):
-        wp = rnd(Co, 9 * 128, scale=(9 * 128) ** -0.5, seed=Co).bfloat16()
+    """conv2.1 (128 -> 64) and conv2.0 (128 -> 128) at the 1024^2 batch-4 decoder size (512 x 512,
+    16 tiles per workgroup) and conv1.4 (256 -> 128 at 256 x 256); against the implicit GEMM and
+    fp64 on a row band."""
+    for Ci, Co, S in ((128, 64, 512), (128, 128, 512), (256, 128, 256)):
+        x = (torch.rand(4, S, S, Ci, generator=torch.Generator().manual_seed(7)).to(DEV) - 0.3).bfloat16()
+        wp = rnd(Co, 9 * Ci, scale=(9 * Ci) ** -0.5, seed=Co).bfloat16()
         b = rnd(Co, seed=3)
         y = ops.conv3x3(x, wp, b, torch.bfloat16, upsample=False)
         with _lib.tuning(conv_dir=0):
@@ -326,7 +327,7 @@ def test_conv3x3_dir_full_size():
         assert rel(y, y0) < 5e-3
         band = x[:, 200:240].permute(0, 3, 1, 2).double()  # rows 201..238 of the output, full width
         ref = torch.relu(F.conv2d(F.pad(band, (1, 1, 0, 0), mode="reflect"),
-                                  wp.double().view(Co, 3, 3, 128).permute(0, 3, 1, 2), b.double()))
+                                  wp.double().view(Co, 3, 3, Ci).permute(0, 3, 1, 2), b.double()))
         assert rel(y[:, 201:239].permute(0, 3, 1, 2), ref) < 5e-3
 
 

@@ -165,7 +165,7 @@ def conv_suite():
             if dt == torch.bfloat16 and not up and Co > 128:
                 fns["oneshot"] = lambda: with_env("MHADA_GEMM_PERSIST", "0", ops.conv3x3, x, w, bias, dt,
                                                   upsample=False)
-            if dt == torch.bfloat16 and Ci == 128 and not up:
+            if dt == torch.bfloat16 and (Ci, Co) in ((128, 64), (128, 128), (256, 128)) and not up:
                 fns["dir_off"] = lambda: with_env("MHADA_CONV_DIR", "0", ops.conv3x3, x, w, bias, dt, upsample=False)
             if Co <= 64:
                 fns["n64_256"] = lambda: with_env("MHADA_GEMM_N64", "256", ops.conv3x3, ops.upsample2x(x) if up else x, w,
