@@ -738,41 +738,37 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ x
 // instructions than the loads it saved, profiles/r05_prof_bench_per_config.txt.)
 template <typename T>
 __global__ void __launch_bounds__(256) upsample2x_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
-                                                             int W, int C) {
+                                                             int W, int C, int gshift) {
+  // one 16-B output vector per thread, consecutive lanes = consecutive vectors of one output row
+  // (fully coalesced stores); the row (b, Y) comes from blockIdx.y, so the per-thread index math
+  // is one shift (or one 32-bit division) instead of three 64-bit divisions
   typedef typename Vec16<T>::type V;
-  constexpr int N = Vec16<T>::N, NV = 8 / N;  // 16-B vectors per 8-channel group
-  const int G = C / 8;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)B * 4 * H * W * G;
-  if (idx >= total) return;
-  const int g = (int)(idx % G);
-  long long pix = idx / G;
-  const int Wo = 2 * W, Ho = 2 * H;
-  const int X = (int)(pix % Wo);
-  pix /= Wo;
-  const int Y = (int)(pix % Ho);
-  const int b = (int)(pix / Ho);
-  const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
+  constexpr int N = Vec16<T>::N;
+  const int G = C / N;  // vectors per pixel
+  const int Wo = 2 * W, Ho = 2 * H, rows = B * Ho;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Wo * G) return;
+  const int X = gshift >= 0 ? i >> gshift : i / G;
+  const int gv = i - X * G;
   const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.f);
-  const int y0 = (int)sy, x0 = (int)sx;
-  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
-  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
-  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-  const T* base = x + (long long)b * H * W * C + g * 8;
-  const V* p00 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x0) * C);
-  const V* p01 = reinterpret_cast<const V*>(base + ((long long)y0 * W + x1) * C);
-  const V* p10 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x0) * C);
-  const V* p11 = reinterpret_cast<const V*>(base + ((long long)y1 * W + x1) * C);
-  V* out = reinterpret_cast<V*>(y + (((long long)b * Ho + Y) * Wo + X) * C + g * 8);
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const V a00 = p00[v], a01 = p01[v], a10 = p10[v], a11 = p11[v];
+  const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+  for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+    const int b = row / Ho, Y = row - b * Ho;
+    const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.f);
+    const int y0 = (int)sy, y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+    const T* base = x + (long long)b * H * W * C + gv * N;
+    const V a00 = *reinterpret_cast<const V*>(base + ((long long)y0 * W + x0) * C);
+    const V a01 = *reinterpret_cast<const V*>(base + ((long long)y0 * W + x1) * C);
+    const V a10 = *reinterpret_cast<const V*>(base + ((long long)y1 * W + x0) * C);
+    const V a11 = *reinterpret_cast<const V*>(base + ((long long)y1 * W + x1) * C);
     V o;
 #pragma unroll
     for (int e = 0; e < N; ++e)
       o[e] = from_f32<T>(bilerp(ly0, ly1, lx0, lx1, to_f32<T>(a00[e]), to_f32<T>(a01[e]), to_f32<T>(a10[e]),
                                 to_f32<T>(a11[e])));
-    out[v] = o;
+    *reinterpret_cast<V*>(y + ((long long)row * Wo + X) * C + gv * N) = o;
   }
 }
 
@@ -1076,15 +1072,19 @@ extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H,
                        (hipStream_t)s_, (const bf16*)x, (bf16*)y, B, H, W, C);
     return check_launch("mhada_upsample2x");
   }
-  if (aligned16(x) && aligned16(y)) {  // 16-B vector loads / stores (round 5); unaligned views: element form
-    const long long total = (long long)B * 4 * H * W * (C / 8);
-    const dim3 grid((unsigned)((total + 255) / 256));
+  if (aligned16(x) && aligned16(y) && (long long)2 * W * C < (1LL << 31)) {
+    // 16-B vector loads / stores (round 5); unaligned views: element form
+    const int G = dtype == MHADA_F32 ? C / 4 : C / 8;
+    const int gshift = (G & (G - 1)) == 0 ? __builtin_ctz(G) : -1;
+    const long long rows = (long long)B * 2 * H;
+    const dim3 grid((unsigned)((2LL * W * G + 255) / 256), (unsigned)std::min<long long>(rows, 65535));
+    if (rows > (1LL << 31) - 1) return fail("mhada_upsample2x: too many rows");
     if (dtype == MHADA_F32)
       hipLaunchKernelGGL((upsample2x_vec_kernel<float>), grid, dim3(256), 0, (hipStream_t)s_, (const float*)x,
-                         (float*)y, B, H, W, C);
+                         (float*)y, B, H, W, C, gshift);
     else
       hipLaunchKernelGGL((upsample2x_vec_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)x,
-                         (bf16*)y, B, H, W, C);
+                         (bf16*)y, B, H, W, C, gshift);
     return check_launch("mhada_upsample2x");
   }
   const long long total = (long long)B * 4 * H * W * (C / 8);
