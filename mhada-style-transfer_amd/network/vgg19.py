@@ -39,3 +39,23 @@ class VGG19(nn.Module):
 
     def forward(self, x):
         return autograd_path.vgg19_forward(self, x)
+
+    def load_torchvision_features(self, src) -> None:
+        """ImageNet weights from a LOCAL torchvision VGG19 checkpoint — the file that
+        ``torchvision.models.vgg19(weights="VGG19_Weights.IMAGENET1K_V1")`` (vgg19.py:18) downloads
+        (``vgg19-dcbb9e9d.pth``), a path to it or its state_dict: ``features.{i}.{weight,bias}``
+        load into ``slice{s}.{i}`` (the reference keeps ``features[0:30]``, vgg19.py:20-36); the
+        classifier and features past index 29 are ignored.  Loaded with ``weights_only=True``.
+        Every conv of the five slices must be present (strict), shapes must match."""
+        import torch
+        sd = torch.load(src, map_location="cpu", weights_only=True) if not isinstance(src, dict) else src
+        convs = {c[0] for c in _CONVS}
+        own = {}
+        for s, (a, b) in enumerate(_SLICES, start=1):
+            for i in (x for x in range(a, b) if x in convs):
+                for t in ("weight", "bias"):
+                    key = f"features.{i}.{t}"
+                    if key not in sd:
+                        raise KeyError(f"load_torchvision_features: {key} missing")
+                    own[f"slice{s}.{i}.{t}"] = sd[key]
+        self.load_state_dict(own, strict=True)

@@ -154,3 +154,25 @@ def test_ds_spill_rule_is_shape_only(monkeypatch):
     assert ops.ds_spill_eligible(3 * 8 * 8, 4096, 4096)  # 512^2 B8, three AdaFormer calls batched
     assert not ops.ds_spill_eligible(4, 4096, 4094)       # Ns % 4 != 0
     assert not ops.ds_spill_eligible(1024, 8192, 8192)    # past DS_SPILL_BYTES
+
+
+def test_vgg19_loads_torchvision_feature_weights(tmp_path):
+    """real VGG19 weights from a local torchvision checkpoint (features.{i}.*
+    keys, classifier ignored) load into the slices; a missing conv raises."""
+    import torch
+    vgg = network.VGG19()
+    g = torch.Generator().manual_seed(3)
+    tv = {}
+    for name, p in vgg.named_parameters():
+        s, i, t = name.split(".")
+        tv[f"features.{i}.{t}"] = torch.randn(p.shape, generator=g)
+    tv["classifier.0.weight"] = torch.randn(4096, 25088 // 64, generator=g)  # ignored
+    torch.save(tv, tmp_path / "vgg19-dcbb9e9d.pth")
+    vgg.load_torchvision_features(str(tmp_path / "vgg19-dcbb9e9d.pth"))
+    for name, p in vgg.named_parameters():
+        s, i, t = name.split(".")
+        assert torch.equal(p, tv[f"features.{i}.{t}"])
+        assert not p.requires_grad
+    del tv["features.28.bias"]
+    with pytest.raises(KeyError):
+        network.VGG19().load_torchvision_features(tv)
