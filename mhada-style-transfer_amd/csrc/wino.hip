@@ -592,6 +592,12 @@ struct WgP {
 // px * 64 + (c ^ (8 * ((px >> 1) & 7)))
 MHADA_DEV int wg_px(int px, int c) { return px * 64 + (c ^ (8 * ((px >> 1) & 7))); }
 
+// ZERO: zero padding (VGG-style), else reflect (the decoder).  Per-chunk work is scalar where it
+// can be: the chunk coordinates are stepped (no divisions), interior chunks (the patch and the
+// dY rows inside the image) load through a per-chunk base plus per-lane constant offsets, and the
+// transforms' LDS offsets (per-lane XOR swizzles) are computed once — every VALU instruction here
+// costs its full issue time beside the fp32 MFMAs (profiles/r05_f32mfma_fill.log).
+template <bool ZERO>
 __global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
   __shared__ __attribute__((aligned(16))) float lds[4 * kWgS + kWgRX + kWgRY];  // 154 KiB
   auto sYh = [&](int i) { return lds + i * kWgS; };
@@ -605,19 +611,23 @@ __global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
   const int cb = blockIdx.x / nib, ib = blockIdx.x - cb * nib;
   const int co0 = cb * 64, ci0 = ib * 64;
   const int c_beg = blockIdx.y * p.cps, c_end = min(p.nchunk, c_beg + p.cps);
-  const int P = 1;  // pad 1: reflect (decoder) or zero
+  constexpr int P = 1;  // pad 1
+  const int TW = p.crow * kWgT, TH = p.H / 2;  // tile columns / rows per image
 
-  auto chunk_pos = [&](int c, int& b, int& ty, int& tx0) {
-    const int per_img = (p.H / 2) * p.crow;
-    b = c / per_img;
-    const int r = c - b * per_img;
-    ty = r / p.crow;
-    tx0 = (r - ty * p.crow) * kWgT;
+  // chunk coordinates, stepped along the chunk order (b, ty, tx0 / 8)
+  struct Pos { int b, ty, tx0; };
+  auto step_pos = [&](Pos& q) {
+    q.tx0 += kWgT;
+    if (q.tx0 >= TW) {
+      q.tx0 = 0;
+      if (++q.ty >= TH) {
+        q.ty = 0;
+        ++q.b;
+      }
+    }
   };
-  auto src_pix = [&](int b, int Y, int X, bool& ok) -> long long {
-    ok = true;
-    if (p.zero) {
-      ok = Y >= 0 && Y < p.H && X >= 0 && X < p.W;
+  auto src_pix = [&](int b, int Y, int X) -> long long {
+    if (ZERO) {
       Y = min(max(Y, 0), p.H - 1);
       X = min(max(X, 0), p.W - 1);
     } else {
@@ -626,50 +636,65 @@ __global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
     }
     return ((long long)b * p.H + Y) * p.W + X;
   };
-  // LDS-DMA of chunk c's raw rows: dY 32 px x 16 quads (8 instructions, one per wave), X 72 px x 16
-  // quads (18 instructions: waves 0-7, then 0-7, then 0-1); slot (px, q) holds source quad
-  // q ^ (2 * ((px >> 1) & 7)); zero-padding pixels of X load a clamped pixel (zeroed in the transform)
-  auto dma = [&](int c) {
+  // per-lane constants of the DMA pieces: dY (one piece per wave: px 4w + lane / 16) and X (pieces
+  // ins = wave + 8 j < 18: px 4 ins + lane / 16); slot (px, q) holds source quad q ^ (2 ((px >> 1) & 7))
+  const int ypx = 4 * wave + (lane >> 4), ysq = (lane & 15) ^ (2 * ((ypx >> 1) & 7));
+  const long long yoff = ((long long)(ypx >> 4) * p.W + (ypx & 15)) * p.ldg + 4 * ysq;
+  int xpx[3], xsq[3];
+  long long xoff[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    xpx[j] = 4 * (wave + 8 * j) + (lane >> 4);
+    xsq[j] = (lane & 15) ^ (2 * ((xpx[j] >> 1) & 7));
+    xoff[j] = ((long long)(xpx[j] / 18) * p.W + xpx[j] % 18) * p.Cin + 4 * xsq[j];
+  }
+  // the chunk's patch rows 2ty-1 .. 2ty+2, columns 2tx0-1 .. 2tx0+16 and its dY rows lie in the image
+  auto interior = [&](const Pos& q) {
+    return q.ty > 0 && 2 * q.ty + 2 < p.H && q.tx0 > 0 && 2 * q.tx0 + 16 < p.W;
+  };
+  auto dma = [&](const Pos& q) {
 #if WINO_DBG & 2
     return;
 #endif
-    int b, ty, tx0;
-    chunk_pos(min(c, p.nchunk - 1), b, ty, tx0);
-    {
-      const int px = 4 * wave + (lane >> 4), q = lane & 15;
-      const int sq = q ^ (2 * ((px >> 1) & 7));
-      const int Y = 2 * ty + (px >> 4), X = 2 * tx0 + (px & 15);
-      glds16(p.g + (((long long)b * p.H + Y) * p.W + X) * p.ldg + co0 + 4 * sq, sRY + wave * 256);
-    }
+    glds16(p.g + (((long long)q.b * p.H + 2 * q.ty) * p.W + 2 * q.tx0) * p.ldg + co0 + yoff, sRY + wave * 256);
+    if (interior(q)) {
+      const float* xb = p.x + (((long long)q.b * p.H + 2 * q.ty - P) * p.W + 2 * q.tx0 - P) * p.Cin + ci0;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int ins = wave + 8 * j;
-      if (ins < 18) {
-        const int px = 4 * ins + (lane >> 4), q = lane & 15;
-        const int sq = q ^ (2 * ((px >> 1) & 7));
-        bool ok;
-        const long long pix = src_pix(b, 2 * ty - P + px / 18, 2 * tx0 - P + px % 18, ok);
-        glds16(p.x + pix * p.Cin + ci0 + 4 * sq, sRX + ins * 256);
-      }
+      for (int j = 0; j < 3; ++j)
+        if (wave + 8 * j < 18) glds16(xb + xoff[j], sRX + (wave + 8 * j) * 256);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (wave + 8 * j < 18) {
+          const long long pix = src_pix(q.b, 2 * q.ty - P + xpx[j] / 18, 2 * q.tx0 - P + xpx[j] % 18);
+          glds16(p.x + pix * p.Cin + ci0 + 4 * xsq[j], sRX + (wave + 8 * j) * 256);
+        }
     }
   };
   // transforms of the chunk whose raw rows are in sRY / sRX into buffer slot n: item (t, row) with
   // t = lane & 7 and row = 8 * wave + (lane >> 3) (both the co of Yh and the ci of V)
   const int it = lane & 7, irow = 8 * wave + (lane >> 3);
   const int wdst = swz(irow, it >> 2) + (it & 3);
+  int ry[4], rx[16];  // LDS offsets of the item's raw reads (wg_px swizzle, per lane)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) ry[2 * i + j] = wg_px(16 * i + 2 * it + j, irow);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rx[4 * i + j] = wg_px(18 * i + 2 * it + j, irow);
   float bsum = 0.f;  // bias gradient partial of co = co0 + irow (ci block 0)
-  auto transform = [&](int c, int n) {
+  auto transform = [&](const Pos& q, int n) {
 #if WINO_DBG & 4
     return;
 #endif
-    int b, ty, tx0;
-    chunk_pos(c, b, ty, tx0);
     // Yh = A dY A^T, A = [[1,0],[1,1],[1,-1],[0,-1]]
     float d[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) d[i][j] = sRY[wg_px(16 * i + 2 * it + j, irow)];
+      for (int j = 0; j < 2; ++j) d[i][j] = sRY[ry[2 * i + j]];
     if (ib == 0) bsum += (d[0][0] + d[0][1]) + (d[1][0] + d[1][1]);
     float a[4][2];
 #pragma unroll
@@ -690,17 +715,16 @@ __global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
     // V = B^T d B on the 4 x 4 patch of tile it (input rows 2ty-1 .. 2ty+2)
     float v[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 16; ++i) v[i] = sRX[rx[i]];
+    if (ZERO && !interior(q)) {  // zero padding: the clamped pixels outside the image read 0
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int px = 18 * i + 2 * it + j;
-        float val = sRX[wg_px(px, irow)];
-        if (p.zero) {
-          const int Y = 2 * ty - P + i, X = 2 * tx0 - P + 2 * it + j;
-          if (Y < 0 || Y >= p.H || X < 0 || X >= p.W) val = 0.f;
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int Y = 2 * q.ty - P + i, X = 2 * q.tx0 - P + 2 * it + j;
+          if (Y < 0 || Y >= p.H || X < 0 || X >= p.W) v[4 * i + j] = 0.f;
         }
-        v[4 * i + j] = val;
-      }
+    }
     float t[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -746,21 +770,30 @@ __global__ void __launch_bounds__(512, 1) wino_wgrad_kernel(const WgP p) {
   };
 
   if (c_beg < c_end) {
-    dma(c_beg);
+    Pos q;  // chunk c_beg: the one division of the kernel
+    {
+      const int per_img = TH * p.crow;
+      q.b = c_beg / per_img;
+      const int r = c_beg - q.b * per_img;
+      q.ty = r / p.crow;
+      q.tx0 = (r - q.ty * p.crow) * kWgT;
+    }
+    dma(q);
     publish();
-    transform(c_beg, 0);
+    transform(q, 0);
     __syncthreads();
     // chunk c: DMA of c+1's raw rows (the raw buffers were last read by transform(c) before the
     // barrier), MFMAs on slot c&1, then (after its DMA landed) transform c+1 into the other slot
     for (int c = c_beg; c < c_end; ++c) {
       const int k = c - c_beg, cur = k & 1;
       const bool more = c + 1 < c_end;
-      if (more) dma(c + 1);
+      step_pos(q);  // chunk c + 1
+      if (more) dma(q);
       mfmas(cur);
       if (more) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's pieces of c+1 landed
-        transform(c + 1, cur ^ 1);
+        transform(q, cur ^ 1);
       }
       __syncthreads();
     }
@@ -863,7 +896,10 @@ extern "C" int mhada_conv3x3_wgrad_wino(const float* x, const float* g, float* d
   p.slab = work;
   p.cslab = db ? work + (long long)S * 16 * Cout * Cin : nullptr;
   const dim3 grid((unsigned)((Cout / 64) * (Cin / 64)), (unsigned)S);
-  hipLaunchKernelGGL(wino_wgrad_kernel, grid, dim3(512), 0, (hipStream_t)s_, p);
+  if (p.zero)
+    hipLaunchKernelGGL(wino_wgrad_kernel<true>, grid, dim3(512), 0, (hipStream_t)s_, p);
+  else
+    hipLaunchKernelGGL(wino_wgrad_kernel<false>, grid, dim3(512), 0, (hipStream_t)s_, p);
   if (int rc = check_launch("mhada_conv3x3_wgrad_wino")) return rc;
   const long long n = (long long)Cout * Cin;
   hipLaunchKernelGGL(wino_wgrad_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s_,

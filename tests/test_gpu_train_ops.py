@@ -619,7 +619,8 @@ def test_feature_loss_fn_matches_aten_autograd(stats, target, B, C, H, W):
 
 
 @pytest.mark.parametrize("pad_mode", ["reflect", "zero"])
-@pytest.mark.parametrize("B,H,W,Ci,Co,ldg", [(2, 8, 16, 64, 64, 64), (1, 18, 32, 128, 256, 256), (3, 6, 48, 64, 128, 132)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,ldg", [(2, 8, 16, 64, 64, 64), (1, 18, 32, 128, 256, 256), (3, 6, 48, 64, 128, 132),
+                                              (2, 24, 64, 64, 128, 128)])
 def test_conv3x3_wgrad_wino(pad_mode, B, H, W, Ci, Co, ldg):
     """mhada_conv3x3_wgrad_wino (the decoder's weight / bias gradients) against fp64: dW[co][tap][ci]
     = sum_pixels g * x_pad (the same im2col contraction the TN GEMM computes) and db = sum g; a
