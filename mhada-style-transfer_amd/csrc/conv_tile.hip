@@ -296,10 +296,11 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_c64_kernel(const ConvTileP p) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Direct 3x3 convolution for the decoder's 128-input-channel layers (conv.py:75-100: conv2.0
-// 128 -> 128 and conv2.1 128 -> 64 at half the output resolution), bf16 MFMA, fp32 accumulation,
-// reflect pad 1, bias + ReLU, NHWC.  The implicit GEMM ran them at 14-16 % of the bf16 peak
-// (K = 1152, N <= 128: per-tile prologue / epilogue, every input pixel gathered 9 times).  Here:
+// Direct 3x3 convolution for the decoder's 128 / 256-input-channel layers (conv.py:75-100: conv2.0
+// 128 -> 128 and conv2.1 128 -> 64 at half the output resolution, conv1.4 256 -> 128), bf16 MFMA,
+// fp32 accumulation, reflect pad 1, bias + ReLU, NHWC.  The implicit GEMM ran the first two at
+// 14-16 % of the bf16 peak (K = 1152, N <= 128: per-tile prologue / epilogue, every input pixel
+// gathered 9 times).  Here (Cin = 128; Cin = 256 uses 4-row tiles, see below):
 //   * the output tile of 8 x 32 pixels stages its 10 x 34 x 128-channel halo ONCE in LDS
 //     (85 KiB; 256-B pixel rows, chunk c at c ^ (row & 15): conflict-free ds_read_b128 over 16
 //     consecutive pixels), prefetched into registers during the previous tile's MFMAs;
@@ -309,7 +310,8 @@ __global__ void __launch_bounds__(kNT, 1) conv3x3_c64_kernel(const ConvTileP p) 
 //     ring runs on across tiles.  ONE barrier per stage, placed before the stage's last k-step:
 //     it proves every wave has read the stage's slot (the last k-step's fragments are already
 //     in registers) and publishes the next stage, whose first fragments are then read beside
-//     that last k-step's MFMAs;
+//     that last k-step's MFMAs.  The slots are three separate __shared__ objects and the DMA
+//     issue is pinned after the barrier (see the comments at sW0 and at the DMA call);
 //   * 4 waves (one per SIMD), wave w = output rows 2w, 2w+1 x all Cout: per 16-channel k-step
 //     Cout/32 + 2 ds_read_b128 per 2 Cout/32 MFMAs (v_mfma_f32_32x32x16_bf16), within the LDS
 //     budget of one read per MFMA; output rows staged in LDS (aliasing the halo after a barrier)
