@@ -208,8 +208,8 @@ def proj_suite():
     Nc = Ns = 4096, 8 heads, fp32 and bf16): q (N = 64, centred A) and K|V' (N = 128 with the
     V'^T image); plus the uncentred q form (which routes to the fp32 LDS-DMA ring kernel)."""
     dev = "cuda"
-    B, H, N, C = 8, 8, 4096, 512
-    for dt in (torch.float32, torch.bfloat16):
+    H, C = 8, 512
+    for B, N, dt in ((8, 4096, torch.float32), (8, 4096, torch.bfloat16), (4, 16384, torch.bfloat16)):
         x = torch.randn(B, N, C, device=dev)
         mu = x.mean(dim=1)
         wq = (torch.randn(B, H, 64, 64, device=dev) / 8).to(dt)
@@ -230,7 +230,7 @@ def proj_suite():
                "kv_vt": lambda: ops.gemm(**ka)}
         t = bench(fns)
         qb, kb = 4 * B * N * C // 8 + B * H * N * 64 * q.element_size(), 4 * B * N * C // 8 + 3 * B * H * N * 64 * q.element_size()
-        print(f"proj {str(dt)[6:]:8s}: " + "  ".join(
+        print(f"proj {str(dt)[6:]:8s} B{B} N{N}: " + "  ".join(
             f"{k} {v * 1e3:6.1f} us {(kb if k.startswith('kv') else qb) / v / 1e6:6.0f} GB/s" for k, v in t.items()))
 
 
