@@ -35,12 +35,22 @@ enum {
   MHADA_A_PATCH8 = 1,      /* A = im2col of an NCHW fp32 image, 8x8 patches, stride 8     */
   MHADA_A_CONV3X3 = 2,     /* A = im2col of NHWC input, 3x3 taps, ReflectionPad2d(1)      */
   MHADA_A_CONV3X3_UP2 = 3, /* as CONV3X3 on bilinear-x2(input) (align_corners=False)      */
-  MHADA_A_CONV3X3_ZERO = 4 /* 3x3 taps with ZERO padding `pad` (1: same size, as VGG19's
+  MHADA_A_CONV3X3_ZERO = 4, /* 3x3 taps with ZERO padding `pad` (1: same size, as VGG19's
                               nn.Conv2d(padding=1); 2: the full correlation, out = in + 2 —
                               the input gradient of a padded 3x3 conv)                   */
+  MHADA_A_SPLIT3 = 5       /* (ABI 15) fp32-accurate products on the bf16 MFMA: A = three bf16
+                              planes [3][M][lda] of an fp32 matrix (x = p0 + p1 + p2, as
+                              mhada_layernorm writes with y_dtype MHADA_BF16X3); K = 6 K0 is
+                              virtual — K-block t (K0 columns) reads plane 1, 2, 0, 1, 0, 0 —
+                              and W is the matching [N][6 K0] bf16 concatenation
+                              q1 | q0 | q2 | q0 | q1 | q0 of W's planes.  bf16 compute,
+                              nb1 = nb2 = 1, N > 128, K0 % 64 == 0, no centring / vt.   */
 };
+/* mhada_layernorm's y_dtype for the MHADA_A_SPLIT3 operand: three bf16 planes [3][rows][cols],
+ * p0 = bf16(y), p1 = bf16(y - p0), p2 = bf16(y - p0 - p1) of the fp32 result y (ABI 15) */
+enum { MHADA_BF16X3 = 2 };
 
-int mhada_abi_version(void);  /* 14 (mhada_cosine_moments / mhada_cosine_attn, mhada_warp_bwd; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 15 (mhada_gemm a_mode MHADA_A_SPLIT3, mhada_layernorm y_dtype MHADA_BF16X3; 14: mhada_cosine_moments / mhada_cosine_attn, mhada_warp_bwd; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -116,7 +126,9 @@ typedef struct mhada_gemm_args {
 int mhada_gemm(const mhada_gemm_args* args, mhada_stream_t stream);
 
 /* Row LayerNorm over `cols` (eps 1e-6 in the ViT): y = (x-mean)/sqrt(var+eps)*gamma + beta.
- * x fp32 [rows][cols]; y dtype y_dtype.  Replaces nn.LayerNorm (vit.py:54-55,58,62). */
+ * x fp32 [rows][cols]; y dtype y_dtype (MHADA_F32, MHADA_BF16, or MHADA_BF16X3: y = three bf16
+ * planes [3][rows][cols] of the fp32 result, the MHADA_A_SPLIT3 GEMM operand).  Replaces
+ * nn.LayerNorm (vit.py:54-55,58,62). */
 int mhada_layernorm(const float* x, void* y, int y_dtype, const float* gamma, const float* beta,
                     int rows, int cols, float eps, mhada_stream_t stream);
 

@@ -91,6 +91,14 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
       if (a->a_mu) return fail("mhada_gemm: centring only in ROWS mode");
       break;
     }
+    case MHADA_A_SPLIT3:
+      if (a->compute != MHADA_BF16 || a->a_dtype != MHADA_BF16)
+        return fail("mhada_gemm: SPLIT3 needs bf16 planes and bf16 compute");
+      if (a->nb1 * a->nb2 != 1 || a->a_mu || a->vt) return fail("mhada_gemm: SPLIT3 is one problem, no centring / vt");
+      if (a->K % 384) return fail("mhada_gemm: SPLIT3 needs K = 6 K0 with K0 % 64 == 0");
+      if (a->lda % 8 || a->lda < a->K / 6) return fail("mhada_gemm: SPLIT3 lda must be a multiple of 8 and >= K0");
+      p.spl = (long long)a->M * a->lda;
+      break;
     default:
       return fail("mhada_gemm: bad a_mode");
   }

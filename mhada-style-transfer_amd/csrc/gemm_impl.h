@@ -39,6 +39,7 @@ struct GemmP {
   int rinit;    // persistent ping-pong, fp32 C, no ReLU: residual + bias loaded into the accumulators
   void* c2; long long ldc2, sc21, sc22;  // optional bf16 copy of an fp32 C
   void* vt; long long ldt, svt1, svt2;   // optional transposed V' image (K|V' projection, N = 128)
+  long long spl;  // MHADA_A_SPLIT3: element stride between the three bf16 planes of A (M * lda)
 };
 
 template <typename TC> struct Cfg {
@@ -120,6 +121,13 @@ MHADA_DEV bool conv_src(const GemmP& p, int y, int x, int dy, int dx, int& Y, in
 // Internal A mode: ROWS with per-column centring (a_mu != NULL), a separate instantiation so
 // the plain ROWS path stages raw chunks with no per-element work.
 constexpr int kRowsCentred = 100;
+// MHADA_A_SPLIT3 (fp32-accurate products on the bf16 MFMA): A is three bf16 planes p0 + p1 + p2 of
+// an fp32 matrix (8 + 8 + 8 mantissa bits), the GEMM's K = 6 K0 is virtual: K-block t (K0 columns)
+// reads plane kSplitPlanes[t] = 1, 2, 0, 1, 0, 0 and W holds the matching [N][6 K0] concatenation
+// q1 | q0 | q2 | q0 | q1 | q0, so the fp32 accumulators sum p1 q1 + p2 q0 + p0 q2 + p1 q0 + p0 q1 +
+// p0 q0 — the six cross products above 2^-24, smallest first (the three dropped are < 2^-32).
+constexpr int kRowsSplit3 = 101;
+constexpr int kSplitPlanes = 0x001021;  // nibble t = plane of K-block t
 
 // ------------------------------------------------------------------------------------
 // A-operand staging for one K step.  Each thread owns A_CH chunks: rows (tid>>3)+32*i,
@@ -945,7 +953,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
         const int m = min(s.m0 + 128 * hh + rr, p.M - 1);
         const int n = min(s.n0 + 128 * (hh % NWH) + rr, p.N - 1);
         s.woff[hh][i] = (unsigned)((long long)n * p.ldw + cofs[i]);
-        if constexpr (AMODE == MHADA_A_ROWS) {
+        if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsSplit3) {
           s.aoff[hh][i] = (unsigned)((long long)m * p.lda + cofs[i]);
         } else {
           const int hw = p.out_h * p.out_w;
@@ -963,6 +971,13 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     if constexpr (AMODE == MHADA_A_ROWS) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds16(s.ab + s.aoff[hh][i] + k0, dst + PE * i);
+    } else if constexpr (AMODE == kRowsSplit3) {
+      // K-tile kt of the virtual 6 K0: block t = kt / ktb (compares: kt is wave-uniform), its plane
+      const int ktb = p.K / (6 * BK);
+      const int t = (kt >= ktb) + (kt >= 2 * ktb) + (kt >= 3 * ktb) + (kt >= 4 * ktb) + (kt >= 5 * ktb);
+      const TC* src = s.ab + ((kSplitPlanes >> (4 * t)) & 15) * p.spl + (kt - t * ktb) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(src + s.aoff[hh][i], dst + PE * i);
     } else {
       const int cin_n = p.img_c;
       const int tap = k0 / cin_n, cin0 = k0 - tap * cin_n;
@@ -1135,7 +1150,7 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
   while (true) {
     // KT >= 2 (checked on the host); the first K-tile skips the pre-staged W and may leave the
     // previous epilogue's stores in flight (wx)
-    if constexpr (AMODE == MHADA_A_ROWS) {
+    if constexpr (AMODE == MHADA_A_ROWS || AMODE == kRowsSplit3) {
       for (int kt = 0; kt + 2 < KT; ++kt) ktile(cur, kt + 1, kt > 0 || !pre, cur, kt + 2, true, kt == 0 && pre);
       ktile(cur, KT - 1, KT > 2 || !pre, nxt, 0, has_nxt, KT == 2 && pre);
     } else {
@@ -1154,7 +1169,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
     // residual loads follow the stores and its first MFMA needs them.
     // (ROWS only: in the implicit-GEMM conv instantiations the extra specialisation of the first
     // K-tile raised register spills and measured slower)
-    pre = AMODE == MHADA_A_ROWS && has_nxt && !p.rinit && cur.m0 + 256 <= p.M && cur.n0 + BN <= p.N;
+    pre = (AMODE == MHADA_A_ROWS || AMODE == kRowsSplit3) && has_nxt && !p.rinit && cur.m0 + 256 <= p.M &&
+          cur.n0 + BN <= p.N;
     if (pre) {
       stage_w(nxt, 0, 1, sl1);
       if constexpr (NWH == 2) stage_w(nxt, 1, 1, sl1);
@@ -1313,12 +1329,12 @@ static int launch_gemm_pp(const GemmP& p0, int nz, hipStream_t stream) {
   p.rinit = (sizeof(TO) == 4 && p.r && !p.relu && tuning().gemm_rinit && ((uintptr_t)p.r & 15) == 0 &&
              p.ldr % 4 == 0 && p.sr1 % 4 == 0 && p.sr2 % 4 == 0 && p.N % 4 == 0) ? 1 : 0;
   const long long total = (long long)p.ntiles * nz;
-  if (sizeof(TC) == 4 || BN != 256 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
+  if (sizeof(TC) == 4 || BN != 256 || AMODE == kRowsSplit3 || (p.K >= 128 && persist_enabled() && total < (1LL << 31))) {
     const int grid = (int)std::min<long long>(total, num_cus());
     hipLaunchKernelGGL((gemm_ppp_kernel<TC, TO, AMODE, BN>), dim3(grid), dim3(512), 0, stream, p, (int)total);
     return check_launch("mhada_gemm");
   }
-  if constexpr (sizeof(TC) == 2 && BN == 256) {
+  if constexpr (sizeof(TC) == 2 && BN == 256 && AMODE != kRowsSplit3) {
     hipLaunchKernelGGL((gemm_pp_kernel<TO, AMODE>), dim3(p.ntiles, nz), dim3(512), 0, stream, p);
     return check_launch("mhada_gemm");
   }
@@ -1450,6 +1466,14 @@ static int dispatch_mode(int mode, const GemmP& p, int nz, hipStream_t s) {
     case MHADA_A_PATCH8:
       if constexpr (sizeof(TA) == 4) return dispatch_tile<TC, TA, TO, MHADA_A_PATCH8>(p, nz, s);
       return fail("mhada_gemm: PATCH8 needs an fp32 image");
+    case MHADA_A_SPLIT3:
+      // the persistent ping-pong kernel only (its K-tile walk knows the planes)
+      if constexpr (sizeof(TC) == 2 && sizeof(TA) == 2) {
+        if (nz != 1 || p.N <= 128 || p.K % (6 * 64) || p.K < 6 * 64 || !pp_offsets_fit(p, MHADA_A_ROWS))
+          return fail("mhada_gemm: SPLIT3 needs one problem, N > 128, K0 = K / 6 a multiple of 64 and 32-bit offsets");
+        return launch_gemm_pp<bf16, TO, kRowsSplit3>(p, nz, s);
+      }
+      return fail("mhada_gemm: SPLIT3 needs bf16 planes and bf16 compute");
   }
   return fail("mhada_gemm: bad a_mode");
 }

@@ -12,7 +12,7 @@ namespace mhada {
 // LayerNorm (vit.py:54-55): one wave per row, VPL = cols/64 values per lane, two-pass in
 // registers (mean, then centred sum of squares) — biased variance as nn.LayerNorm.
 // ---------------------------------------------------------------------------------------
-template <typename TO, int VPL>
+template <typename TO, int VPL, bool SPLIT = false>
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, TO* __restrict__ y,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ b, int rows, float eps) {
@@ -39,12 +39,23 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
   }
   const float rstd = rsqrtf(wave_sum(ss) * (1.0f / COLS) + eps);
   TO* yr = y + (long long)row * COLS;
+  const long long plane = (long long)rows * COLS;
 #pragma unroll
   for (int i = 0; i < VPL / 4; ++i) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = (i * 64 + lane) * 4 + e;
-      yr[c] = from_f32<TO>((v[4 * i + e] - mean) * rstd * g[c] + b[c]);
+      const float val = (v[4 * i + e] - mean) * rstd * g[c] + b[c];
+      if constexpr (SPLIT) {  // three bf16 planes: val = p0 + p1 + p2 to 2^-25 (the SPLIT3 GEMM operand)
+        const bf16 p0 = (bf16)val;
+        const float r1 = val - (float)p0;
+        const bf16 p1 = (bf16)r1;
+        yr[c] = p0;
+        yr[plane + c] = p1;
+        yr[2 * plane + c] = (bf16)(r1 - (float)p1);
+      } else {
+        yr[c] = from_f32<TO>(val);
+      }
     }
   }
 }
@@ -781,7 +792,8 @@ using namespace mhada;
 extern "C" int mhada_layernorm(const float* x, void* y, int y_dtype, const float* gamma, const float* beta,
                                int rows, int cols, float eps, mhada_stream_t s_) {
   hipStream_t s = (hipStream_t)s_;
-  if (!x || !y || !gamma || !beta || rows < 0) return fail("mhada_layernorm: bad args");
+  if (!x || !y || !gamma || !beta || rows < 0 || y_dtype < MHADA_F32 || y_dtype > MHADA_BF16X3)
+    return fail("mhada_layernorm: bad args");
   if (rows == 0) return MHADA_OK;
   if (!aligned16(x)) return fail("mhada_layernorm: x must be 16-byte aligned");
   const dim3 grid((rows + 3) / 4), blk(256);
@@ -789,6 +801,8 @@ extern "C" int mhada_layernorm(const float* x, void* y, int y_dtype, const float
   case VPL * 64:                                                                                       \
     if (y_dtype == MHADA_F32)                                                                          \
       hipLaunchKernelGGL((layernorm_kernel<float, VPL>), grid, blk, 0, s, x, (float*)y, gamma, beta, rows, eps); \
+    else if (y_dtype == MHADA_BF16X3)                                                                  \
+      hipLaunchKernelGGL((layernorm_kernel<bf16, VPL, true>), grid, blk, 0, s, x, (bf16*)y, gamma, beta, rows, eps); \
     else                                                                                               \
       hipLaunchKernelGGL((layernorm_kernel<bf16, VPL>), grid, blk, 0, s, x, (bf16*)y, gamma, beta, rows, eps); \
     break;

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmhada_hi
 
 F32, BF16 = 0, 1
 ACT_SOFTMAX, ACT_COSINE = 0, 1
-A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO = 0, 1, 2, 3, 4
+A_ROWS, A_PATCH8, A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO, A_SPLIT3 = 0, 1, 2, 3, 4, 5
+BF16X3 = 2  # mhada_layernorm y_dtype: three bf16 planes (the A_SPLIT3 operand)
 PAD_REFLECT, PAD_ZERO = 0, 1
 
 _c_ll = ctypes.c_longlong
@@ -140,7 +141,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 def get_tuning(name: str) -> int:

@@ -151,6 +151,15 @@ def vit_prep(vit, dtype):
     return cached_prep(vit, dtype, build)
 
 
+def _w6(L: dict, key: str) -> torch.Tensor:
+    """The SPLIT3 form of an fp32 ViT weight (ops.split3_weight), built once per prepared layer."""
+    k6 = key + "_split3"
+    if k6 not in L:
+        with torch.no_grad():
+            L[k6] = ops.split3_weight(L[key])
+    return L[k6]
+
+
 def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
     """VisionTransformer.forward (vit.py:148-169) on the HIP path."""
     require_device(x, "VisionTransformer")
@@ -174,12 +183,21 @@ def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
     xs = tok.view(B * N, C)
     outs = []
     for L in prep["layers"]:
-        hb = ops.layernorm(xs, L["ln1_g"], L["ln1_b"], dt, L["eps"])
-        qkv = ops.linear(hb, L["w_qkv"], L["b_qkv"], dt)
+        split = dt == torch.float32 and ops.F32_SPLIT
+        if split:  # fp32: LayerNorm -> bf16 planes -> SPLIT3 GEMM (fp32-accurate on the bf16 MFMA)
+            qkv = ops.linear_split3(ops.layernorm_split3(xs, L["ln1_g"], L["ln1_b"], L["eps"]), _w6(L, "w_qkv"),
+                                    L["b_qkv"], dt)
+        else:
+            hb = ops.layernorm(xs, L["ln1_g"], L["ln1_b"], dt, L["eps"])
+            qkv = ops.linear(hb, L["w_qkv"], L["b_qkv"], dt)
         att = ops.vit_batch_attn(qkv.view(B, N, 3 * C), B, N, L["heads"])
         xs = ops.linear(att.view(B * N, C), L["w_o"], L["b_o"], torch.float32, residual=xs)
-        h2 = ops.layernorm(xs, L["ln2_g"], L["ln2_b"], dt, L["eps"])
-        m1 = ops.linear(h2, L["w1"], L["b1"], dt, relu=True)
+        if split:
+            m1 = ops.linear_split3(ops.layernorm_split3(xs, L["ln2_g"], L["ln2_b"], L["eps"]), _w6(L, "w1"),
+                                   L["b1"], dt, relu=True)
+        else:
+            h2 = ops.layernorm(xs, L["ln2_g"], L["ln2_b"], dt, L["eps"])
+            m1 = ops.linear(h2, L["w1"], L["b1"], dt, relu=True)
         xs = ops.linear(m1, L["w2"], L["b2"], torch.float32, residual=xs)
         outs.append(tokens_to_nchw(xs.view(B, N, C), h, w))
     return outs

@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO, A_PATCH8, A_ROWS, BF16, F32, GemmArgs, GemmTnArgs
+from ._lib import A_CONV3X3, A_CONV3X3_UP2, A_CONV3X3_ZERO, A_PATCH8, A_ROWS, A_SPLIT3, BF16, BF16X3, F32, GemmArgs, GemmTnArgs
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -288,6 +288,50 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, out_dtype: torc
     _call("mhada_layernorm", x, x.data_ptr(), y.data_ptr(), dt_code(out_dtype), g.data_ptr(), b.data_ptr(),
                                      rows, cols, eps)
     return y
+
+
+# fp32 GEMMs whose A comes from a LayerNorm (the ViT's QKV and MLP1) run as SPLIT3 products on the
+# bf16 MFMA (mhada_gemm a_mode MHADA_A_SPLIT3): fp32-accurate — against fp64 their error is below
+# the fp32 MFMA path's (tools/split_bf16_probe.py) — and 1.4-1.5x faster.  False: the fp32 MFMA.
+F32_SPLIT = True
+
+
+def layernorm_split3(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    """``mhada_layernorm`` with y_dtype MHADA_BF16X3: the fp32 LayerNorm of x as three bf16 planes
+    [3][rows][cols] (y = p0 + p1 + p2 to 2^-25 relative), the A operand of ``linear_split3``."""
+    _need_gpu(x, g, b)
+    rows, cols = x.shape
+    y = torch.empty(3, rows, cols, device=x.device, dtype=torch.bfloat16)
+    _call("mhada_layernorm", x, x.data_ptr(), y.data_ptr(), BF16X3, g.data_ptr(), b.data_ptr(), rows, cols, eps)
+    return y
+
+
+def split3_weight(w: torch.Tensor) -> torch.Tensor:
+    """An fp32 weight [N][K0] as the SPLIT3 GEMM's W operand: its bf16 planes q0 + q1 + q2 (8 + 8 + 8
+    mantissa bits) concatenated along K as q1 | q0 | q2 | q0 | q1 | q0 -> [N][6 K0] bf16 (one-time
+    weight preparation, cached with the module's other prepared weights)."""
+    w = w.float()
+    q0 = w.bfloat16()
+    r = w - q0.float()
+    q1 = r.bfloat16()
+    q2 = (r - q1.float()).bfloat16()
+    return torch.cat([q1, q0, q2, q0, q1, q0], dim=1).contiguous()
+
+
+def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
+                  residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+    """fp32-accurate x @ w^T (+bias, relu, residual) from x's bf16 planes [3][M][K0] and
+    ``split3_weight(w)`` [N][6 K0]: the six significant cross products summed in fp32 accumulators
+    on the bf16 MFMA (mhada_gemm MHADA_A_SPLIT3)."""
+    if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_contiguous():
+        raise ValueError("linear_split3: planes must be contiguous bf16 [3][M][K0]")
+    _, M, K0 = planes.shape
+    N = w6.shape[0]
+    if w6.dtype != torch.bfloat16 or w6.shape[1] != 6 * K0:
+        raise ValueError("linear_split3: w6 must be split3_weight(w), bf16 [N][6*K0]")
+    c = torch.empty(M, N, device=planes.device, dtype=out_dtype)
+    return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
+                ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)
 
 
 def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int, groups: int = 1) -> torch.Tensor:

@@ -53,6 +53,74 @@ def test_linear(cdt, M, N, K):
     assert rel(y2, ref2) < TOL[cdt] + (4e-3 if cdt == torch.bfloat16 else 0)
 
 
+@pytest.mark.parametrize("cols", [512, 1024])
+def test_layernorm_split3_planes(cols):
+    """mhada_layernorm y_dtype MHADA_BF16X3: plane 0 is the bf16 LayerNorm bit for bit; each later
+    plane is at most half a bf16 ulp of the one before (a non-overlapping expansion); the sum agrees
+    with the fp32 LayerNorm to a few fp32 ulp of the affine step's O(1) terms (the two kernel
+    instantiations may contract (x - mean) * rstd * g + b into FMAs differently: where y cancels to
+    ~1e-5 that is a large RELATIVE difference of two equally valid fp32 evaluations)."""
+    x = rnd(3001, cols, seed=11) * 3 + 0.5
+    g = rnd(cols, seed=12)
+    b = rnd(cols, seed=13)
+    pl = ops.layernorm_split3(x, g, b, 1e-6)
+    y32 = ops.layernorm(x, g, b, torch.float32, 1e-6)
+    assert torch.equal(pl[0], ops.layernorm(x, g, b, torch.bfloat16, 1e-6))
+    p0, p1, p2 = (pl[i].double() for i in range(3))
+    assert (p1.abs() <= p0.abs() * 2.0 ** -8).all() and (p2.abs() <= p1.abs() * 2.0 ** -8).all()
+    s = p0 + p1 + p2
+    assert ((s - y32.double()).abs() <= 2.0 ** -20 * (y32.double().abs() + b.double().abs() + 4 * g.double().abs())).all()
+
+
+@pytest.mark.parametrize("M,N,K0", [(4096, 1536, 512), (1000, 2048, 512), (70000, 768, 512), (333, 512, 2048),
+                                    (300, 256, 256), (257, 2048, 1024)])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (False, True)])
+def test_linear_split3_fp32_accuracy(M, N, K0, relu, res):
+    """SPLIT3 (fp32-accurate products on the bf16 MFMA, mhada_gemm MHADA_A_SPLIT3): against fp64 at
+    an fp32-class error (< 2e-6, a tenth of the fp32 kernel tolerance) and within 2.5x of the fp32
+    MFMA GEMM's error on the same operands — the products are exact to 2^-24, the accumulator sees
+    6 K0 instead of K0 roundings (measured: below the fp32 path without a residual, up to 1.75x it
+    with a residual preloaded into the accumulators); bias / ReLU / residual epilogues, partial row
+    tiles, one to several tiles per CU, K0 = 256 .. 2048; run-to-run bit-identical."""
+    x = rnd(M, K0, seed=1) * 2
+    w = rnd(N, K0, scale=K0 ** -0.5, seed=2)
+    b = rnd(N, seed=3)
+    r = rnd(M, N, seed=4) if res else None
+    g1 = torch.ones(K0, device=DEV)
+    b0 = torch.zeros(K0, device=DEV)
+    # the planes of x itself: LayerNorm with unit gain of an already-normalised x is x up to its
+    # own rounding, so use the LayerNorm output y as THE fp32 operand of both paths
+    y = ops.layernorm(x, g1, b0, torch.float32, 1e-6)
+    pl = ops.layernorm_split3(x, g1, b0, 1e-6)
+    w6 = ops.split3_weight(w)
+    out = ops.linear_split3(pl, w6, b, torch.float32, residual=r, relu=relu)
+    out2 = ops.linear_split3(pl, w6, b, torch.float32, residual=r, relu=relu)
+    assert torch.equal(out, out2)
+    ref = y.double() @ w.double().T + b.double()
+    if relu:
+        ref = torch.relu(ref)
+    if res:
+        ref = ref + r.double()
+    f32 = ops.linear(y, w, b, torch.float32, residual=r, relu=relu)
+    e_split, e_f32 = rel(out, ref), rel(f32, ref)
+    assert e_split < 2e-6, (e_split, e_f32)
+    assert e_split <= 2.5 * e_f32 + 1e-7, (e_split, e_f32)
+
+
+def test_linear_split3_rejects_unsupported_shapes():
+    """SPLIT3 runs only on the persistent ping-pong kernel: N <= 128 fails loudly in the library,
+    mismatched operands in the host wrapper."""
+    x = rnd(256, 512, seed=1)
+    g1, b0 = torch.ones(512, device=DEV), torch.zeros(512, device=DEV)
+    pl = ops.layernorm_split3(x, g1, b0, 1e-6)
+    with pytest.raises(ValueError, match="SPLIT3"):
+        ops.linear_split3(pl, ops.split3_weight(rnd(128, 512, seed=2)), None, torch.float32)
+    with pytest.raises(ValueError):
+        ops.linear_split3(pl, ops.split3_weight(rnd(256, 256, seed=2)), None, torch.float32)
+    with pytest.raises(ValueError):
+        ops.linear_split3(pl[:, :, :256], ops.split3_weight(rnd(256, 256, seed=2)), None, torch.float32)
+
+
 @pytest.mark.parametrize("M,N,K", [(70000, 1024, 64), (70000, 768, 512), (32400, 512, 2048), (57000, 600, 96),
                                    (65536, 2048, 512)])
 def test_gemm_f32_persistent_epilogues(M, N, K):
