@@ -121,6 +121,10 @@ typedef struct mhada_gemm_args {
    * (dtype of C; row stride ldt >= M rounded up to 64, z-strides svt1/svt2; pos = the
    * mhada_transpose_v key order; positions M..ldt-1 written 0).  Replaces mhada_transpose_v. */
   void* vt; long long ldt, svt1, svt2;
+  /* (ABI 15) 1: c2 receives the fp32 result as three bf16 planes [3][M][ldc2] (p0 = bf16(y),
+   * p1 = bf16(y - p0), p2 = bf16(y - p0 - p1): the MHADA_A_SPLIT3 operand of the next GEMM) and
+   * C may be NULL (not written).  SPLIT3 mode, fp32 C dtype, one problem. */
+  int c2_planes;
 } mhada_gemm_args;
 
 int mhada_gemm(const mhada_gemm_args* args, mhada_stream_t stream);

@@ -18,7 +18,10 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   if (a->r && a->r_dtype != a->c_dtype) return fail("mhada_gemm: residual dtype must equal output dtype");
   if (a->compute == MHADA_F32 && (a->a_dtype != MHADA_F32 || a->c_dtype != MHADA_F32))
     return fail("mhada_gemm: fp32 compute needs fp32 A and C");
-  if (!a->a || !a->w || !a->c) return fail("mhada_gemm: null operand");
+  if (!a->a || !a->w || (!a->c && !a->c2_planes)) return fail("mhada_gemm: null operand");
+  if (a->c2_planes && (a->a_mode != MHADA_A_SPLIT3 || !a->c2 || a->c_dtype != MHADA_F32 || a->N % 4 ||
+                       !tuning().gemm_ldsepi))
+    return fail("mhada_gemm: c2_planes needs SPLIT3 mode, a c2 buffer, fp32 C, N % 4 == 0 and the LDS epilogue");
   const int ec = a->compute == MHADA_F32 ? 4 : 8;      // compute elements per 16 B
   const int ea = a->a_dtype == MHADA_F32 ? 4 : 8;      // A elements per 16 B
   const int bk = a->compute == MHADA_F32 ? 32 : 64;
@@ -48,6 +51,7 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
     return fail("mhada_gemm: relu = 2 (ReLU-adjoint mask) needs fp32 C, an fp32 mask in r, ROWS mode, no c2 / vt");
   p.relu = a->relu;
   p.c2 = a->c2; p.ldc2 = a->ldc2; p.sc21 = a->sc21; p.sc22 = a->sc22;
+  p.c2planes = a->c2_planes ? 1 : 0;
   p.vt = a->vt; p.ldt = a->ldt; p.svt1 = a->svt1; p.svt2 = a->svt2;
   if (a->c2 && (a->c_dtype != MHADA_F32 || ((uintptr_t)a->c2 & 7) || a->ldc2 % 4 || a->sc21 % 4 || a->sc22 % 4))
     return fail("mhada_gemm: c2 (bf16 copy) needs fp32 C, 8-byte alignment and strides that are multiples of 4");

@@ -40,6 +40,7 @@ struct GemmP {
   void* c2; long long ldc2, sc21, sc22;  // optional bf16 copy of an fp32 C
   void* vt; long long ldt, svt1, svt2;   // optional transposed V' image (K|V' projection, N = 128)
   long long spl;  // MHADA_A_SPLIT3: element stride between the three bf16 planes of A (M * lda)
+  int c2planes;   // c2 = three bf16 planes [3][M][ldc2] of the fp32 result (C may be null)
 };
 
 template <typename TC> struct Cfg {
@@ -368,10 +369,25 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[e] = p.relu == 2 ? (q[e] > 0.f ? x[e] : 0.f) : x[e] + q[e];
             }
-            *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
-            if (p.c2)
-              *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 +
-                                         (long long)m * p.ldc2 + n) = bf16x4{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+            if (p.c) *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+            if (p.c2) {
+              bf16* c2row = reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 + (long long)m * p.ldc2 + n;
+              const bf16x4 h0 = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+              *reinterpret_cast<bf16x4*>(c2row) = h0;
+              if (p.c2planes) {  // the SPLIT3 operand of the next GEMM: x = p0 + p1 + p2
+                const long long pl = (long long)p.M * p.ldc2;
+                float r1[4];
+                bf16x4 h1, h2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  r1[e] = x[e] - (float)h0[e];
+                  h1[e] = (bf16)r1[e];
+                  h2[e] = (bf16)(r1[e] - (float)h1[e]);
+                }
+                *reinterpret_cast<bf16x4*>(c2row + pl) = h1;
+                *reinterpret_cast<bf16x4*>(c2row + 2 * pl) = h2;
+              }
+            }
           } else {
             if (rrow) {
               const bf16x4 q = *reinterpret_cast<const bf16x4*>(rrow + n);

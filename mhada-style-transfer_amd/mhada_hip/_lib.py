@@ -38,6 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("relu", ctypes.c_int), ("pad", ctypes.c_int),
         ("c2", _vp), ("ldc2", _c_ll), ("sc21", _c_ll), ("sc22", _c_ll),
         ("vt", _vp), ("ldt", _c_ll), ("svt1", _c_ll), ("svt2", _c_ll),
+        ("c2_planes", ctypes.c_int),
     ]
 
 

@@ -192,13 +192,14 @@ def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
             qkv = ops.linear(hb, L["w_qkv"], L["b_qkv"], dt)
         att = ops.vit_batch_attn(qkv.view(B, N, 3 * C), B, N, L["heads"])
         xs = ops.linear(att.view(B * N, C), L["w_o"], L["b_o"], torch.float32, residual=xs)
-        if split:
+        if split:  # MLP1 writes its ReLU output as planes, MLP2 consumes them (SPLIT3 both)
             m1 = ops.linear_split3(ops.layernorm_split3(xs, L["ln2_g"], L["ln2_b"], L["eps"]), _w6(L, "w1"),
-                                   L["b1"], dt, relu=True)
+                                   L["b1"], dt, relu=True, out_planes=True)
+            xs = ops.linear_split3(m1, _w6(L, "w2"), L["b2"], torch.float32, residual=xs)
         else:
             h2 = ops.layernorm(xs, L["ln2_g"], L["ln2_b"], dt, L["eps"])
             m1 = ops.linear(h2, L["w1"], L["b1"], dt, relu=True)
-        xs = ops.linear(m1, L["w2"], L["b2"], torch.float32, residual=xs)
+            xs = ops.linear(m1, L["w2"], L["b2"], torch.float32, residual=xs)
         outs.append(tokens_to_nchw(xs.view(B, N, C), h, w))
     return outs
 

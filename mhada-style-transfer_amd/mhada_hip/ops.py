@@ -62,12 +62,18 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
          r: Optional[torch.Tensor] = None, ldr: int = 0, sr=(0, 0),
          ldc: int = 0, sc=(0, 0), relu: bool = False, pad: int = 0,
          c2: Optional[torch.Tensor] = None, ldc2: int = 0, sc2=(0, 0),
-         vt: Optional[torch.Tensor] = None, ldt: int = 0, svt=(0, 0)) -> torch.Tensor:
+         vt: Optional[torch.Tensor] = None, ldt: int = 0, svt=(0, 0), c2_planes: bool = False) -> torch.Tensor:
     """``mhada_gemm``: C[z] = act(A[z] W[z]^T + bias[z]) + R[z]; strides in elements.  Optional
-    c2 (a bf16 copy of an fp32 C) and vt (the transposed V' image of the K|V' projection)."""
+    c2 (a bf16 copy of an fp32 C; ``c2_planes``: C's three bf16 planes [3][M][ldc2], the next
+    SPLIT3 GEMM's operand, with C None = not written) and vt (the transposed V' image of the
+    K|V' projection)."""
     _need_gpu(a, w, c, a_mu, bias, r, c2, vt)
-    if c2 is not None and (c2.dtype != torch.bfloat16 or c.dtype != torch.float32):
+    if c is None and not c2_planes:
+        raise ValueError("gemm: C may be None only with c2_planes")
+    if c2 is not None and (c2.dtype != torch.bfloat16 or (c is not None and c.dtype != torch.float32)):
         raise ValueError("c2 is the bf16 copy of an fp32 C")
+    if c2_planes and (c2 is None or c2.shape[0] != 3 or not c2.is_contiguous()):
+        raise ValueError("c2_planes needs c2 = contiguous bf16 [3][M][ldc2]")
     if vt is not None and vt.dtype != c.dtype:
         raise ValueError("vt has the dtype of C")
     if w.dtype != compute:
@@ -95,7 +101,7 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     args.r_dtype = dt_code(r.dtype) if r is not None else 0
     args.ldr = ldr
     args.sr1, args.sr2 = sr
-    args.c, args.c_dtype, args.ldc = c.data_ptr(), dt_code(c.dtype), ldc
+    args.c, args.c_dtype, args.ldc = _ptr(c), dt_code(c.dtype) if c is not None else F32, ldc
     args.sc1, args.sc2 = sc
     args.relu = int(relu)
     args.pad = int(pad)
@@ -103,8 +109,9 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     args.sc21, args.sc22 = sc2
     args.vt, args.ldt = _ptr(vt), ldt
     args.svt1, args.svt2 = svt
-    _call("mhada_gemm", c, ctypes.byref(args))
-    return c
+    args.c2_planes = int(c2_planes)
+    _call("mhada_gemm", a, ctypes.byref(args))
+    return c if c is not None else c2
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
@@ -319,16 +326,25 @@ def split3_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
-                  residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+                  residual: Optional[torch.Tensor] = None, relu: bool = False,
+                  out_planes: bool = False) -> torch.Tensor:
     """fp32-accurate x @ w^T (+bias, relu, residual) from x's bf16 planes [3][M][K0] and
     ``split3_weight(w)`` [N][6 K0]: the six significant cross products summed in fp32 accumulators
-    on the bf16 MFMA (mhada_gemm MHADA_A_SPLIT3)."""
+    on the bf16 MFMA (mhada_gemm MHADA_A_SPLIT3).  ``out_planes``: return the fp32 result as its
+    three bf16 planes [3][M][N] (the next SPLIT3 GEMM's operand) instead of an fp32 [M][N]."""
     if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_contiguous():
         raise ValueError("linear_split3: planes must be contiguous bf16 [3][M][K0]")
     _, M, K0 = planes.shape
     N = w6.shape[0]
     if w6.dtype != torch.bfloat16 or w6.shape[1] != 6 * K0:
         raise ValueError("linear_split3: w6 must be split3_weight(w), bf16 [N][6*K0]")
+    if out_planes:
+        if out_dtype != torch.float32:
+            raise ValueError("linear_split3: out_planes splits an fp32 result")
+        c2 = torch.empty(3, M, N, device=planes.device, dtype=torch.bfloat16)
+        return gemm(a=planes, w=w6, c=None, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
+                    ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu,
+                    c2=c2, ldc2=N, c2_planes=True)
     c = torch.empty(M, N, device=planes.device, dtype=out_dtype)
     return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
                 ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)

@@ -107,6 +107,34 @@ def test_linear_split3_fp32_accuracy(M, N, K0, relu, res):
     assert e_split <= 2.5 * e_f32 + 1e-7, (e_split, e_f32)
 
 
+@pytest.mark.parametrize("M,N,K0", [(4096, 2048, 512), (1000, 512, 256), (70000, 1024, 512)])
+def test_linear_split3_plane_output_chain(M, N, K0):
+    """SPLIT3 with the result written as three bf16 planes (c2_planes, C not written): the planes
+    are the split of exactly the fp32 result the plain SPLIT3 call returns (plane 0 = its bf16
+    rounding, the sum within 2^-26), and a MLP1 -> MLP2 chain through them (ReLU, then a residual)
+    matches fp64 at an fp32-class error."""
+    x = rnd(M, K0, seed=1) * 2
+    w1 = rnd(N, K0, scale=K0 ** -0.5, seed=2)
+    b1 = rnd(N, seed=3)
+    g1, b0 = torch.ones(K0, device=DEV), torch.zeros(K0, device=DEV)
+    y = ops.layernorm(x, g1, b0, torch.float32, 1e-6)
+    pl = ops.layernorm_split3(x, g1, b0, 1e-6)
+    w16 = ops.split3_weight(w1)
+    full = ops.linear_split3(pl, w16, b1, torch.float32, relu=True)
+    m1 = ops.linear_split3(pl, w16, b1, torch.float32, relu=True, out_planes=True)
+    assert m1.shape == (3, M, N) and m1.dtype == torch.bfloat16
+    assert torch.equal(m1[0], full.bfloat16())
+    s = m1[0].double() + m1[1].double() + m1[2].double()
+    assert ((s - full.double()).abs() <= full.double().abs() * 2.0 ** -26).all()
+    w2 = rnd(K0, N, scale=N ** -0.5, seed=5)
+    b2 = rnd(K0, seed=6)
+    r = rnd(M, K0, seed=7)
+    out = ops.linear_split3(m1, ops.split3_weight(w2), b2, torch.float32, residual=r)
+    h = torch.relu(y.double() @ w1.double().T + b1.double())
+    ref = h @ w2.double().T + b2.double() + r.double()
+    assert rel(out, ref) < 2e-6
+
+
 def test_linear_split3_rejects_unsupported_shapes():
     """SPLIT3 runs only on the persistent ping-pong kernel: N <= 128 fails loudly in the library,
     mismatched operands in the host wrapper."""
