@@ -314,7 +314,8 @@ MHADA_DEV void store_tile(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, i
 // bias, ReLU and the residual (read in the same coalesced layout) are applied in row layout.
 // The 16-B chunk c of row r sits at slot c ^ (r & 7) (spreads both the column-group writes and
 // the row reads over the banks).  No barrier: each wave owns its scratch.
-template <typename TO, int TM, int TN>
+// PLANES (the SPLIT3 kernel only): c2 may hold the result's three bf16 planes and C may be null.
+template <typename TO, int TM, int TN, bool PLANES = false>
 MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z1, int z2, int mrow0, int ncol0,
                               int lane, float* scr) {
   TO* cbase = reinterpret_cast<TO*>(p.c) + z1 * p.sc1 + z2 * p.sc2;
@@ -369,12 +370,12 @@ MHADA_DEV void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TM][TN], int z
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[e] = p.relu == 2 ? (q[e] > 0.f ? x[e] : 0.f) : x[e] + q[e];
             }
-            if (p.c) *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
+            if (!PLANES || p.c) *reinterpret_cast<f32x4*>(crow + n) = f32x4{x[0], x[1], x[2], x[3]};
             if (p.c2) {
               bf16* c2row = reinterpret_cast<bf16*>(p.c2) + z1 * p.sc21 + z2 * p.sc22 + (long long)m * p.ldc2 + n;
               const bf16x4 h0 = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
               *reinterpret_cast<bf16x4*>(c2row) = h0;
-              if (p.c2planes) {  // the SPLIT3 operand of the next GEMM: x = p0 + p1 + p2
+              if (PLANES && p.c2planes) {  // the SPLIT3 operand of the next GEMM: x = p0 + p1 + p2
                 const long long pl = (long long)p.M * p.ldc2;
                 float r1[4];
                 bf16x4 h1, h2;
@@ -1198,7 +1199,8 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
         if constexpr (sizeof(TO) == 2 && TN == 2) {
           store_tile_lds_bf16<4>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
         } else {
-          store_tile_lds<TO, 4, TN>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128, cur.n0 + wc * TN * 32, lane, scr);
+          store_tile_lds<TO, 4, TN, AMODE == kRowsSplit3>(pe, acc, cur.z1, cur.z2, cur.m0 + grp * 128,
+                                                           cur.n0 + wc * TN * 32, lane, scr);
         }
       }
       else
