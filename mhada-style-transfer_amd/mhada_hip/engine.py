@@ -151,6 +151,20 @@ def vit_prep(vit, dtype):
     return cached_prep(vit, dtype, build)
 
 
+_NUM_CUS: Dict = {}
+
+
+def _split3_fills(M: int, N: int, dev: torch.device) -> bool:
+    """ops.F32_SPLIT and the SPLIT3 GEMM's 256x256 tiles cover >= 7/8 of the CUs (the rule the fp32
+    GEMM dispatch uses for its own persistent kernel)."""
+    if not ops.F32_SPLIT:
+        return False
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _NUM_CUS:
+        _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return 8 * ((M + 255) // 256) * ((N + 255) // 256) >= 7 * _NUM_CUS[idx]
+
+
 def _w6(L: dict, key: str) -> torch.Tensor:
     """The SPLIT3 form of an fp32 ViT weight (ops.split3_weight), built once per prepared layer."""
     k6 = key + "_split3"
@@ -183,8 +197,12 @@ def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
     xs = tok.view(B * N, C)
     outs = []
     for L in prep["layers"]:
-        split = dt == torch.float32 and ops.F32_SPLIT
-        if split:  # fp32: LayerNorm -> bf16 planes -> SPLIT3 GEMM (fp32-accurate on the bf16 MFMA)
+        # fp32: LayerNorm -> bf16 planes -> SPLIT3 GEMM (fp32-accurate on the bf16 MFMA) where the
+        # 256x256 tiles fill the chip; small batches keep the fp32 MFMA GEMMs (their 128x128 tiles
+        # cover more CUs than 6x-longer SPLIT3 tiles would)
+        split = dt == torch.float32 and _split3_fills(B * N, 3 * C, xs.device)
+        split_mlp = dt == torch.float32 and _split3_fills(B * N, C, xs.device)
+        if split:
             qkv = ops.linear_split3(ops.layernorm_split3(xs, L["ln1_g"], L["ln1_b"], L["eps"]), _w6(L, "w_qkv"),
                                     L["b_qkv"], dt)
         else:
@@ -192,7 +210,7 @@ def vit_forward(vit, x: torch.Tensor) -> List[torch.Tensor]:
             qkv = ops.linear(hb, L["w_qkv"], L["b_qkv"], dt)
         att = ops.vit_batch_attn(qkv.view(B, N, 3 * C), B, N, L["heads"])
         xs = ops.linear(att.view(B * N, C), L["w_o"], L["b_o"], torch.float32, residual=xs)
-        if split:  # MLP1 writes its ReLU output as planes, MLP2 consumes them (SPLIT3 both)
+        if split_mlp:  # MLP1 writes its ReLU output as planes, MLP2 consumes them (SPLIT3 both)
             m1 = ops.linear_split3(ops.layernorm_split3(xs, L["ln2_g"], L["ln2_b"], L["eps"]), _w6(L, "w1"),
                                    L["b1"], dt, relu=True, out_planes=True)
             xs = ops.linear_split3(m1, _w6(L, "w2"), L["b2"], torch.float32, residual=xs)
