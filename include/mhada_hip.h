@@ -41,10 +41,11 @@ enum {
   MHADA_A_SPLIT3 = 5       /* (ABI 15) fp32-accurate products on the bf16 MFMA: A = three bf16
                               planes [3][M][lda] of an fp32 matrix (x = p0 + p1 + p2, as
                               mhada_layernorm writes with y_dtype MHADA_BF16X3); K = 6 K0 is
-                              virtual — K-block t (K0 columns) reads plane 1, 2, 0, 1, 0, 0 —
-                              and W is the matching [N][6 K0] bf16 concatenation
-                              q1 | q0 | q2 | q0 | q1 | q0 of W's planes.  bf16 compute,
-                              nb1 = nb2 = 1, N > 128, K0 % 64 == 0, no centring / vt.   */
+                              virtual — K-tile 6 kk + t reads columns 64 kk .. 64 kk + 63 of
+                              plane (1, 2, 0, 1, 0, 0)[t] — and W is the matching [N][6 K0]
+                              bf16 interleave: 64-column chunk kk of W's planes
+                              q1, q0, q2, q0, q1, q0 in turn.  bf16 compute, nb1 = nb2 = 1,
+                              N > 128, K0 % 64 == 0, no centring / vt.                  */
 };
 /* mhada_layernorm's y_dtype for the MHADA_A_SPLIT3 operand: three bf16 planes [3][rows][cols],
  * p0 = bf16(y), p1 = bf16(y - p0), p2 = bf16(y - p0 - p1) of the fp32 result y (ABI 15) */

@@ -123,10 +123,11 @@ MHADA_DEV bool conv_src(const GemmP& p, int y, int x, int dy, int dx, int& Y, in
 // the plain ROWS path stages raw chunks with no per-element work.
 constexpr int kRowsCentred = 100;
 // MHADA_A_SPLIT3 (fp32-accurate products on the bf16 MFMA): A is three bf16 planes p0 + p1 + p2 of
-// an fp32 matrix (8 + 8 + 8 mantissa bits), the GEMM's K = 6 K0 is virtual: K-block t (K0 columns)
-// reads plane kSplitPlanes[t] = 1, 2, 0, 1, 0, 0 and W holds the matching [N][6 K0] concatenation
-// q1 | q0 | q2 | q0 | q1 | q0, so the fp32 accumulators sum p1 q1 + p2 q0 + p0 q2 + p1 q0 + p0 q1 +
-// p0 q0 — the six cross products above 2^-24, smallest first (the three dropped are < 2^-32).
+// an fp32 matrix (8 + 8 + 8 mantissa bits), the GEMM's K = 6 K0 is virtual: K-tile 6 kk + t reads
+// columns 64 kk .. of plane kSplitPlanes[t] = 1, 2, 0, 1, 0, 0, and W holds the matching [N][6 K0]
+// interleave (chunk kk of q1, q0, q2, q0, q1, q0), so the fp32 accumulators sum p1 q1 + p2 q0 +
+// p0 q2 + p1 q0 + p0 q1 + p0 q0 chunk by chunk — the six cross products above 2^-24 (the three
+// dropped are < 2^-32).
 constexpr int kRowsSplit3 = 101;
 constexpr int kSplitPlanes = 0x001021;  // nibble t = plane of K-block t
 
@@ -989,10 +990,11 @@ __global__ void __launch_bounds__(512) gemm_ppp_kernel(const GemmP p, int total)
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds16(s.ab + s.aoff[hh][i] + k0, dst + PE * i);
     } else if constexpr (AMODE == kRowsSplit3) {
-      // K-tile kt of the virtual 6 K0: block t = kt / ktb (compares: kt is wave-uniform), its plane
-      const int ktb = p.K / (6 * BK);
-      const int t = (kt >= ktb) + (kt >= 2 * ktb) + (kt >= 3 * ktb) + (kt >= 4 * ktb) + (kt >= 5 * ktb);
-      const TC* src = s.ab + ((kSplitPlanes >> (4 * t)) & 15) * p.spl + (kt - t * ktb) * BK;
+      // K-tile kt of the virtual 6 K0 = term t = kt % 6 of the 64-column chunk kk = kt / 6: the six
+      // terms of a chunk run back to back, so its A planes are re-read from L2 within six K-tiles
+      // (term-major order re-fetched them from HBM: 3.8-5x the algorithmic A bytes)
+      const int kk = kt / 6, t = kt - 6 * kk;
+      const TC* src = s.ab + ((kSplitPlanes >> (4 * t)) & 15) * p.spl + kk * BK;
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds16(src + s.aoff[hh][i], dst + PE * i);
     } else {

@@ -314,15 +314,20 @@ def layernorm_split3(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: flo
 
 
 def split3_weight(w: torch.Tensor) -> torch.Tensor:
-    """An fp32 weight [N][K0] as the SPLIT3 GEMM's W operand: its bf16 planes q0 + q1 + q2 (8 + 8 + 8
-    mantissa bits) concatenated along K as q1 | q0 | q2 | q0 | q1 | q0 -> [N][6 K0] bf16 (one-time
-    weight preparation, cached with the module's other prepared weights)."""
+    """An fp32 weight [N][K0] (K0 % 64 == 0) as the SPLIT3 GEMM's W operand: its bf16 planes q0 + q1 +
+    q2 (8 + 8 + 8 mantissa bits) interleaved per 64-column chunk kk as q1 | q0 | q2 | q0 | q1 | q0
+    -> [N][6 K0] bf16, the GEMM's K-tile 6 kk + t (one-time weight preparation, cached with the
+    module's other prepared weights)."""
     w = w.float()
+    N, K0 = w.shape
+    if K0 % 64:
+        raise ValueError("split3_weight: K0 must be a multiple of 64")
     q0 = w.bfloat16()
     r = w - q0.float()
     q1 = r.bfloat16()
     q2 = (r - q1.float()).bfloat16()
-    return torch.cat([q1, q0, q2, q0, q1, q0], dim=1).contiguous()
+    terms = torch.stack([t.view(N, K0 // 64, 64) for t in (q1, q0, q2, q0, q1, q0)], dim=2)
+    return terms.reshape(N, 6 * K0).contiguous()
 
 
 def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
