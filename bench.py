@@ -20,9 +20,11 @@ Multi-GPU: inference replicas: the ViT's batch-axis attention c
 images of one forward call, so a call's batch is never split; each rank runs its own batch,
 no collective on the data path (barrier + max-over-ranks timing only) -> scaling "weak".
 
-Roofline: the dominant kernel is the fused MHAda attention (mhada_attn, 6 launches/step);
-its algorithmic FLOPs per launch = 6*Nc*Ns*C*B (QK^T, PV, PV^2; 2 FLOP/MAC), timed live with
-HIP events on its launch stream over the timed region.  After every timed region the same process
+Roofline: the dominant kernel is the fused MHAda attention (6 launches/step); its algorithmic FLOPs
+per launch = 6*Nc*Ns*C*B (QK^T, PV, PV^2; 2 FLOP/MAC), timed live with HIP events on its launch
+stream over the timed region.  The fp32 headline's attention (mhada_attn_split3) runs fp32-accurate
+SPLIT3 products on the bf16 MFMA, so its line prices the bf16 MFMA FLOPs it issues (6.25x the
+algorithmic fp32 FLOPs) against the bf16 peak and states the fp32-equivalent rate beside them.  After every timed region the same process
 runs a shader-clock probe (csrc/probe.hip) and reports the box's clock under dense MFMA load
 ("clock_ghz"; "frac_at_clock" = the fraction of the peak scaled to that clock).  CPU baseline (rank 0, N=1): the
 reference's aten fp32 expression (tests/torch_ref.py, golden-pinned) at B=1 on the job's host
@@ -83,8 +85,13 @@ def flops_per_frame(res: int, style_res: int) -> dict:
     return {"total": vit(nc) + vit(ns) + mhada + dec, "attn_per_block": 6 * nc * ns * C}
 
 
-ATTN_SOURCES = ("mhada-style-transfer_amd/csrc/attn.hip", "mhada-style-transfer_amd/csrc/attn_common.h",
-                "mhada-style-transfer_amd/csrc/common.h")
+ATTN_SOURCES = ("mhada-style-transfer_amd/csrc/attn.hip", "mhada-style-transfer_amd/csrc/attn_split3.hip",
+                "mhada-style-transfer_amd/csrc/attn_common.h", "mhada-style-transfer_amd/csrc/common.h")
+
+# The fp32 softmax attention runs as SPLIT3 products on the bf16 MFMA (csrc/attn_split3.hip, round 6):
+# per (query, key, head) 6 x 128 (Q K^T) + 6 x 256 (P [V' | V'^2]) + 3 x 32 (row sum, all-ones A)
+# bf16 MFMA FLOP for the 384 algorithmic fp32 FLOP
+SPLIT3_MFMA_PER_FP32 = (6 * 128 + 6 * 256 + 3 * 32) / 384
 
 
 def attn_source_sha() -> str:
@@ -193,20 +200,35 @@ def run_config(res, batch, dtype, steps, warmup, rank, world):
     fl = flops_per_frame(res, res)
     avg_attn_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
     attn_flops = fl["attn_per_block"] * batch
-    achieved = attn_flops / avg_attn_s / 1e12
     traffic, tsrc = pmc_traffic(f"{res}x{res}_b{batch}_{dts}")
+    from mhada_hip import ops
+    split3 = dtype == torch.float32 and ops.F32_SPLIT_ATTN
+    if split3:
+        # priced against the pipe it runs on: bf16 MFMA FLOP / 2.5 PF; the fp32-equivalent rate
+        # (algorithmic fp32 FLOP / time, against the fp32 MFMA peak) is stated beside it
+        mfma_flops = attn_flops * SPLIT3_MFMA_PER_FP32
+        achieved, peak = mfma_flops / avg_attn_s / 1e12, PEAK_TFLOPS["bf16"]
+    else:
+        mfma_flops = attn_flops
+        achieved, peak = attn_flops / avg_attn_s / 1e12, PEAK_TFLOPS[dts]
+    roof = {"bound": "mfma", "kernel": "mhada_attn_split3" if split3 else "mhada_attn", "achieved": round(achieved, 2),
+            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
+            "avg_launch_ms": round(avg_attn_s * 1e3, 4),
+            "flop_per_launch": mfma_flops, "launches_timed": len(attn_ms),
+            "clock_ghz": clock, "frac_at_clock": round(achieved / (peak * clock / PEAK_CLOCK_GHZ), 4)}
+    if split3:
+        roof["pipe"] = "bf16 MFMA (fp32-accurate SPLIT3 products: 3 bf16 planes per fp32 operand, 6 cross products)"
+        roof["algorithmic_fp32_flop_per_launch"] = attn_flops
+        roof["fp32_equiv_tflops"] = round(attn_flops / avg_attn_s / 1e12, 2)
+        roof["fp32_equiv_frac_of_fp32_peak"] = round(attn_flops / avg_attn_s / 1e12 / PEAK_TFLOPS["f32"], 4)
     return {
         "value": frames / elapsed,
         "ms_per_step": elapsed / steps * 1e3,
         "dtype": dts,
         "frames_per_s_per_gpu": frames / elapsed / world,
         "tflops_whole_step": fl["total"] * batch * steps / (elapsed) / 1e12,
-        "roofline": {"bound": "mfma", "kernel": "mhada_attn", "achieved": round(achieved, 2),
-                     "peak": PEAK_TFLOPS[dts], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dts], 4),
-                     "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
-                     "avg_launch_ms": round(avg_attn_s * 1e3, 4),
-                     "flop_per_launch": attn_flops, "launches_timed": len(attn_ms),
-                     "clock_ghz": clock, "frac_at_clock": round(achieved / (PEAK_TFLOPS[dts] * clock / PEAK_CLOCK_GHZ), 4)},
+        "roofline": roof,
         "clock_ghz": clock,
         "config": {"workload": f"stylize {res}x{res} content+style, batch {batch}", "resolution": res,
                    "batch_per_gpu": batch, "global_batch": batch * world, "compute_dtype": dts,
@@ -631,7 +653,8 @@ def main():
                                       "clock_ghz")}
         if probes:
             line.setdefault("configs", {}).update(probes)
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
+            # rank 0 only, after every timed region (the other ranks wait at the final barrier)
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
     if world > 1:

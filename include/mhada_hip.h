@@ -51,7 +51,7 @@ enum {
  * p0 = bf16(y), p1 = bf16(y - p0), p2 = bf16(y - p0 - p1) of the fp32 result y (ABI 15) */
 enum { MHADA_BF16X3 = 2 };
 
-int mhada_abi_version(void);  /* 15 (mhada_gemm a_mode MHADA_A_SPLIT3, mhada_layernorm y_dtype MHADA_BF16X3; 14: mhada_cosine_moments / mhada_cosine_attn, mhada_warp_bwd; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
+int mhada_abi_version(void);  /* 16 (mhada_split3_kv / mhada_attn_split3; 15: mhada_gemm a_mode MHADA_A_SPLIT3, mhada_layernorm y_dtype MHADA_BF16X3; 14: mhada_cosine_moments / mhada_cosine_attn, mhada_warp_bwd; 13: mhada_clock_probe; tuning knobs of removed kernel variants dropped, attn_waves 0 = auto; 12: mhada_feat_stats; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints mhada_vgg_stem_dgrad / mhada_out3_dgrad / mhada_out3_wgrad; 8: mhada_feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed training adjoints; 5: Winograd conv; 4: training CONV3X3_ZERO, mhada_gemm_tn, backward helpers) */
 const char* mhada_last_error(void);
 
 /* Kernel-variant table.  Defaults are the measured winners; the other variants serve A/B
@@ -62,7 +62,7 @@ const char* mhada_last_error(void);
  * 8-wave grid has fewer blocks than CUs), attn_tk (64|128), attn_prio (0|1), vit_attn_vec (0|1),
  * out3_mfma (0|1), out3_tile (0|1), gemm_pp (0|1), gemm_persist (0|1), gemm_pp128 (0|1),
  * gemm_ldsepi (0|1), gemm_n64 (128|256), conv_c64 (0|1), conv_dir (0|1), gemm_rinit (0|1), tn_skinny_lds (0|1),
- * train_dkv_dma (0|1), wino4 (0|1), xknob (0..15, read by no shipped dispatch).
+ * train_dkv_dma (0|1), wino4 (0|1), upsample_quad (0|1; ABI 16), xknob (0..15, read by no shipped dispatch).
  * Returns MHADA_ERR_ARG for an unknown knob or an out-of-range value.  No reference
  * counterpart (the reference has no kernels). */
 int mhada_set_tuning(const char* name, int value);
@@ -192,6 +192,22 @@ int mhada_cosine_prep(void* q, void* kv, int dtype, int B, int H, int Nc, int Ns
 int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
                const float* fcs_mu, const float* fcs_rstd, const float* v_mu, void* out,
                int dtype, int B, int H, int Nc, int Ns, int activation, mhada_stream_t stream);
+
+/* The fp32 softmax MHAda attention (adaDecoder.py:186-198, mhada_attn's contract and output) as
+ * fp32-accurate SPLIT3 products on the bf16 MFMA (ABI 16; csrc/attn_split3.hip): every fp32 operand as
+ * three bf16 planes x = x0 + x1 + x2 (round to nearest: x0 = bf16(x), x1 = bf16(x - x0),
+ * x2 = bf16(x - x0 - x1)) and every product as the six cross products x_i y_j, i + j <= 2, summed in
+ * fp32 accumulators (dropped terms < 2^-24 |x y|).  Replaces mhada_attn(dtype MHADA_F32, softmax).
+ * mhada_split3_kv: the style-side operands kv fp32 [B][H][Ns][128] (K | V', only K read) and the fp32
+ *   vt image [B][H][128][ldt] (mhada_transpose_v, ldt = ceil64(Ns)) -> img bf16 [B][H][576 ldt]:
+ *   K planes [3][ldt][64] (rows >= Ns zero) | V'^T|V'^2^T planes [3][128][ldt] (key positions permuted
+ *   in groups of 16 as the bf16 vt image).  Once per style (cacheable like kv / vt); B * H <= 65535.
+ * mhada_attn_split3: q fp32 [B][H][Nc][64] (split on load) and img -> out fp32 [B][Nc][64H]; the other
+ *   arguments as mhada_attn. */
+int mhada_split3_kv(const float* kv, const float* vt, void* img, int B, int H, int Ns, mhada_stream_t stream);
+int mhada_attn_split3(const float* q, const void* img, const float* fcs, const float* fcs_mu,
+                      const float* fcs_rstd, const float* v_mu, float* out, int B, int H, int Nc, int Ns,
+                      mhada_stream_t stream);
 
 /* The cosine activation (CosineSimilarity, adaDecoder.py:20-34) in its linear form (ABI 14):
  * A[i][j] = (q^_i.k^_j + 1) / l_i with l_i = q^_i.sum_j k^_j + Ns, so A V' and A V'^2 need only the

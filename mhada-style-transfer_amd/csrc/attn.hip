@@ -667,14 +667,6 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_bf16_fs_kernel(const AttnP p)
 }
 
 // --------------------------------------------------------------------------------------
-// LDS-DMA (global_load_lds, 16 B per lane) for the fixed-shift kernel's K / V'^T ring below.
-// --------------------------------------------------------------------------------------
-MHADA_DEV void attn_glds16(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-}
-
-// --------------------------------------------------------------------------------------
 // Fixed-shift LDS-DMA kernel on v_mfma_f32_16x16x32_bf16 ("fsq1", the bf16 softmax default when
 // Ns % 128 == 0): the fixed shift of attn_bf16_fs_kernel with the K / V'^T tiles staged by
 // global_load_lds into a 2-slot ring (no staging registers, no LDS write pass, the next tile's DMA
@@ -703,7 +695,6 @@ MHADA_DEV void attn_glds16(const void* src, void* lds) {
 // +8 MFMAs (72 instead of 64 PV MFMAs per tile and wave); l is then the sum of the bf16-rounded P
 // that the PV products use.
 // --------------------------------------------------------------------------------------
-MHADA_DEV int fsq_key(int r, int t) { return 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3) + 8 * t; }
 
 // Exact two-pass recompute of one wave's 2 x 16 queries (16x16x32 layout; the rare path when a row
 // sum trips kShiftSumThr): true row max over all keys, then the full pass, operands from L2.
@@ -767,46 +758,6 @@ MHADA_DEV void attn_exact_q(const AttnP& p, const bf16* kvb, const bf16* vtb, co
   for (int qg = 0; qg < 2; ++qg) {
     lt[qg] += __shfl_xor(lt[qg], 16, 64);
     lt[qg] += __shfl_xor(lt[qg], 32, 64);
-  }
-}
-
-// Epilogue of the 16x16x32 layout: O[qg][dvb] holds O^T[dv][q] for q = q0 + 16 qg + r16,
-// dv = 16 dvb + 4g + e (dvb 0-3: sum p v', 4-7: sum p v'^2); lt = the full row sums.
-template <typename T>
-MHADA_DEV void attn_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], const float (&lt)[2], int b, int hh, int q0,
-                               int g, int r16) {
-  const int C = p.H * 64;
-#pragma unroll
-  for (int qg = 0; qg < 2; ++qg) {
-    const int q = q0 + 16 * qg + r16;
-    if (q >= p.Nc) continue;
-    const float inv = 1.0f / lt[qg];
-    const float* fr = p.fcs + ((long long)b * p.Nc + q) * C + hh * 64;
-    const float* mu = p.fcs_mu + (long long)b * C + hh * 64;
-    const float* rs = p.fcs_rstd + (long long)b * C + hh * 64;
-    const float* vm = p.v_mu + (long long)b * C + hh * 64;
-    T* orow = reinterpret_cast<T*>(p.out) + ((long long)b * p.Nc + q) * C + hh * 64;
-#pragma unroll
-    for (int dvb = 0; dvb < 4; ++dvb) {
-      const int dv0 = 16 * dvb + 4 * g;
-      const f32x4 f = *reinterpret_cast<const f32x4*>(fr + dv0);
-      const f32x4 m4 = *reinterpret_cast<const f32x4*>(mu + dv0);
-      const f32x4 r4 = *reinterpret_cast<const f32x4*>(rs + dv0);
-      const f32x4 v4 = *reinterpret_cast<const f32x4*>(vm + dv0);
-      float res[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float m1 = O[qg][dvb][e] * inv;
-        const float e2 = O[qg][dvb + 4][e] * inv;
-        const float sd = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f));
-        res[e] = sd * ((f[e] - m4[e]) * r4[e]) + (m1 + v4[e]);
-      }
-      if constexpr (sizeof(T) == 4) {
-        *reinterpret_cast<f32x4*>(orow + dv0) = f32x4{res[0], res[1], res[2], res[3]};
-      } else {
-        *reinterpret_cast<bf16x4*>(orow + dv0) = bf16x4{(bf16)res[0], (bf16)res[1], (bf16)res[2], (bf16)res[3]};
-      }
-    }
   }
 }
 

@@ -130,4 +130,57 @@ MHADA_DEV void attn_exact_half(const AttnP& p, const bf16* kvb, const bf16* vtb,
   }
 }
 
+
+// --------------------------------------------------------------------------------------
+// LDS-DMA (global_load_lds, 16 B per lane) for the K / V'^T rings of the LDS-DMA kernels.
+// --------------------------------------------------------------------------------------
+MHADA_DEV void attn_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// Key of score row r (0..15) of tile t (0, 1) in a 32-key group of the 16x16x32 attention layout
+// (attn_bf16_fsq_kernel, attn_s3_kernel): lane group g then holds the 8 keys its PV B slots need.
+MHADA_DEV int fsq_key(int r, int t) { return 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3) + 8 * t; }
+
+// Epilogue of the 16x16x32 layout: O[qg][dvb] holds O^T[dv][q] for q = q0 + 16 qg + r16,
+// dv = 16 dvb + 4g + e (dvb 0-3: sum p v', 4-7: sum p v'^2); lt = the full row sums.
+template <typename T>
+MHADA_DEV void attn_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], const float (&lt)[2], int b, int hh, int q0,
+                               int g, int r16) {
+  const int C = p.H * 64;
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q0 + 16 * qg + r16;
+    if (q >= p.Nc) continue;
+    const float inv = 1.0f / lt[qg];
+    const float* fr = p.fcs + ((long long)b * p.Nc + q) * C + hh * 64;
+    const float* mu = p.fcs_mu + (long long)b * C + hh * 64;
+    const float* rs = p.fcs_rstd + (long long)b * C + hh * 64;
+    const float* vm = p.v_mu + (long long)b * C + hh * 64;
+    T* orow = reinterpret_cast<T*>(p.out) + ((long long)b * p.Nc + q) * C + hh * 64;
+#pragma unroll
+    for (int dvb = 0; dvb < 4; ++dvb) {
+      const int dv0 = 16 * dvb + 4 * g;
+      const f32x4 f = *reinterpret_cast<const f32x4*>(fr + dv0);
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(mu + dv0);
+      const f32x4 r4 = *reinterpret_cast<const f32x4*>(rs + dv0);
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(vm + dv0);
+      float res[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[qg][dvb][e] * inv;
+        const float e2 = O[qg][dvb + 4][e] * inv;
+        const float sd = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f));
+        res[e] = sd * ((f[e] - m4[e]) * r4[e]) + (m1 + v4[e]);
+      }
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(orow + dv0) = f32x4{res[0], res[1], res[2], res[3]};
+      } else {
+        *reinterpret_cast<bf16x4*>(orow + dv0) = bf16x4{(bf16)res[0], (bf16)res[1], (bf16)res[2], (bf16)res[3]};
+      }
+    }
+  }
+}
+
 }  // namespace mhada

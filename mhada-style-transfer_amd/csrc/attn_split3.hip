@@ -1,0 +1,417 @@
+// fp32 MHAda attention as fp32-accurate SPLIT3 products on the bf16 MFMA (round 6).
+//
+// Reference: AdaAttnMultiHead.forward, adaDecoder.py:186-198 (A = softmax(Q K^T), M = A V,
+// E2 = A V^2, out = sqrt(max(E2 - M^2, 1e-6)) * IN(fcs) + M), the fp32 arithmetic of the reference
+// (BASELINE configs[1]).  attn_f32_kernel (attn.hip) computes it on v_mfma_f32_32x32x2_f32 and sits at
+// that pipe's ceiling (0.83-0.87 of 157.3 TF/s, HBM traffic 1.02x the algorithmic bytes); the bf16
+// pipe has 16x the MACs per cycle.  Here every fp32 operand x travels as three bf16 planes
+// x = x0 + x1 + x2 (round-to-nearest split: x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1);
+// exact for normal fp32 values, |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|), and each fp32 product
+// x * y is the sum of the six cross products x_i y_j with i + j <= 2, accumulated in fp32 by
+// v_mfma_f32_16x16x32_bf16; the three dropped terms are below 2^-24 |x y| (x1 y2, x2 y1) and 2^-32
+// (x2 y2).  Both products of the loop are split this way:
+//   S = Q K^T       Q split in registers on load, K from the pre-split K planes;
+//   O = P [V' | V'^2]   P = exp2(S - m) computed in fp32 and split in registers after the exp,
+//                   V'^T | V'^2^T from the pre-split planes of the fp32 vt image;
+//   l = sum P       three all-ones MFMAs per 32 keys (one per P plane) — the exact sum of the planes.
+// Against fp64 the result is at or below attn_f32_kernel's error (tests/test_gpu_kernels.py).
+//
+// Structure: attn_bf16_fsq_kernel's (attn.hip) — swapped products with the query on the MFMA column,
+// two 16-query groups per wave sharing every K / V'^T fragment, the fsq_key score-row choice that
+// leaves each lane group holding exactly its PV B-operand keys, fixed-shift softmax (the shift is the
+// max of each query's first key tile; the accumulators start at -m; a row whose later scores outgrow
+// it by 2^64 is recomputed exactly after the loop, attn_exact_q3) — with 64-key tiles: one ring slot
+// holds the three K planes (3 x 8 KiB) and the three V'^T | V'^2^T planes (3 x 16 KiB), two slots
+// = 144 KiB of LDS, filled by LDS-DMA.  Per tile and wave: 96 QK + 192 PV + 12 row-sum MFMAs for
+// 64 keys x 32 queries, 24 + 48 ds_read_b128, and 32 v_exp_f32 plus ~4.5 VALU per score for the
+// split of P.
+//
+// LDS images (per 128-B row of 64 bf16): K planes [3][64 keys][64 d], chunk c of key row k at 16-B
+// slot c ^ (k & 7) (attn_bf16_fsq_kernel's K swizzle); V'^T planes [3][128 rows][64 key positions],
+// chunk c of row r at slot c ^ ((r >> 1) & 7) — conflict-free for the ds_read_b128 lane groups of
+// MI355X_MICROARCH.md's LDS table (rows 16 dvb + r16, chunk 4 kg + g: the 16 lanes of a group cover
+// every (row parity, slot) pair once).
+//
+// Plane image in HBM (mhada_split3_kv), per (b, h), ldt = ceil64(Ns):
+//   K planes  [3][ldt][64]   rows >= Ns zero;
+//   V planes  [3][128][ldt]  V'^T (rows 0..63) | V'^2^T (64..127), key positions permuted inside
+//             groups of 16 (bits 2 and 3 swapped, the bf16 vt image's order), zero padded.
+#include "attn_common.h"
+
+namespace mhada {
+
+constexpr int kS3Tk = 64;  // keys per tile
+
+// bf16 elements of one (b, h)'s plane image: K 3 * 64 * ldt, V 3 * 128 * ldt
+__host__ __device__ constexpr long long s3_image(int ldt) { return 576LL * ldt; }
+
+// Round-to-nearest three-way split (the split of mhada_layernorm BF16X3 and ops.split3_weight).
+struct Bf3 { bf16 a, b, c; };
+MHADA_DEV Bf3 split3(float x) {
+  const bf16 a = (bf16)x;
+  const float r = x - (float)a;
+  const bf16 b = (bf16)r;
+  return Bf3{a, b, (bf16)(r - (float)b)};
+}
+template <typename V>
+MHADA_DEV void split3_into(float x, V& a, V& b, V& c, int e) {
+  const Bf3 s = split3(x);
+  a[e] = s.a;
+  b[e] = s.b;
+  c[e] = s.c;
+}
+
+// kv fp32 [BH][Ns][128] (K in columns 0..63; V' is read from vt) and the fp32 vt image [BH][128][ldt]
+// (natural key order, zero padded) -> the plane image.  One workgroup per (64-key chunk, b h).
+__global__ void __launch_bounds__(256) split3_kv_kernel(const float* __restrict__ kv, const float* __restrict__ vt,
+                                                        bf16* __restrict__ img, int Ns, int ldt) {
+  const int bh = blockIdx.y, n0 = blockIdx.x * 64, tid = threadIdx.x;
+  bf16* kp = img + (long long)bh * s3_image(ldt);
+  bf16* vp = kp + 192LL * ldt;
+  const float* kvb = kv + (long long)bh * Ns * 128;
+  const float* vtb = vt + (long long)bh * 128 * ldt;
+  const long long kps = 64LL * ldt, vps = 128LL * ldt;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // K: 64 keys x 16 groups of 4 d
+    const int idx = tid + 256 * i, key = n0 + (idx >> 4), d = (idx & 15) * 4;
+    const f32x4 x = key < Ns ? *reinterpret_cast<const f32x4*>(kvb + (long long)key * 128 + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x4 a, b, c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_into(x[e], a, b, c, e);
+    bf16* dst = kp + (long long)key * 64 + d;
+    *reinterpret_cast<bf16x4*>(dst) = a;
+    *reinterpret_cast<bf16x4*>(dst + kps) = b;
+    *reinterpret_cast<bf16x4*>(dst + 2 * kps) = c;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // V'^T | V'^2^T: 128 rows x 8 runs of 8 key positions
+    const int idx = tid + 256 * i, row = idx >> 3, a8 = idx & 7;
+    // positions 8 a8 + j hold keys 16 (a8 >> 1) + 8 (j >> 2) + 4 (a8 & 1) + (j & 3)
+    const float* src = vtb + (long long)row * ldt + n0 + 16 * (a8 >> 1) + 4 * (a8 & 1);
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 8);
+    bf16x8 a, b, c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_into(j < 4 ? lo[j] : hi[j - 4], a, b, c, j);
+    bf16* dst = vp + (long long)row * ldt + n0 + 8 * a8;
+    *reinterpret_cast<bf16x8*>(dst) = a;
+    *reinterpret_cast<bf16x8*>(dst + vps) = b;
+    *reinterpret_cast<bf16x8*>(dst + 2 * vps) = c;
+  }
+}
+
+// x_i y_j, i + j <= 2, small terms first: acc + x2y0 + x1y1 + x0y2 + x1y0 + x0y1 + x0y0 (A = x, B = y)
+MHADA_DEV f32x4 mfma6(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0, const bf16x8& b1,
+                      const bf16x8& b2, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+}
+
+// Exact two-pass recompute of one wave's 2 x 16 queries (the rare path when a row sum trips
+// kShiftSumThr): the true row max over all keys, then the full pass, planes read from L2.
+MHADA_DEV void attn_exact_q3(const AttnP& p, const bf16* kp, const bf16* vp, const bf16x8 (&qf)[3][2][2],
+                             f32x4 (&O)[2][8], float (&lt)[2], int g, int r16) {
+  const int Ns = p.Ns;
+  const long long kps = 64LL * p.ldt, vps = 128LL * p.ldt;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto scores = [&](int k0, f32x4 (&S)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16* kr = kp + (long long)(k0 + fsq_key(r16, t)) * 64 + 8 * g;  // k0 + 31 < ldt
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) S[qg][t] = z4;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const bf16x8 k0f = *reinterpret_cast<const bf16x8*>(kr + 32 * dh);
+        const bf16x8 k1f = *reinterpret_cast<const bf16x8*>(kr + kps + 32 * dh);
+        const bf16x8 k2f = *reinterpret_cast<const bf16x8*>(kr + 2 * kps + 32 * dh);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg)
+          S[qg][t] = mfma6(k0f, k1f, k2f, qf[0][qg][dh], qf[1][qg][dh], qf[2][qg][dh], S[qg][t]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k0 + fsq_key(4 * g + j, t) >= Ns) S[0][t][j] = S[1][t][j] = -INFINITY;
+    }
+  };
+  float m2[2] = {-INFINITY, -INFINITY};
+  for (int k0 = 0; k0 < Ns; k0 += 32) {
+    f32x4 S[2][2];
+    scores(k0, S);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m2[qg] = fmaxf(m2[qg], S[qg][t][j]);
+  }
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    m2[qg] = fmaxf(m2[qg], __shfl_xor(m2[qg], 16, 64));
+    m2[qg] = fmaxf(m2[qg], __shfl_xor(m2[qg], 32, 64));
+    lt[qg] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) O[qg][i] = z4;
+  }
+  for (int k0 = 0; k0 < Ns; k0 += 32) {
+    f32x4 S[2][2];
+    scores(k0, S);
+    bf16x8 pf[3][2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = fast_exp2(S[qg][j >> 2][j & 3] - m2[qg]);
+        lt[qg] += e;
+        split3_into(e, pf[0][qg], pf[1][qg], pf[2][qg], j);
+      }
+#pragma unroll
+    for (int dvb = 0; dvb < 8; ++dvb) {
+      const bf16* vr = vp + (long long)(16 * dvb + r16) * p.ldt + k0 + 8 * g;
+      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vr);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vr + vps);
+      const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vr + 2 * vps);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) O[qg][dvb] += mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], z4);
+    }
+  }
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    lt[qg] += __shfl_xor(lt[qg], 16, 64);
+    lt[qg] += __shfl_xor(lt[qg], 32, 64);
+  }
+}
+
+// Scores of keys >= Ns (the ragged last tile): -inf.  S[qg][kg][t][j] is key key0 + 32 kg + fsq_key(4 g + j, t).
+MHADA_DEV void s3_mask(f32x4 (&S)[2][2][2], int key0, int Ns, int g) {
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (key0 + 32 * kg + fsq_key(4 * g + j, t) >= Ns) S[0][kg][t][j] = S[1][kg][t][j] = -INFINITY;
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
+  constexpr int TK = kS3Tk;
+  constexpr int KPL = TK * 64, VPL = 128 * TK, SLOT = 3 * (KPL + VPL);  // bf16 elements
+  constexpr int KPC = 3 * KPL / 512, VPC = 3 * VPL / 512;                // 1-KiB DMA pieces per slot: 24 + 48
+  static_assert(KPC % NW == 0 && VPC % NW == 0, "tile config");
+  constexpr int KPW = KPC / NW, VPW = VPC / NW;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * SLOT];  // 144 KiB
+  int b, hh, qb;
+  decode_block(p, b, hh, qb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q0 = qb * (32 * NW) + wave * 32;
+  const long long bh = (long long)b * p.H + hh;
+  const int Ns = p.Ns, ldt = p.ldt;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 qf[3][2][2];  // Q^T planes: query q0 + 16 qg + r16, d = 32 dh + 8 g .. + 8
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q0 + 16 * qg + r16;
+    const float* qp = reinterpret_cast<const float*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * g;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(qp + 32 * dh);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(qp + 32 * dh + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = q < p.Nc ? (e < 4 ? lo[e] : hi[e - 4]) : 0.f;
+        split3_into(x, qf[0][qg][dh], qf[1][qg][dh], qf[2][qg][dh], e);
+      }
+    }
+  }
+  const bf16* kp = reinterpret_cast<const bf16*>(p.kv) + bh * s3_image(ldt);
+  const bf16* vp = kp + 192LL * ldt;
+  // per-lane DMA sources: piece NW i + wave; K pieces hold 8 key rows of one plane, V pieces 8 rows
+  int ksrc[KPW], vsrc[VPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int pc = NW * i + wave, pl = pc >> 3, row = 8 * (pc & 7) + (lane >> 3), slot = lane & 7;
+    ksrc[i] = pl * 64 * ldt + row * 64 + 8 * (slot ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int pc = NW * i + wave, pl = pc >> 4, row = 8 * (pc & 15) + (lane >> 3), slot = lane & 7;
+    vsrc[i] = pl * 128 * ldt + row * ldt + 8 * (slot ^ ((row >> 1) & 7));
+  }
+  auto stage = [&](int key0, int sl) {
+    bf16* kd = smem + sl * SLOT;
+    bf16* vd = kd + 3 * KPL;
+    const bf16* ks = kp + (long long)key0 * 64;
+    const bf16* vs = vp + key0;
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (NW * i + wave));
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) attn_glds16(vs + vsrc[i], vd + 512 * (NW * i + wave));
+  };
+  int krow[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) krow[t] = fsq_key(r16, t) * 64;
+  auto qk = [&](int sl, f32x4 (&S)[2][2][2], const f32x4 (&init)[2]) {
+    const bf16* ck = smem + sl * SLOT;
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16* kr = ck + kg * 32 * 64 + krow[t];
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const int off = 8 * ((4 * dh + g) ^ (r16 & 7));  // key & 7 == r16 & 7
+          const bf16x8 k0f = *reinterpret_cast<const bf16x8*>(kr + off);
+          const bf16x8 k1f = *reinterpret_cast<const bf16x8*>(kr + KPL + off);
+          const bf16x8 k2f = *reinterpret_cast<const bf16x8*>(kr + 2 * KPL + off);
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg)
+            S[qg][kg][t] = mfma6(k0f, k1f, k2f, qf[0][qg][dh], qf[1][qg][dh], qf[2][qg][dh],
+                                 dh == 0 ? init[qg] : S[qg][kg][t]);
+        }
+      }
+  };
+  f32x4 O[2][8], L[2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    L[qg] = z4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) O[qg][i] = z4;
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  auto finish = [&](int sl, const f32x4 (&S)[2][2][2]) {
+    const bf16* cv = smem + sl * SLOT + 3 * KPL;
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      bf16x8 pf[3][2];
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3_into(fast_exp2(S[qg][kg][j >> 2][j & 3]), pf[0][qg], pf[1][qg], pf[2][qg], j);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[2][qg], L[qg], 0, 0, 0);
+        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][qg], L[qg], 0, 0, 0);
+        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][qg], L[qg], 0, 0, 0);
+      }
+      const int off = 8 * ((4 * kg + g) ^ ((r16 >> 1) & 7));  // row 16 dvb + r16
+#pragma unroll
+      for (int dvb = 0; dvb < 8; ++dvb) {
+        const bf16* vr = cv + (16 * dvb + r16) * TK + off;
+        const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vr);
+        const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vr + VPL);
+        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vr + 2 * VPL);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], O[qg][dvb]);
+      }
+    }
+  };
+
+  const int NTILE = (Ns + TK - 1) / TK, NFULL = Ns / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 Sa[2][2][2], Cm[2];
+  {  // tile 0: unshifted scores, m2 = their max, then shift
+    const f32x4 zi[2] = {z4, z4};
+    qk(0, Sa, zi);
+    if (NFULL == 0) s3_mask(Sa, 0, Ns, g);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m = fmaxf(m, Sa[qg][kg][t][j]);
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Sa[qg][kg][t][j] -= m;
+      Cm[qg] = f32x4{-m, -m, -m, -m};
+    }
+  }
+  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (NTILE > 1) stage(TK, 1);
+  finish(0, Sa);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 1; t < NFULL; ++t) {
+    if (t + 1 < NTILE) stage((t + 1) * TK, (t + 1) & 1);
+    qk(t & 1, Sa, Cm);
+    finish(t & 1, Sa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if (NFULL < NTILE && NFULL > 0) {  // ragged last tile (its DMA was issued by the previous iteration)
+    qk(NFULL & 1, Sa, Cm);
+    s3_mask(Sa, NFULL * TK, Ns, g);
+    finish(NFULL & 1, Sa);
+  }
+  float lt[2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
+  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3(p, kp, vp, qf, O, lt, g, r16);
+  attn_epilogue_q<float>(p, O, lt, b, hh, q0, g, r16);
+}
+
+static int s3_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+}  // namespace mhada
+
+using namespace mhada;
+
+extern "C" int mhada_split3_kv(const float* kv, const float* vt, void* img, int B, int H, int Ns, mhada_stream_t s_) {
+  if (!kv || !vt || !img || B <= 0 || H <= 0 || Ns <= 0) return fail("mhada_split3_kv: bad args");
+  const long long bhn = (long long)B * H;
+  if (bhn > 65535) return fail("mhada_split3_kv: B * H > 65535");
+  const int ldt = (Ns + 63) / 64 * 64;
+  hipLaunchKernelGGL(split3_kv_kernel, dim3(ldt / 64, (unsigned)bhn), dim3(256), 0, (hipStream_t)s_, kv, vt,
+                     reinterpret_cast<bf16*>(img), Ns, ldt);
+  return check_launch("mhada_split3_kv");
+}
+
+extern "C" int mhada_attn_split3(const float* q, const void* img, const float* fcs, const float* fcs_mu,
+                                 const float* fcs_rstd, const float* v_mu, float* out, int B, int H, int Nc, int Ns,
+                                 mhada_stream_t s_) {
+  if (!q || !img || !fcs || !fcs_mu || !fcs_rstd || !v_mu || !out || B <= 0 || H <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_split3: bad args");
+  AttnP p = {};
+  p.q = q; p.kv = img; p.vt = img; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
+  p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
+  p.prio = tuning().attn_prio;
+  p.ldt = (Ns + 63) / 64 * 64;
+  if (384LL * p.ldt >= (1LL << 31)) return fail("mhada_attn_split3: Ns too large for 32-bit plane offsets");
+  // waves per block as mhada_attn: tuning attn_waves, 0 = 8, or 4 when the 8-wave grid has fewer
+  // blocks than CUs
+  int nw = tuning().attn_waves;
+  if (nw == 0) nw = (long long)B * H * ((Nc + 255) / 256) < s3_num_cus() ? 4 : 8;
+  p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
+  const long long nblk = (long long)B * H * p.nqb;
+  if (nblk > (1LL << 31) - 1) return fail("mhada_attn_split3: grid too large");
+  p.nblk = (int)nblk;
+  const hipStream_t s = (hipStream_t)s_;
+  if (nw == 8) hipLaunchKernelGGL(attn_s3_kernel<8>, dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL(attn_s3_kernel<4>, dim3(p.nblk), dim3(256), 0, s, p);
+  return check_launch("mhada_attn_split3");
+}

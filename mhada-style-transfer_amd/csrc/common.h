@@ -46,6 +46,7 @@ struct Tuning {
   int tn_skinny_lds = 1;     // M <= 4 conv weight gradient: LDS-tiled kernel (0: the gather kernel)
   int wino4 = 1;             // fp32 Winograd conv: 4-wave kernel (round 5; 0: the 8-wave kernel, also the fallback for inputs >= 2 GiB)
   int train_dkv_dma = 1;     // training dK/dV' with the dS spill: LDS-DMA kernel, one wave per SIMD, software-pipelined (0: round 3's)
+  int upsample_quad = 1;     // bf16 bilinear x2: 2 x 2-output-block kernel (0: the 16-B per-pixel kernel)
   int xknob = 0;             // scratch knob for one-off A/B builds; no shipped kernel or dispatch reads it
 };
 const Tuning& tuning();

@@ -744,9 +744,10 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ x
 
 // 16-B vector form (round 5) for 16-B aligned tensors: the same thread mapping, coordinates,
 // weights and blend expression as upsample2x_kernel (bit-identical), with each tap's 8 channels
-// read and the output written as whole 16-B vectors.  (A 2 x 2-output-block form that loaded the
-// 3 x 3 source window once measured 1.1-1.6x SLOWER: its window indexing cost more vector
-// instructions than the loads it saved, profiles/r05_prof_bench_per_config.txt.)
+// read and the output written as whole 16-B vectors.  The fp32 path and unaligned views use it;
+// bf16 takes upsample2x_quad_kernel (2 x 2 output blocks, compile-time window indexing), which
+// measured faster (mhada_upsample2x).  An earlier 2 x 2-block form with runtime window indexing
+// measured 1.1-1.6x SLOWER than this kernel (profiles/r05_prof_bench_per_config.txt).
 template <typename T>
 __global__ void __launch_bounds__(256) upsample2x_vec_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
                                                              int W, int C, int gshift) {
@@ -1079,8 +1080,8 @@ extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H,
   if (!x || !y || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return fail("mhada_upsample2x: bad args");
   // bf16: 2 x 2 output blocks (34 / 88 us vs 53 / 105 us for the 16-B per-pixel form at the
   // 1024^2 B4 decoder shapes, profiles/r05_opbench_conv_upsample.log); fp32 (two vectors per
-  // 8-channel group): equal or slower, per-pixel.  tuning xknob = 1 forces the per-pixel form (A/B)
-  if (dtype != MHADA_F32 && aligned16(x) && aligned16(y) && H >= 3 && W >= 3 && tuning().xknob != 1) {
+  // 8-channel group): equal or slower, per-pixel.  tuning upsample_quad = 0 forces the per-pixel form (A/B)
+  if (dtype != MHADA_F32 && aligned16(x) && aligned16(y) && H >= 3 && W >= 3 && tuning().upsample_quad) {
     const long long total = (long long)B * H * W * (C / 8);
     hipLaunchKernelGGL((upsample2x_quad_kernel<bf16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)s_, (const bf16*)x, (bf16*)y, B, H, W, C);

@@ -72,6 +72,8 @@ SIGNATURES = {
     "mhada_cosine_moments": (_I, [_vp, _vp, _I, _I, _I, _I, _vp, _vp, _I, _vp]),
     "mhada_cosine_attn": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_attn": (_I, [_vp] * 8 + [_I, _I, _I, _I, _I, _I, _vp]),
+    "mhada_split3_kv": (_I, [_vp, _vp, _vp, _I, _I, _I, _vp]),
+    "mhada_attn_split3": (_I, [_vp] * 7 + [_I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
     "mhada_transpose64": (_I, [_vp, _vp, _I, _I, _I, _vp]),
@@ -142,7 +144,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 
 def get_tuning(name: str) -> int:

@@ -281,8 +281,10 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
     B, Nc, Cc = fc.t.shape
     cached = bool(side)
     mom = None
+    img = None
     if cached:
         mu_s, rstd_s, kv, vt, mom = side["mu_s"], side["rstd_s"], side["kv"], side["vt"], side.get("mom")
+        img = side.get("img")
         if kv.shape[0] != B:
             raise ValueError(f"cached style batch {kv.shape[0]} != content batch {B}")
     else:
@@ -319,10 +321,19 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
             mom = ops.cosine_moments(kv, vt)
         if side is not None:
             side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt, mom=mom)
+    # fp32 softmax: K and V'^T | V'^2^T as bf16 planes for the SPLIT3 attention (once per style)
+    split_attn = act == ACT_SOFTMAX and dt == torch.float32 and ops.F32_SPLIT_ATTN
+    if split_attn and img is None:
+        img = ops.split3_kv(kv, vt)
+        if side is not None:
+            side["img"] = img
     if act == ACT_COSINE:
         ops.cosine_prep(q, None)
         with _timed("mhada_attn"):
             att = ops.cosine_attn(q, mom, fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] dt
+    elif split_attn:
+        with _timed("mhada_attn"):
+            att = ops.attn_split3(q, img, kv.shape[2], fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] fp32
     else:
         with _timed("mhada_attn"):
             att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt

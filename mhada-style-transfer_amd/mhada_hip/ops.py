@@ -81,8 +81,8 @@ def gemm(*, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, M: int, N: int, K
     for t in (a_mu, bias):
         if t is not None and t.dtype != torch.float32:
             raise ValueError("a_mu / bias must be float32")
-    if r is not None and r.dtype != c.dtype:
-        raise ValueError("residual dtype must equal the output dtype")
+    if r is not None and r.dtype != (c.dtype if c is not None else torch.float32):
+        raise ValueError("residual dtype must equal the output dtype (fp32 for a c2_planes-only output)")
     args = GemmArgs()
     args.M, args.N, args.K = M, N, K
     args.nb1, args.nb2 = nb
@@ -543,6 +543,42 @@ def mhada_attn(q, kv, vt, fcs, fcs_mu, fcs_rstd, v_mu, activation: int) -> torch
     _call("mhada_attn", q, q.data_ptr(), kv.data_ptr(), _ptr(vt), fcs.data_ptr(), fcs_mu.data_ptr(),
                                 fcs_rstd.data_ptr(), v_mu.data_ptr(), out.data_ptr(), dt_code(q.dtype), B, H, Nc,
                                 Ns, activation)
+    return out
+
+
+# The fp32 softmax MHAda attention as SPLIT3 products on the bf16 MFMA (mhada_attn_split3): fp32-accurate
+# (against fp64 at or below the fp32 MFMA kernel's error) and faster.  False: the fp32 MFMA kernel.
+F32_SPLIT_ATTN = True
+
+
+def split3_kv(kv: torch.Tensor, vt: torch.Tensor) -> torch.Tensor:
+    """``mhada_split3_kv``: the fp32 K half of kv [B][H][Ns][128] and the fp32 V'^T | V'^2^T image vt
+    [B][H][128][ceil64(Ns)] as the bf16 plane image [B][H][576 ceil64(Ns)] of ``attn_split3``."""
+    _need_gpu(kv, vt)
+    B, H, Ns, _ = kv.shape
+    ldt = (Ns + 63) // 64 * 64
+    if kv.dtype != torch.float32 or vt.dtype != torch.float32 or vt.shape != (B, H, 128, ldt) \
+            or kv.shape[3] != 128 or not kv.is_contiguous() or not vt.is_contiguous():
+        raise ValueError(f"split3_kv: needs contiguous fp32 kv [B][H][Ns][128] and vt [B][H][128][{ldt}], "
+                         f"got {tuple(kv.shape)} / {tuple(vt.shape)}")
+    img = torch.empty(B, H, 576 * ldt, device=kv.device, dtype=torch.bfloat16)
+    _call("mhada_split3_kv", kv, kv.data_ptr(), vt.data_ptr(), img.data_ptr(), B, H, Ns)
+    return img
+
+
+def attn_split3(q, img, Ns: int, fcs, fcs_mu, fcs_rstd, v_mu) -> torch.Tensor:
+    """``mhada_attn_split3``: mhada_attn's fp32 softmax output from fp32 q [B][H][Nc][64] and the
+    ``split3_kv`` plane image of Ns keys."""
+    _need_gpu(q, img, fcs, fcs_mu, fcs_rstd, v_mu)
+    B, H, Nc, _ = q.shape
+    ldt = (Ns + 63) // 64 * 64
+    if q.dtype != torch.float32 or not q.is_contiguous() or img.dtype != torch.bfloat16 \
+            or img.shape != (B, H, 576 * ldt):
+        raise ValueError(f"attn_split3: q must be contiguous fp32 and img bf16 [B][H][576*{ldt}], got "
+                         f"{q.dtype} / {tuple(img.shape)}")
+    out = torch.empty(B, Nc, H * 64, device=q.device, dtype=torch.float32)
+    _call("mhada_attn_split3", q, q.data_ptr(), img.data_ptr(), fcs.data_ptr(), fcs_mu.data_ptr(),
+          fcs_rstd.data_ptr(), v_mu.data_ptr(), out.data_ptr(), B, H, Nc, Ns)
     return out
 
 

@@ -133,6 +133,15 @@ def test_linear_split3_plane_output_chain(M, N, K0):
     h = torch.relu(y.double() @ w1.double().T + b1.double())
     ref = h @ w2.double().T + b2.double() + r.double()
     assert rel(out, ref) < 2e-6
+    # plane output with a residual and no ReLU (residual + bias preloaded into the accumulators, then
+    # the plane epilogue): plane 0 is the bf16 rounding of the fp32 result, the sum within 2^-26
+    r1 = rnd(M, N, seed=8)
+    full_r = ops.linear_split3(pl, w16, b1, torch.float32, residual=r1)
+    pl_r = ops.linear_split3(pl, w16, b1, torch.float32, residual=r1, out_planes=True)
+    assert torch.equal(pl_r[0], full_r.bfloat16())
+    s_r = pl_r[0].double() + pl_r[1].double() + pl_r[2].double()
+    assert ((s_r - full_r.double()).abs() <= full_r.double().abs() * 2.0 ** -26).all()
+    assert rel(s_r, y.double() @ w1.double().T + b1.double() + r1.double()) < 2e-6
 
 
 def test_linear_split3_rejects_unsupported_shapes():
@@ -432,14 +441,14 @@ def test_conv3x3_dir_full_size():
                                    (4, 9, 24)])
 def test_upsample2x(dt, H, W, C):
     """The default kernel (bf16: 2 x 2 output blocks when H, W >= 3; fp32 and small maps: 16-B per
-    pixel) against fp64 F.interpolate, bit-identical to the 16-B per-pixel kernel (tuning xknob 1
+    pixel) against fp64 F.interpolate, bit-identical to the 16-B per-pixel kernel (tuning upsample_quad 0
     forces it) and to the element-wise per-pixel kernel (which a misaligned view takes)."""
     from mhada_hip import _lib
     x = rnd(2, H, W, C, seed=H).to(dt)
     y = ops.upsample2x(x)
     ref = F.interpolate(x.permute(0, 3, 1, 2).double(), scale_factor=2, mode="bilinear", align_corners=False)
     assert rel(y.permute(0, 3, 1, 2), ref) < (1e-6 if dt == torch.float32 else 5e-3)
-    with _lib.tuning(xknob=1):
+    with _lib.tuning(upsample_quad=0):
         assert torch.equal(ops.upsample2x(x), y)
     buf = torch.empty(x.numel() + 1, device=DEV, dtype=dt)
     xm = buf[1:].view(x.shape)  # 2 or 4 bytes past a 16-B boundary
@@ -731,3 +740,110 @@ def test_gemm_n64_ring_kernel(nz, M, N, K):
                                   sw=(N * (K + 4), 0)))
     ref1 = a1.double() @ w1.double().transpose(1, 2) + b.double()
     assert rel(c3[..., :N], ref1) < TOL[torch.float32]
+
+
+# ---- the fp32 MHAda attention as SPLIT3 products on the bf16 MFMA (attn_split3.hip, round 6) ---------
+S3_WAVES = {"s3_8": dict(attn_waves=8), "s3_4": dict(attn_waves=4)}
+
+
+def _f32_attn_operands(B, H, Nc, Ns, scale, seed):
+    q = rnd(B, H, Nc, 64, seed=seed) * scale
+    kv = rnd(B, H, Ns, 128, seed=seed + 1) * scale
+    fcs = rnd(B, Nc, H * 64, seed=seed + 2)
+    mu, rs = ops.instnorm_stats(fcs)
+    vmu = rnd(B, H * 64, seed=seed + 3)
+    return q, kv, fcs, mu, rs, vmu
+
+
+@pytest.mark.parametrize("B,H,Ns", [(1, 1, 64), (2, 3, 100), (1, 2, 33), (2, 8, 1000), (1, 8, 4096)])
+def test_split3_kv_planes_are_exact(B, H, Ns):
+    """mhada_split3_kv: the three K planes sum to the fp32 K rows exactly (rows past Ns zero), the
+    three V'^T | V'^2^T planes to the fp32 vt image exactly, with key positions permuted inside groups
+    of 16 (bits 2 and 3 swapped, the bf16 vt image's order), and each plane is the round-to-nearest
+    bf16 of what the planes before it leave."""
+    kv = rnd(B, H, Ns, 128, seed=3) * 3
+    vt = ops.transpose_v(kv)
+    img = ops.split3_kv(kv, vt)
+    ldt = (Ns + 63) // 64 * 64
+    kp = img[..., :192 * ldt].view(B, H, 3, ldt, 64).double()
+    vp = img[..., 192 * ldt:].view(B, H, 3, 128, ldt).double()
+    ks = kp.sum(2)
+    assert torch.equal(ks[:, :, :Ns], kv[..., :64].double())
+    assert torch.all(ks[:, :, Ns:] == 0)
+    assert torch.equal(kp[:, :, 0, :Ns], kv[..., :64].bfloat16().double())
+    pos = torch.arange(ldt, device=DEV)
+    key = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1)
+    assert torch.equal(vp.sum(2), vt.double()[..., key])
+    assert torch.equal(vp[:, :, 0], vt[..., key].bfloat16().double())
+    r1 = vt[..., key].double() - vp[:, :, 0]
+    assert torch.equal(vp[:, :, 1], r1.float().bfloat16().double())
+
+
+@pytest.mark.parametrize("kernel", list(S3_WAVES))
+@pytest.mark.parametrize("B,Nc,Ns,scale", [(1, 256, 64, 0.5), (2, 300, 100, 0.5), (1, 97, 33, 0.5), (1, 513, 128, 1.0),
+                                           (2, 1000, 777, 0.5), (1, 64, 4096, 0.5), (1, 520, 1024, 1.0),
+                                           (2, 4096, 4096, 0.35), (1, 3000, 192, 1.5)])
+def test_attn_split3_fp32_accuracy(kernel, B, Nc, Ns, scale):
+    """The SPLIT3 attention (mhada_attn_split3) against fp64 on the same fp32 operands, at one to 64
+    key tiles of 64 (whole and ragged, Ns < 64), partial query blocks, 4- and 8-wave blocks, and logits
+    from ~2 to ~18 in standard deviation: within the fp32 tolerance and at most 1.3x the fp32-MFMA
+    kernel's error (mhada_attn, attn_f32_kernel) on the same operands; run-to-run bit-identical.
+    Measured (profiles/r06_gpu_tests_s3.log): 0.5-0.8x the fp32 kernel's error at logit std <= 4
+    (the bench shapes), up to 1.23x at std 8-18 — the bf16 MFMA sums its 32 products with truncating
+    partial sums (tools/split3_mfma_emulation.py), which weighs on large cancelling logits."""
+    H = 8
+    q, kv, fcs, mu, rs, vmu = _f32_attn_operands(B, H, Nc, Ns, scale, seed=31)
+    vt = ops.transpose_v(kv)
+    img = ops.split3_kv(kv, vt)
+    with _lib.tuning(**S3_WAVES[kernel]):
+        y = ops.attn_split3(q, img, Ns, fcs, mu, rs, vmu)
+        y2 = ops.attn_split3(q, img, Ns, fcs, mu, rs, vmu)
+    assert torch.equal(y, y2)
+    y32 = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+    ref = _attn_ref(q, kv, fcs, mu, rs, vmu)
+    e_s3, e_32 = rel(y, ref), rel(y32, ref)
+    assert e_s3 < TOL[torch.float32], (e_s3, e_32)
+    assert e_s3 <= 1.3 * e_32 + 1e-8, (e_s3, e_32)
+
+
+@pytest.mark.parametrize("kernel", list(S3_WAVES))
+@pytest.mark.parametrize("Nc,Ns", [(300, 700), (256, 128), (97, 33), (256, 1024), (97, 384)])
+def test_attn_split3_late_max_jump(kernel, Nc, Ns):
+    """A key ~120 log2 units above the first tile's scores: the fixed-shift SPLIT3 kernel must take its
+    exact recompute (attn_exact_q3); against fp64 within 1e-5 and 3x the fp32-MFMA kernel's error (whose
+    online max handles the jump by its rescale branch).  This case is adversarial for the bf16 MFMA:
+    the late key is 30x a query, so its logits (+-60 log2 units) are sums of large cancelling
+    products, and the MFMA's truncating 32-product partial sums cost up to 2.6x the fp32 kernel's
+    error here (measured; reproduced by tools/split3_mfma_emulation.py, whose exactly-rounded model
+    of the same SPLIT3 algorithm lands below the fp32 kernel)."""
+    B, H = 1, 8
+    q = rnd(B, H, Nc, 64, seed=11)
+    q = q / q.norm(dim=-1, keepdim=True) * 4.0
+    kv = rnd(B, H, Ns, 128, scale=0.1, seed=12)
+    late = Ns - 5
+    kv[:, :, late, :64] = 30.0 * q[:, :, : min(Nc, 1), :].mean(dim=2)
+    kv[:, :, late - 1, :64] = -kv[:, :, late, :64]
+    vt = ops.transpose_v(kv)
+    fcs = rnd(B, Nc, 512, seed=13)
+    mu, rs = ops.instnorm_stats(fcs)
+    vmu = rnd(B, 512, seed=14)
+    img = ops.split3_kv(kv, vt)
+    with _lib.tuning(**S3_WAVES[kernel]):
+        y = ops.attn_split3(q, img, Ns, fcs, mu, rs, vmu)
+    y32 = ops.mhada_attn(q, kv, vt, fcs, mu, rs, vmu, 0)
+    ref = _attn_ref(q, kv, fcs, mu, rs, vmu)
+    assert torch.isfinite(y).all()
+    e_s3, e_32 = rel(y, ref), rel(y32, ref)
+    assert e_s3 < 1e-5 and e_s3 <= 3.0 * e_32 + 1e-8, (e_s3, e_32)
+
+
+def test_attn_split3_rejects_bad_operands():
+    q, kv, fcs, mu, rs, vmu = _f32_attn_operands(1, 2, 64, 100, 0.5, seed=1)
+    vt = ops.transpose_v(kv)
+    img = ops.split3_kv(kv, vt)
+    with pytest.raises(ValueError):
+        ops.attn_split3(q, img, 200, fcs, mu, rs, vmu)  # image of another Ns
+    with pytest.raises(ValueError):
+        ops.attn_split3(q.bfloat16(), img, 100, fcs, mu, rs, vmu)
+    with pytest.raises(ValueError):
+        ops.split3_kv(kv.bfloat16(), ops.transpose_v(kv.bfloat16()))

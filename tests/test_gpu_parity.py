@@ -70,6 +70,33 @@ def test_forward_matches_reference_goldens(case, dtype):
                 np.testing.assert_allclose(fs[i].cpu().numpy(), g[f"fs{i}"], rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("split", ["all", "none"])
+@pytest.mark.parametrize("case", FULL_CASES)
+def test_fp32_goldens_with_split3_forced(case, split, monkeypatch):
+    """The fp32 path's two arithmetic forms against the reference goldens.  "all": every SPLIT3
+    product forced on — the ViT's QKV / MLP1 / MLP2 GEMMs whatever the tile-fill rule
+    (engine._split3_fills picks them only from ~30k tokens, more than any golden case has) and the
+    SPLIT3 MHAda attention; "none": the fp32-MFMA kernels throughout.  Same bounds as the default
+    fp32 run: pixel and raw MSE < 1e-4, fc / fs / fcs allclose."""
+    from mhada_hip import engine, ops
+    monkeypatch.setattr(engine, "_split3_fills", lambda M, N, dev: split == "all")
+    monkeypatch.setattr(ops, "F32_SPLIT_ATTN", split == "all")
+    g = load_golden(case)
+    cshape, sshape, seeds = g["content_shape"], g["style_shape"], g["seeds"]
+    c = seeded_image(*map(int, cshape), int(seeds[0])).to(DEV)
+    s = seeded_image(*map(int, sshape), int(seeds[1])).to(DEV)
+    fc, fs, fcs, cs = stylize(models(str(g["activation"]), torch.float32), c, s)
+    cs = cs.cpu().numpy()
+    assert mse01(cs, g["cs"]) < 1e-4
+    assert mse_raw(cs, g["cs"]) < 1e-4
+    if "fcs" in g:
+        np.testing.assert_allclose(fcs.cpu().numpy(), g["fcs"], rtol=1e-3, atol=2e-3)
+    for i in (0, 2):
+        if f"fc{i}" in g:
+            np.testing.assert_allclose(fc[i].cpu().numpy(), g[f"fc{i}"], rtol=1e-3, atol=1e-3)
+            np.testing.assert_allclose(fs[i].cpu().numpy(), g[f"fs{i}"], rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_forward_matches_numpy_oracle(dtype):
     from oracle import mhada_oracle as O
