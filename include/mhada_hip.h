@@ -205,6 +205,13 @@ int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
  * mhada_attn_split3: q fp32 [B][H][Nc][64] (split on load) and img -> out fp32 [B][Nc][64H]; the other
  *   arguments as mhada_attn. */
 int mhada_split3_kv(const float* kv, const float* vt, void* img, int B, int H, int Ns, mhada_stream_t stream);
+/* The block's K|V' projection written straight as that plane image (the engine's fp32 softmax path:
+ * replaces mhada_gemm with the vt epilogue plus mhada_split3_kv, adaDecoder.py:178,182):
+ *   Y[n][o] = sum_c (fs[b][n][64h+c] - mu_s[b][64h+c]) wkv[b][h][o][c] + bkv[h][o]  (fp32 MFMA),
+ * K = Y[:, :64], V' = Y[:, 64:] (V'^2 its fp32 square); fs [B][Ns][64H] fp32, mu_s [B][64H], wkv
+ * [B][H][128][64] fp32 and bkv [H][128] from mhada_fold_block (dtype MHADA_F32). */
+int mhada_kv_proj_split3(const float* fs, const float* mu_s, const float* wkv, const float* bkv, void* img,
+                         int B, int H, int Ns, mhada_stream_t stream);
 int mhada_attn_split3(const float* q, const void* img, const float* fcs, const float* fcs_mu,
                       const float* fcs_rstd, const float* v_mu, float* out, int B, int H, int Nc, int Ns,
                       mhada_stream_t stream);

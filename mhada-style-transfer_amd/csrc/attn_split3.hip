@@ -99,6 +99,103 @@ __global__ void __launch_bounds__(256) split3_kv_kernel(const float* __restrict_
   }
 }
 
+// The K|V' projection of one MHAda block (adaDecoder.py:178,182 after the fold of mhada_fold_block)
+// written straight as the plane image (replaces the fp32 projection GEMM with its vt epilogue plus
+// split3_kv_kernel, and their fp32 kv / vt round trip through HBM):
+//   Y[n][o] = sum_c (fs[b][n][64h + c] - mu[b][64h + c]) wkv[b][h][o][c] + bkv[h][o]
+// K = Y[:, 0:64] -> K planes, V' = Y[:, 64:128] -> V'^T and V'^2^T (the fp32 square of the fp32 V')
+// planes.  One workgroup per (64 keys, b h): X (centred on load) and W staged in LDS, the 64 x 128
+// product on v_mfma_f32_32x32x2_f32 (4 waves, two 32 x 32 blocks each, K = 64), Y through LDS (over
+// the operand images), then 16-B plane stores.  Keys >= Ns are written as zeros.
+__global__ void __launch_bounds__(256) kv_proj_s3_kernel(const float* __restrict__ fs, const float* __restrict__ mu,
+                                                         const float* __restrict__ wkv, const float* __restrict__ bkv,
+                                                         bf16* __restrict__ img, int H, int Ns, int ldt) {
+  constexpr int LX = 65, LY = 65;  // padded rows: the MFMA operand reads and the transposed Y reads
+  __shared__ float sm[192 * LX];   // X [key][c] (centred) | W [o][c]; then Y [o][key] (50 KiB: 3 workgroups per CU)
+  float* sX = sm;
+  float* sW = sm + 64 * LX;
+  float* sY = sm;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H, n0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int C = 64 * H;
+  const float* xb = fs + (long long)b * Ns * C + 64 * h;
+  const float* mb = mu + (long long)b * C + 64 * h;
+  const float* wb = wkv + (long long)bh * 128 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 256 * i, n = idx >> 4, c = (idx & 15) * 4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (n0 + n < Ns) {
+      x = *reinterpret_cast<const f32x4*>(xb + (long long)(n0 + n) * C + c);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(mb + c);
+      x = x - m;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sX[n * LX + c + e] = x[e];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int idx = tid + 256 * i, o = idx >> 4, c = (idx & 15) * 4;
+    const f32x4 w = *reinterpret_cast<const f32x4*>(wb + o * 64 + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sW[o * LX + c + e] = w[e];
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, r32 = lane & 31, hh = lane >> 5;
+  const int nb = wave & 1, ob = wave >> 1;  // keys 32 nb .., outputs 64 ob ..
+  f32x16 acc[2] = {};
+#pragma unroll 8
+  for (int k = 0; k < 64; k += 2) {
+    const float bv = sX[(32 * nb + r32) * LX + k + hh];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+      acc[ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(sW[(64 * ob + 32 * ni + r32) * LX + k + hh], bv, acc[ni], 0, 0, 0);
+  }
+  const float* bb = bkv + h * 128;
+  __syncthreads();  // every wave's operand reads are done before Y overwrites them
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = 64 * ob + 32 * ni + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      sY[o * LY + 32 * nb + r32] = acc[ni][r] + bb[o];
+    }
+  __syncthreads();
+  bf16* kp = img + (long long)bh * s3_image(ldt);
+  bf16* vp = kp + 192LL * ldt;
+  const long long kps = 64LL * ldt, vps = 128LL * ldt;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // K planes: 64 keys x 8 runs of 8 outputs
+    const int idx = tid + 256 * i, n = idx >> 3, o0 = (idx & 7) * 8;
+    const bool valid = n0 + n < Ns;
+    bf16x8 a, c1, c2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_into(valid ? sY[(o0 + j) * LY + n] : 0.f, a, c1, c2, j);
+    bf16* dst = kp + (long long)(n0 + n) * 64 + o0;
+    *reinterpret_cast<bf16x8*>(dst) = a;
+    *reinterpret_cast<bf16x8*>(dst + kps) = c1;
+    *reinterpret_cast<bf16x8*>(dst + 2 * kps) = c2;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // V'^T | V'^2^T planes: 64 rows x 8 runs of 8 key positions
+    const int idx = tid + 256 * i, vo = idx >> 3, a8 = idx & 7;
+    bf16x8 a, c1, c2, s0, s1, s2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = 16 * (a8 >> 1) + 8 * (j >> 2) + 4 * (a8 & 1) + (j & 3);  // position 8 a8 + j
+      const float v = n0 + n < Ns ? sY[(64 + vo) * LY + n] : 0.f;
+      split3_into(v, a, c1, c2, j);
+      split3_into(v * v, s0, s1, s2, j);
+    }
+    bf16* dst = vp + (long long)vo * ldt + n0 + 8 * a8;
+    *reinterpret_cast<bf16x8*>(dst) = a;
+    *reinterpret_cast<bf16x8*>(dst + vps) = c1;
+    *reinterpret_cast<bf16x8*>(dst + 2 * vps) = c2;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt) = s0;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt + vps) = s1;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt + 2 * vps) = s2;
+  }
+}
+
 // x_i y_j, i + j <= 2, small terms first: acc + x2y0 + x1y1 + x0y2 + x1y0 + x0y1 + x0y0 (A = x, B = y)
 MHADA_DEV f32x4 mfma6(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0, const bf16x8& b1,
                       const bf16x8& b2, f32x4 acc) {
@@ -389,6 +486,17 @@ extern "C" int mhada_split3_kv(const float* kv, const float* vt, void* img, int 
   hipLaunchKernelGGL(split3_kv_kernel, dim3(ldt / 64, (unsigned)bhn), dim3(256), 0, (hipStream_t)s_, kv, vt,
                      reinterpret_cast<bf16*>(img), Ns, ldt);
   return check_launch("mhada_split3_kv");
+}
+
+extern "C" int mhada_kv_proj_split3(const float* fs, const float* mu_s, const float* wkv, const float* bkv, void* img,
+                                    int B, int H, int Ns, mhada_stream_t s_) {
+  if (!fs || !mu_s || !wkv || !bkv || !img || B <= 0 || H <= 0 || Ns <= 0) return fail("mhada_kv_proj_split3: bad args");
+  const long long bhn = (long long)B * H;
+  if (bhn > 65535) return fail("mhada_kv_proj_split3: B * H > 65535");
+  const int ldt = (Ns + 63) / 64 * 64;
+  hipLaunchKernelGGL(kv_proj_s3_kernel, dim3(ldt / 64, (unsigned)bhn), dim3(256), 0, (hipStream_t)s_, fs, mu_s, wkv, bkv,
+                     reinterpret_cast<bf16*>(img), H, Ns, ldt);
+  return check_launch("mhada_kv_proj_split3");
 }
 
 extern "C" int mhada_attn_split3(const float* q, const void* img, const float* fcs, const float* fcs_mu,

@@ -280,13 +280,15 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
     C = H * HEAD_DIM
     B, Nc, Cc = fc.t.shape
     cached = bool(side)
-    mom = None
-    img = None
+    mom = img = kv = vt = None
+    act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
+    # fp32 softmax: the SPLIT3 attention on bf16 planes of K and V'^T | V'^2^T (csrc/attn_split3.hip)
+    split_attn = act == ACT_SOFTMAX and dt == torch.float32 and ops.F32_SPLIT_ATTN
     if cached:
-        mu_s, rstd_s, kv, vt, mom = side["mu_s"], side["rstd_s"], side["kv"], side["vt"], side.get("mom")
-        img = side.get("img")
-        if kv.shape[0] != B:
-            raise ValueError(f"cached style batch {kv.shape[0]} != content batch {B}")
+        mu_s, rstd_s, mom, Ns = side["mu_s"], side["rstd_s"], side.get("mom"), side["Ns"]
+        kv, vt, img = side.get("kv"), side.get("vt"), side.get("img")
+        if side["B"] != B:
+            raise ValueError(f"cached style batch {side['B']} != content batch {B}")
     else:
         if fs.t.shape[2] != C:
             raise ValueError(f"channel mismatch: block expects {C}")
@@ -295,7 +297,6 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
         raise ValueError(f"channel mismatch: block expects {C}")
     mu_c, rstd_c = fc.stats()
     mu_o, rstd_o = fcs.stats()
-    act = ACT_COSINE if blk.activation_name == "cosine" else ACT_SOFTMAX
     wq, wkv, bkv, v_mu = ops.fold_block(prep["wf"], prep["wg"], prep["wh"], prep["bg"], prep["bh"],
                                         rstd_c, mu_s, rstd_s, dt, ops.LOG2E if act == ACT_SOFTMAX else 1.0)
     dev = fc.t.device
@@ -303,7 +304,13 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
     ops.gemm(a=fc.t, w=wq, c=q, M=Nc, N=HEAD_DIM, K=HEAD_DIM, compute=dt, lda=C, sa=(Nc * C, HEAD_DIM),
              nb=(B, H), a_mu=mu_c, smu=(C, HEAD_DIM), ldw=HEAD_DIM, sw=(H * HEAD_DIM * HEAD_DIM, HEAD_DIM * HEAD_DIM),
              bias=prep["bf"], sb=(0, HEAD_DIM), ldc=HEAD_DIM, sc=(H * Nc * HEAD_DIM, Nc * HEAD_DIM))
-    if not cached:
+    if not cached and split_attn:
+        Ns = fs.t.shape[1]
+        # K|V' projection written straight as the SPLIT3 attention's bf16 plane image (no fp32 kv / vt)
+        img = ops.kv_proj_split3(fs.t, mu_s, wkv, bkv)
+        if side is not None:
+            side.update(mu_s=mu_s, rstd_s=rstd_s, img=img, Ns=Ns, B=B)
+    elif not cached:
         Ns = fs.t.shape[1]
         # K|V' projection: K rows into kv[..., :64] (the attention's K operand), V' straight into
         # the transposed V'^T | V'^2^T image vt (the GEMM's vt epilogue; kv[..., 64:] unused)
@@ -320,20 +327,14 @@ def block_forward(blk, fc: _Feat, fs: Optional[_Feat], fcs: _Feat, dt: torch.dty
             ops.cosine_prep(None, kv)
             mom = ops.cosine_moments(kv, vt)
         if side is not None:
-            side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt, mom=mom)
-    # fp32 softmax: K and V'^T | V'^2^T as bf16 planes for the SPLIT3 attention (once per style)
-    split_attn = act == ACT_SOFTMAX and dt == torch.float32 and ops.F32_SPLIT_ATTN
-    if split_attn and img is None:
-        img = ops.split3_kv(kv, vt)
-        if side is not None:
-            side["img"] = img
+            side.update(mu_s=mu_s, rstd_s=rstd_s, kv=kv, vt=vt, mom=mom, Ns=Ns, B=B)
     if act == ACT_COSINE:
         ops.cosine_prep(q, None)
         with _timed("mhada_attn"):
             att = ops.cosine_attn(q, mom, fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] dt
     elif split_attn:
         with _timed("mhada_attn"):
-            att = ops.attn_split3(q, img, kv.shape[2], fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] fp32
+            att = ops.attn_split3(q, img, Ns, fcs.t, mu_o, rstd_o, v_mu)  # [B][Nc][C] fp32
     else:
         with _timed("mhada_attn"):
             att = ops.mhada_attn(q, kv, vt, fcs.t, mu_o, rstd_o, v_mu, act)  # [B][Nc][C] dt
@@ -358,12 +359,13 @@ def style_cache(ada, fs: Sequence[torch.Tensor], dt: torch.dtype):
         return [None] * len(ada.adaAttnHead), False
     sig = tuple(_signature(b) for b in ada.adaAttnHead)
     vers = tuple(t._version for t in fs)
+    mode = (dt, ops.F32_SPLIT_ATTN)  # the cached side tensors depend on the attention form
     c = ada.__dict__.get("_mhada_style")
-    if (c is not None and c["dt"] == dt and c["sig"] == sig and c["vers"] == vers
+    if (c is not None and c["mode"] == mode and c["sig"] == sig and c["vers"] == vers
             and len(c["refs"]) == len(fs) and all(r() is t for r, t in zip(c["refs"], fs))):
         return c["sides"], True
     sides = [dict() for _ in ada.adaAttnHead]
-    ada.__dict__["_mhada_style"] = dict(dt=dt, sig=sig, vers=vers, refs=[weakref.ref(t) for t in fs], sides=sides)
+    ada.__dict__["_mhada_style"] = dict(mode=mode, sig=sig, vers=vers, refs=[weakref.ref(t) for t in fs], sides=sides)
     return sides, False
 
 

@@ -566,6 +566,26 @@ def split3_kv(kv: torch.Tensor, vt: torch.Tensor) -> torch.Tensor:
     return img
 
 
+def kv_proj_split3(fs: torch.Tensor, mu_s: torch.Tensor, wkv: torch.Tensor, bkv: torch.Tensor) -> torch.Tensor:
+    """``mhada_kv_proj_split3``: the MHAda block's K|V' projection of the fp32 style tokens fs [B][Ns][64H]
+    (centred by mu_s [B][64H], folded fp32 weights wkv [B][H][128][64] and bias bkv [H][128] of
+    ``fold_block``) written straight as the ``attn_split3`` plane image [B][H][576 ceil64(Ns)]."""
+    _need_gpu(fs, mu_s, wkv, bkv)
+    B, Ns, C = fs.shape
+    H = C // 64
+    for t in (fs, mu_s, wkv, bkv):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("kv_proj_split3 needs contiguous float32 operands")
+    if C % 64 or mu_s.shape != (B, C) or wkv.shape != (B, H, 128, 64) or bkv.shape != (H, 128):
+        raise ValueError(f"kv_proj_split3: bad shapes fs {tuple(fs.shape)} mu {tuple(mu_s.shape)} "
+                         f"wkv {tuple(wkv.shape)} bkv {tuple(bkv.shape)}")
+    ldt = (Ns + 63) // 64 * 64
+    img = torch.empty(B, H, 576 * ldt, device=fs.device, dtype=torch.bfloat16)
+    _call("mhada_kv_proj_split3", fs, fs.data_ptr(), mu_s.data_ptr(), wkv.data_ptr(), bkv.data_ptr(), img.data_ptr(),
+          B, H, Ns)
+    return img
+
+
 def attn_split3(q, img, Ns: int, fcs, fcs_mu, fcs_rstd, v_mu) -> torch.Tensor:
     """``mhada_attn_split3``: mhada_attn's fp32 softmax output from fp32 q [B][H][Nc][64] and the
     ``split3_kv`` plane image of Ns keys."""

@@ -847,3 +847,41 @@ def test_attn_split3_rejects_bad_operands():
         ops.attn_split3(q.bfloat16(), img, 100, fcs, mu, rs, vmu)
     with pytest.raises(ValueError):
         ops.split3_kv(kv.bfloat16(), ops.transpose_v(kv.bfloat16()))
+
+
+@pytest.mark.parametrize("B,H,Ns", [(1, 8, 64), (2, 8, 100), (1, 2, 33), (2, 8, 4096), (1, 8, 1000)])
+def test_kv_proj_split3_matches_projection_then_split(B, H, Ns):
+    """mhada_kv_proj_split3 (the K|V' projection written straight as the SPLIT3 plane image) against
+    fp64 and against the fp32 projection GEMM with its vt epilogue followed by mhada_split3_kv: the
+    plane sums agree to fp32 rounding (the two fp32 MFMA reductions differ in order only), keys past Ns
+    are zero in both."""
+    C = 64 * H
+    fs = rnd(B, Ns, C, seed=1) * 2 + 0.3
+    mu = fs.mean(1)
+    w = rnd(B, H, 128, 64, scale=0.125, seed=2)
+    bkv = rnd(H, 128, seed=3)
+    bkv[:, 64:] = 0
+    img = ops.kv_proj_split3(fs, mu, w, bkv)
+    ldt = (Ns + 63) // 64 * 64
+    kv = torch.empty(B, H, Ns, 128, device=DEV)
+    vt = torch.empty(B, H, 128, ldt, device=DEV)
+    ops.gemm(a=fs, w=w, c=kv, M=Ns, N=128, K=64, compute=torch.float32, lda=C, sa=(Ns * C, 64), nb=(B, H), a_mu=mu,
+             smu=(C, 64), ldw=64, sw=(H * 128 * 64, 128 * 64), bias=bkv, sb=(0, 128), ldc=128,
+             sc=(H * Ns * 128, Ns * 128), vt=vt, ldt=ldt, svt=(H * 128 * ldt, 128 * ldt))
+    ref = ops.split3_kv(kv, vt)
+
+    def sums(im):
+        kp = im[..., :192 * ldt].view(B, H, 3, ldt, 64).double().sum(2)
+        vp = im[..., 192 * ldt:].view(B, H, 3, 128, ldt).double().sum(2)
+        return kp, vp
+    (k1, v1), (k2, v2) = sums(img), sums(ref)
+    assert torch.all(k1[:, :, Ns:] == 0) and torch.all(v1[..., Ns:] == 0)
+    assert rel(k1, k2) < 1e-6 and rel(v1, v2) < 1e-6
+    y = torch.einsum("bnhc,bhoc->bhno", (fs.double() - mu.double()[:, None]).view(B, Ns, H, 64), w.double()) + \
+        bkv.double()[None, :, None, :]
+    assert rel(k1[:, :, :Ns], y[..., :64]) < 1e-6
+    pos = torch.arange(ldt, device=DEV)
+    key = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1)
+    vref = torch.zeros(B, H, 128, ldt, device=DEV, dtype=torch.float64)
+    vref[..., :Ns] = torch.cat([y[..., 64:], y[..., 64:] ** 2], -1).transpose(-1, -2)
+    assert rel(v1, vref[..., key]) < 2e-6
