@@ -5,6 +5,11 @@ AdaFormer calls, VGG19 features, global-style / local-feature / output- and feat
 identity losses weighted 100 / 15 / 2 / 2 / 0.05 / 0.1, backward.  Stores the inputs' seeds, the
 flow and mask, the seven losses and per-parameter gradient norms.
 
+Two cases: 64x64 frames with a 64x64 style (train_video_64_b2.npz) and 64x128 frames with a 64x64
+style (train_video_64x128_s64_b2.npz) — the latter has train_video.py's shape structure (frames of
+twice the style's width, 256x512 / 256x256 there), so VideoTrainer's shape grouping splits its ViT and
+AdaFormer calls as it does at the real shapes.
+
 Usage:  python tests/golden/make_video_train_goldens.py
 """
 from __future__ import annotations
@@ -25,7 +30,7 @@ from make_video_goldens import smooth_flow  # noqa: E402
 from mhada_hip.recipe import load_recipe, seeded_image  # noqa: E402
 
 
-def main():
+def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2"):
     torch.set_num_threads(8)
     R = load_reference()
     U, L = R["utilities"], R["lossfn"]
@@ -42,8 +47,8 @@ def main():
     mseMatrix = nn.MSELoss(reduction="none")
     # batch 2: at batch 1 this CPU PyTorch build's instance_norm backward misreads a gradient with
     # channels-last strides (which the reference's permuted head outputs produce), see DESIGN.md §4
-    B, H, W = 2, 64, 64
-    style = seeded_image(B, H, W, 201)
+    B = 2
+    style = seeded_image(B, Hs, Ws, 201)
     c1 = seeded_image(B, H, W, 202)
     c2 = seeded_image(B, H, W, 203)
     g = torch.Generator().manual_seed(204)
@@ -90,14 +95,16 @@ def main():
 
     out = {
         "seeds": np.array([201, 202, 203]), "flow": np32(flow), "mask": np32(mask),
+        "frame_shape": np.array([H, W]), "style_shape": np.array([Hs, Ws]),
         "losses": np.array([float(v) for v in (loss_gs, loss_lf, loss_ot, loss_ft, loss_id1, loss_id2, loss)]),
         "grad_vit_c": grad_summary(vit_c), "grad_vit_s": grad_summary(vit_s), "grad_ada": grad_summary(ada),
         "grad_ada_last_conv_w": np32(ada.decoder.conv3[1].conv.conv.weight.grad),
     }
-    path = os.path.join(HERE, "train_video_64_b2.npz")
+    path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
     print(f"wrote {path}: losses {out['losses']}, mask mean {float(mask.mean()):.3f}")
 
 
 if __name__ == "__main__":
     main()
+    main(64, 128, 64, 64, "train_video_64x128_s64_b2")

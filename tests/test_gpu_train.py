@@ -8,17 +8,19 @@ pytestmark = pytest.mark.gpu
 
 from mhada_hip.recipe import seeded_image
 from mhada_hip.train import Trainer, VideoTrainer
-from test_train_cpu import build, check_against_golden, check_video_against_golden
+from test_train_cpu import VIDEO_GOLDENS, build, check_against_golden, check_video_against_golden
 
 
 def test_train_step_matches_reference_golden_gpu():
     check_against_golden(Trainer(*build("cuda")), "cuda")
 
 
-def test_video_train_step_matches_reference_golden_gpu():
+@pytest.mark.parametrize("name", VIDEO_GOLDENS)
+def test_video_train_step_matches_reference_golden_gpu(name):
     """One train_video.py step (5 AdaFormer calls, temporal losses with the warp and its adjoint on
-    HIP) against the reference's own composition of it (tests/golden/make_video_train_goldens.py)."""
-    check_video_against_golden(VideoTrainer(*build("cuda")), "cuda")
+    HIP) against the reference's own composition of it (tests/golden/make_video_train_goldens.py),
+    square frames and frames of twice the style's width (the grouped calls split by shape)."""
+    check_video_against_golden(VideoTrainer(*build("cuda")), "cuda", name)
 
 
 def test_train_step_256_b2_losses_match_oracle_and_grads_match_cpu():

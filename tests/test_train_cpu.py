@@ -48,11 +48,17 @@ def test_train_step_matches_reference_golden():
     check_against_golden(Trainer(*build()), "cpu")
 
 
-def check_video_against_golden(tr, device):
+VIDEO_GOLDENS = ["train_video_64_b2", "train_video_64x128_s64_b2"]
+
+
+def check_video_against_golden(tr, device, name="train_video_64_b2"):
     """One train_video.py:110-166 step against the reference's own composition of it
     (tests/golden/make_video_train_goldens.py): the seven losses and every gradient norm."""
-    g = load_golden("train_video_64_b2")
-    style, c1, c2 = (seeded_image(2, 64, 64, int(x)).to(device) for x in g["seeds"])
+    g = load_golden(name)
+    fh, fw = (int(x) for x in g["frame_shape"]) if "frame_shape" in g else (64, 64)
+    sh, sw = (int(x) for x in g["style_shape"]) if "style_shape" in g else (64, 64)
+    style = seeded_image(2, sh, sw, int(g["seeds"][0])).to(device)
+    c1, c2 = (seeded_image(2, fh, fw, int(x)).to(device) for x in g["seeds"][1:])
     flow = torch.from_numpy(g["flow"]).to(device)
     mask = torch.from_numpy(g["mask"]).to(device)
     out = tr.backward(style, c1, c2, flow, mask)
@@ -66,9 +72,12 @@ def check_video_against_golden(tr, device):
                                g["grad_ada_last_conv_w"], rtol=2e-3, atol=1e-3)
 
 
-def test_video_train_step_matches_reference_golden():
+@pytest.mark.parametrize("name", VIDEO_GOLDENS)
+def test_video_train_step_matches_reference_golden(name):
+    """Both video goldens; the 64x128-frame / 64x64-style one splits VideoTrainer's grouped ViT and
+    AdaFormer calls by shape as train_video.py's 256x512 / 256x256 shapes do."""
     torch.set_num_threads(8)
-    check_video_against_golden(VideoTrainer(*build()), "cpu")
+    check_video_against_golden(VideoTrainer(*build()), "cpu", name)
 
 
 def test_checkpoint_dict_roundtrip(tmp_path):
