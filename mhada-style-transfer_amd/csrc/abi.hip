@@ -73,7 +73,7 @@ const Tuning& tuning() {
 
 }  // namespace mhada
 
-extern "C" int mhada_abi_version(void) { return 16; }  // 16: mhada_split3_kv / mhada_kv_proj_split3 / mhada_attn_split3 (the fp32 softmax MHAda attention as SPLIT3 products on the bf16 MFMA); 15: mhada_gemm a_mode MHADA_A_SPLIT3 (fp32-accurate products on the bf16 MFMA), mhada_layernorm y_dtype MHADA_BF16X3; 14: mhada_cosine_moments / mhada_cosine_attn (linear cosine activation), mhada_warp_bwd; 13: mhada_clock_probe, knob wino4, knobs of removed variants dropped (attn_sched, wino_ws, wino_l2pf, gemm_f32b, gemm_n64_pp, gemm_n64_cen), attn_waves 0 = auto; 12: mhada_feat_stats; 10-12 also added a trailing relu_mask / relu argument to mhada_conv3x3_wino, mhada_reflect_fold and mhada_feat_loss_bwd and mhada_gemm relu = 2; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
+extern "C" int mhada_abi_version(void) { return 16; }  // 16: mhada_split3_kv / mhada_kv_proj_split3 / mhada_attn_split3 / mhada_attn_train_fwd_split3 (the fp32 softmax MHAda attention as SPLIT3 products on the bf16 MFMA); 15: mhada_gemm a_mode MHADA_A_SPLIT3 (fp32-accurate products on the bf16 MFMA), mhada_layernorm y_dtype MHADA_BF16X3; 14: mhada_cosine_moments / mhada_cosine_attn (linear cosine activation), mhada_warp_bwd; 13: mhada_clock_probe, knob wino4, knobs of removed variants dropped (attn_sched, wino_ws, wino_l2pf, gemm_f32b, gemm_n64_pp, gemm_n64_cen), attn_waves 0 = auto; 12: mhada_feat_stats; 10-12 also added a trailing relu_mask / relu argument to mhada_conv3x3_wino, mhada_reflect_fold and mhada_feat_loss_bwd and mhada_gemm relu = 2; 11: mhada_transpose64; 10: mhada_attn_train_fwd_vt; 9: 3-channel conv adjoints; 8: feat_loss_bwd; 7: gemm c2 / vt outputs, instnorm / attention backward helpers; 6: LayerNorm / pos-embed adjoints; 5: Winograd conv; 4: CONV3X3_ZERO, gemm_tn, backward helpers
 
 extern "C" const char* mhada_last_error(void) { return mhada::g_last_error.c_str(); }
 

@@ -210,7 +210,7 @@ MHADA_DEV f32x4 mfma6(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, cons
 // Exact two-pass recompute of one wave's 2 x 16 queries (the rare path when a row sum trips
 // kShiftSumThr): the true row max over all keys, then the full pass, planes read from L2.
 MHADA_DEV void attn_exact_q3(const AttnP& p, const bf16* kp, const bf16* vp, const bf16x8 (&qf)[3][2][2],
-                             f32x4 (&O)[2][8], float (&lt)[2], int g, int r16) {
+                             f32x4 (&O)[2][8], float (&lt)[2], float (&mx)[2], int g, int r16) {
   const int Ns = p.Ns;
   const long long kps = 64LL * p.ldt, vps = 128LL * p.ldt;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
@@ -279,6 +279,7 @@ MHADA_DEV void attn_exact_q3(const AttnP& p, const bf16* kp, const bf16* vp, con
   for (int qg = 0; qg < 2; ++qg) {
     lt[qg] += __shfl_xor(lt[qg], 16, 64);
     lt[qg] += __shfl_xor(lt[qg], 32, 64);
+    mx[qg] = m2[qg];
   }
 }
 
@@ -293,7 +294,94 @@ MHADA_DEV void s3_mask(f32x4 (&S)[2][2][2], int key0, int Ns, int g) {
         if (key0 + 32 * kg + fsq_key(4 * g + j, t) >= Ns) S[0][kg][t][j] = S[1][kg][t][j] = -INFINITY;
 }
 
-template <int NW>
+// Training forward (mhada_attn_train_fwd_split3): k [BH][Ns][64] and the centred v [BH][Ns][64] rows
+// of the training attention -> the plane image (K planes from k; V'^T | V'^2^T planes from v, its fp32
+// square, key positions permuted as split3_kv_kernel's).  One workgroup per (64 keys, b h).
+__global__ void __launch_bounds__(256) train_s3_prep_kernel(const float* __restrict__ k, const float* __restrict__ v,
+                                                            bf16* __restrict__ img, int Ns, int ldt) {
+  __shared__ float sv[64 * 65];  // [key][o]
+  const int bh = blockIdx.y, n0 = blockIdx.x * 64, tid = threadIdx.x;
+  bf16* kp = img + (long long)bh * s3_image(ldt);
+  bf16* vp = kp + 192LL * ldt;
+  const float* kb = k + (long long)bh * Ns * 64;
+  const float* vb = v + (long long)bh * Ns * 64;
+  const long long kps = 64LL * ldt, vps = 128LL * ldt;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 256 * i, n = idx >> 4, d = (idx & 15) * 4;
+    const bool ok = n0 + n < Ns;
+    const f32x4 x = ok ? *reinterpret_cast<const f32x4*>(kb + (long long)(n0 + n) * 64 + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 y = ok ? *reinterpret_cast<const f32x4*>(vb + (long long)(n0 + n) * 64 + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x4 a, b, c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_into(x[e], a, b, c, e);
+    bf16* dst = kp + (long long)(n0 + n) * 64 + d;
+    *reinterpret_cast<bf16x4*>(dst) = a;
+    *reinterpret_cast<bf16x4*>(dst + kps) = b;
+    *reinterpret_cast<bf16x4*>(dst + 2 * kps) = c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sv[n * 65 + d + e] = y[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 64 rows o x 8 runs of 8 key positions
+    const int idx = tid + 256 * i, o = idx >> 3, a8 = idx & 7;
+    bf16x8 a, c1, c2, s0, s1, s2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = 16 * (a8 >> 1) + 8 * (j >> 2) + 4 * (a8 & 1) + (j & 3);  // position 8 a8 + j
+      const float x = sv[n * 65 + o];
+      split3_into(x, a, c1, c2, j);
+      split3_into(x * x, s0, s1, s2, j);
+    }
+    bf16* dst = vp + (long long)o * ldt + n0 + 8 * a8;
+    *reinterpret_cast<bf16x8*>(dst) = a;
+    *reinterpret_cast<bf16x8*>(dst + vps) = c1;
+    *reinterpret_cast<bf16x8*>(dst + 2 * vps) = c2;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt) = s0;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt + vps) = s1;
+    *reinterpret_cast<bf16x8*>(dst + 64LL * ldt + 2 * vps) = s2;
+  }
+}
+
+// Training epilogue in the 16x16x32 layout (attn_train_epilogue's contract, attn.hip): per query row
+// out' = sqrt(max(E2' - M'^2, 1e-6)) x + M', mo = [M' | E2'], lse2 = m2 + log2(l); x = p.fcs
+// [BH][Nc][64].  O[qg][dvb] holds O^T[dv][q] for dv = 16 dvb + 4 g + e (dvb 0-3: M', 4-7: E2').
+MHADA_DEV void attn_train_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], const float (&lt)[2],
+                                     const float (&m2)[2], long long bh, int q0, int g, int r16) {
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q0 + 16 * qg + r16;
+    if (q >= p.Nc) continue;
+    const float inv = 1.0f / lt[qg];
+    const long long row = bh * p.Nc + q;
+    const float* xr = p.fcs + row * 64;
+    float* orow = reinterpret_cast<float*>(p.out) + row * 64;
+    float* mrow = p.mo + row * 128;
+#pragma unroll
+    for (int dvb = 0; dvb < 4; ++dvb) {
+      const int dv0 = 16 * dvb + 4 * g;
+      const f32x4 xx = *reinterpret_cast<const f32x4*>(xr + dv0);
+      f32x4 o, mm, ee;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = O[qg][dvb][e] * inv;
+        const float e2 = O[qg][dvb + 4][e] * inv;
+        o[e] = sqrtf(fmaxf(e2 - m1 * m1, 1e-6f)) * xx[e] + m1;
+        mm[e] = m1;
+        ee[e] = e2;
+      }
+      *reinterpret_cast<f32x4*>(orow + dv0) = o;
+      *reinterpret_cast<f32x4*>(mrow + dv0) = mm;
+      *reinterpret_cast<f32x4*>(mrow + 64 + dv0) = ee;
+    }
+    if (g == 0) p.lse[row] = m2[qg] + __log2f(lt[qg]);
+  }
+}
+
+// TRAIN: the training forward — Q in natural units (log2 e applied in fp32 on load, as attn_f32_kernel's
+// TRAIN form), the training epilogue (out', [M' | E2'], lse2).
+template <int NW, bool TRAIN = false>
 __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   constexpr int TK = kS3Tk;
   constexpr int KPL = TK * 64, VPL = 128 * TK, SLOT = 3 * (KPL + VPL);  // bf16 elements
@@ -321,7 +409,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
       const f32x4 hi = *reinterpret_cast<const f32x4*>(qp + 32 * dh + 4);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float x = q < p.Nc ? (e < 4 ? lo[e] : hi[e - 4]) : 0.f;
+        const float x = q < p.Nc ? (e < 4 ? lo[e] : hi[e - 4]) * (TRAIN ? 1.4426950408889634f : 1.0f) : 0.f;
         split3_into(x, qf[0][qg][dh], qf[1][qg][dh], qf[2][qg][dh], e);
       }
     }
@@ -457,11 +545,15 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
     s3_mask(Sa, NFULL * TK, Ns, g);
     finish(NFULL & 1, Sa);
   }
-  float lt[2];
+  float lt[2], mx[2];
 #pragma unroll
-  for (int qg = 0; qg < 2; ++qg) lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
-  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3(p, kp, vp, qf, O, lt, g, r16);
-  attn_epilogue_q<float>(p, O, lt, b, hh, q0, g, r16);
+  for (int qg = 0; qg < 2; ++qg) {
+    lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
+    mx[qg] = -Cm[qg][0];
+  }
+  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3(p, kp, vp, qf, O, lt, mx, g, r16);
+  if constexpr (TRAIN) attn_train_epilogue_q(p, O, lt, mx, bh, q0, g, r16);
+  else attn_epilogue_q<float>(p, O, lt, b, hh, q0, g, r16);
 }
 
 static int s3_num_cus() {
@@ -519,7 +611,36 @@ extern "C" int mhada_attn_split3(const float* q, const void* img, const float* f
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn_split3: grid too large");
   p.nblk = (int)nblk;
   const hipStream_t s = (hipStream_t)s_;
-  if (nw == 8) hipLaunchKernelGGL(attn_s3_kernel<8>, dim3(p.nblk), dim3(512), 0, s, p);
-  else hipLaunchKernelGGL(attn_s3_kernel<4>, dim3(p.nblk), dim3(256), 0, s, p);
+  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8>), dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((attn_s3_kernel<4>), dim3(p.nblk), dim3(256), 0, s, p);
   return check_launch("mhada_attn_split3");
+}
+
+// Training forward as SPLIT3 products (the contract of mhada_attn_train_fwd_vt, attn.hip): q, x
+// [BH][Nc][64]; k, v [BH][Ns][64] (v centred) -> out' [BH][Nc][64], mo = [M' | E2'] [BH][Nc][128],
+// lse2 [BH][Nc]; img: caller-provided workspace of BH * 576 * ceil64(Ns) bf16, filled here from k, v.
+extern "C" int mhada_attn_train_fwd_split3(const float* q, const float* k, const float* v, void* img, const float* x,
+                                           float* out, float* mo, float* lse, int BH, int Nc, int Ns,
+                                           mhada_stream_t s_) {
+  if (!q || !k || !v || !img || !x || !out || !mo || !lse || BH <= 0 || Nc <= 0 || Ns <= 0)
+    return fail("mhada_attn_train_fwd_split3: bad args");
+  if (BH > 65535) return fail("mhada_attn_train_fwd_split3: BH > 65535");
+  const hipStream_t s = (hipStream_t)s_;
+  AttnP p = {};
+  p.q = q; p.kv = img; p.vt = img; p.fcs = x; p.out = out; p.mo = mo; p.lse = lse;
+  p.B = BH; p.H = 1; p.Nc = Nc; p.Ns = Ns; p.ldk = 64;
+  p.prio = tuning().attn_prio;
+  p.ldt = (Ns + 63) / 64 * 64;
+  if (384LL * p.ldt >= (1LL << 31)) return fail("mhada_attn_train_fwd_split3: Ns too large for 32-bit plane offsets");
+  int nw = tuning().attn_waves;
+  if (nw == 0) nw = (long long)BH * ((Nc + 255) / 256) < s3_num_cus() ? 4 : 8;
+  p.nqb = (Nc + 32 * nw - 1) / (32 * nw);
+  const long long nblk = (long long)BH * p.nqb;
+  if (nblk > (1LL << 31) - 1) return fail("mhada_attn_train_fwd_split3: grid too large");
+  p.nblk = (int)nblk;
+  hipLaunchKernelGGL(train_s3_prep_kernel, dim3(p.ldt / 64, BH), dim3(256), 0, s, k, v, reinterpret_cast<bf16*>(img),
+                     Ns, p.ldt);
+  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, true>), dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((attn_s3_kernel<4, true>), dim3(p.nblk), dim3(256), 0, s, p);
+  return check_launch("mhada_attn_train_fwd_split3");
 }

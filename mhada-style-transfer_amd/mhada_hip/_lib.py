@@ -77,6 +77,7 @@ SIGNATURES = {
     "mhada_attn_split3": (_I, [_vp] * 7 + [_I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
+    "mhada_attn_train_fwd_split3": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
     "mhada_transpose64": (_I, [_vp, _vp, _I, _I, _I, _vp]),
     "mhada_attn_train_bwd": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_attn_train_dkv": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),

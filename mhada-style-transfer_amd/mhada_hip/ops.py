@@ -621,7 +621,13 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     out = torch.empty_like(q)
     mo = torch.empty(BH, Nc, 128, device=q.device, dtype=torch.float32)
     lse = torch.empty(BH, Nc, device=q.device, dtype=torch.float32)
-    if TRAIN_FWD_VT:
+    if TRAIN_FWD_S3:
+        # SPLIT3 products on the bf16 MFMA (csrc/attn_split3.hip) over a bf16 plane image of k, v
+        # (workspace, freed after)
+        img = torch.empty(BH, 576 * ((Ns + 63) // 64 * 64), device=q.device, dtype=torch.bfloat16)
+        _call("mhada_attn_train_fwd_split3", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), img.data_ptr(), x.data_ptr(),
+              out.data_ptr(), mo.data_ptr(), lse.data_ptr(), BH, Nc, Ns)
+    elif TRAIN_FWD_VT:
         # the inference fp32 attention structure on a V'^T | V'^2^T image (workspace, freed after)
         vt = torch.empty(BH, 128, (Ns + 63) // 64 * 64, device=q.device, dtype=torch.float32)
         _call("mhada_attn_train_fwd_vt", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), vt.data_ptr(), x.data_ptr(),
@@ -632,7 +638,10 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     return out, mo, lse
 
 
-# attn_train_fwd: True = mhada_attn_train_fwd_vt (the default), False = the round-1 kernel (A/B, tests)
+# attn_train_fwd: TRAIN_FWD_S3 = the SPLIT3 kernel on the bf16 MFMA (round 6, the default); else
+# TRAIN_FWD_VT = mhada_attn_train_fwd_vt (the fp32-MFMA inference structure), False = the round-1
+# kernel (A/B, tests)
+TRAIN_FWD_S3 = True
 TRAIN_FWD_VT = True
 
 

@@ -207,15 +207,18 @@ def test_fused_block_under_autocast_runs_fp32_kernels():
     assert _rel(ys[1][1].double(), ys[0][1].double()) < 5e-2
 
 
-@pytest.mark.parametrize("vt", [True, False])
+@pytest.mark.parametrize("form", ["s3", "vt", "r1"])
 @pytest.mark.parametrize("BH,Nc,Ns,scale", [(2, 300, 700, 0.5), (3, 97, 33, 1.0), (1, 512, 4096, 0.35),
-                                            (2, 256, 130, 2.5)])
-def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, vt, BH, Nc, Ns, scale):
-    """Both training forwards — mhada_attn_train_fwd_vt (the inference fp32 structure: 64-key tiles,
-    lazy rescale, V'^T | V'^2^T image; the default) and the round-1 mhada_attn_train_fwd — against
-    fp64: out', [M' | E2'] and lse2 (exact although the running max is rescaled lazily), ragged
-    key tiles, peaky logits (scale 2.5: the max moves late and by a lot)."""
-    monkeypatch.setattr(ops, "TRAIN_FWD_VT", vt)
+                                            (2, 256, 130, 2.5), (2, 600, 1000, 4.0)])
+def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, form, BH, Nc, Ns, scale):
+    """The three training forwards — mhada_attn_train_fwd_split3 (SPLIT3 products on the bf16 MFMA,
+    fixed-shift softmax with the exact recompute, the default), mhada_attn_train_fwd_vt (the inference
+    fp32 structure: 64-key tiles, lazy rescale, V'^T | V'^2^T image) and the round-1
+    mhada_attn_train_fwd — against fp64: out', [M' | E2'] and lse2 (exact whether the running max is
+    rescaled lazily or fixed to the first tile's), ragged key tiles, peaky logits (scale 2.5 / 4: the
+    max moves late and by a lot — for the fixed shift past 2^64, so rows are recomputed exactly)."""
+    monkeypatch.setattr(ops, "TRAIN_FWD_S3", form == "s3")
+    monkeypatch.setattr(ops, "TRAIN_FWD_VT", form == "vt")
     g = torch.Generator().manual_seed(BH * 100 + Ns)
     q = torch.randn(BH, Nc, 64, generator=g) * scale
     k = torch.randn(BH, Ns, 64, generator=g) * scale
