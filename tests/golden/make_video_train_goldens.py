@@ -30,7 +30,12 @@ from make_video_goldens import smooth_flow  # noqa: E402
 from mhada_hip.recipe import load_recipe, seeded_image  # noqa: E402
 
 
-def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2"):
+def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2", f64=False):
+    """f64: the same composition with the trained modules (ViTs, AdaFormer) and inputs in float64 —
+    VGG19 stays fp32, its reference forward casts to float; its gradient norms are added to the fp32
+    golden as grad_*_f64 — the yardstick for how far an fp32 evaluation of this step may land from
+    the fp32 reference (near-degenerate attention rows make E2' - M'^2 cancel, and sqrt's gradient
+    1/(2 S) amplifies that)."""
     torch.set_num_threads(8)
     R = load_reference()
     U, L = R["utilities"], R["lossfn"]
@@ -56,6 +61,12 @@ def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2"):
     # [B][H][W] as the data loader yields it: forward/backward consistency of a noisy inverse flow
     mask = torch.stack([U.flow_warp_mask(flow[b], -flow[b] + 1.0 * torch.randn(2, H, W, generator=g))
                         for b in range(B)])
+    if f64:
+        # the trained modules in float64; VGG19 stays fp32 (network/vgg19.py:6-12 casts its input to
+        # float, so the reference cannot run it in float64) and so do the loss attentions on its features
+        for m in (vit_c, vit_s, ada):
+            m.double()
+        style, c1, c2, flow, mask = (t.double() for t in (style, c1, c2, flow, mask))
 
     # train_video.py:110-166
     vitc_fc1 = vit_c(c1)
@@ -93,6 +104,15 @@ def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2"):
     loss = loss_gs + loss_lf + loss_ot + loss_ft + loss_id1 + loss_id2
     loss.backward()
 
+    path = os.path.join(HERE, name + ".npz")
+    if f64:
+        old = dict(np.load(path))
+        for n, m in (("vit_c", vit_c), ("vit_s", vit_s), ("ada", ada)):
+            old[f"grad_{n}_f64"] = grad_summary(m)
+        old["losses_f64"] = np.array([float(v) for v in (loss_gs, loss_lf, loss_ot, loss_ft, loss_id1, loss_id2, loss)])
+        np.savez_compressed(path, **old)
+        print(f"added the float64 gradient norms to {path}")
+        return
     out = {
         "seeds": np.array([201, 202, 203]), "flow": np32(flow), "mask": np32(mask),
         "frame_shape": np.array([H, W]), "style_shape": np.array([Hs, Ws]),
@@ -100,11 +120,11 @@ def main(H=64, W=64, Hs=64, Ws=64, name="train_video_64_b2"):
         "grad_vit_c": grad_summary(vit_c), "grad_vit_s": grad_summary(vit_s), "grad_ada": grad_summary(ada),
         "grad_ada_last_conv_w": np32(ada.decoder.conv3[1].conv.conv.weight.grad),
     }
-    path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
     print(f"wrote {path}: losses {out['losses']}, mask mean {float(mask.mean()):.3f}")
 
 
 if __name__ == "__main__":
-    main()
-    main(64, 128, 64, 64, "train_video_64x128_s64_b2")
+    for args in ((64, 64, 64, 64, "train_video_64_b2"), (64, 128, 64, 64, "train_video_64x128_s64_b2")):
+        main(*args)
+        main(*args, f64=True)

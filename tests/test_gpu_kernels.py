@@ -875,13 +875,13 @@ def test_kv_proj_split3_matches_projection_then_split(B, H, Ns):
         vp = im[..., 192 * ldt:].view(B, H, 3, 128, ldt).double().sum(2)
         return kp, vp
     (k1, v1), (k2, v2) = sums(img), sums(ref)
-    assert torch.all(k1[:, :, Ns:] == 0) and torch.all(v1[..., Ns:] == 0)
+    pos = torch.arange(ldt, device=DEV)
+    key = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1)  # the key at each (permuted) position
+    assert torch.all(k1[:, :, Ns:] == 0) and torch.all(v1[..., key >= Ns] == 0)
     assert rel(k1, k2) < 1e-6 and rel(v1, v2) < 1e-6
     y = torch.einsum("bnhc,bhoc->bhno", (fs.double() - mu.double()[:, None]).view(B, Ns, H, 64), w.double()) + \
         bkv.double()[None, :, None, :]
     assert rel(k1[:, :, :Ns], y[..., :64]) < 1e-6
-    pos = torch.arange(ldt, device=DEV)
-    key = (pos & ~12) | ((pos & 4) << 1) | ((pos & 8) >> 1)
     vref = torch.zeros(B, H, 128, ldt, device=DEV, dtype=torch.float64)
     vref[..., :Ns] = torch.cat([y[..., 64:], y[..., 64:] ** 2], -1).transpose(-1, -2)
     assert rel(v1, vref[..., key]) < 2e-6

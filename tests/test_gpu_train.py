@@ -23,6 +23,7 @@ def test_video_train_step_matches_reference_golden_gpu(name):
     check_video_against_golden(VideoTrainer(*build("cuda")), "cuda", name)
 
 
+
 def test_train_step_256_b2_losses_match_oracle_and_grads_match_cpu():
     """One train_image.py step at 256^2, batch 2 (16x the golden's pixels; every VGG / loss-attention
     level is non-trivial): the five loss terms against the numpy oracle's restatement of
