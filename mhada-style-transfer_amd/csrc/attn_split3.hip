@@ -528,11 +528,13 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
       Cm[qg] = f32x4{-m, -m, -m, -m};
     }
   }
-  if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if (NTILE > 1) stage(TK, 1);
   finish(0, Sa);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  // Measured and not kept (profiles/r06_attn_s3_order_prio_ab.log): Q K^T and P V interleaved per
+  // 32-key group (all waves or the younger half, so that the softmax VALU bursts of the two waves of a
+  // SIMD fall apart) within +-1 %; s_setprio(1) for the younger half 1.5-4 % slower than none.
   for (int t = 1; t < NFULL; ++t) {
     if (t + 1 < NTILE) stage((t + 1) * TK, (t + 1) & 1);
     qk(t & 1, Sa, Cm);
@@ -599,7 +601,6 @@ extern "C" int mhada_attn_split3(const float* q, const void* img, const float* f
   AttnP p = {};
   p.q = q; p.kv = img; p.vt = img; p.fcs = fcs; p.fcs_mu = fcs_mu; p.fcs_rstd = fcs_rstd; p.v_mu = v_mu;
   p.out = out; p.B = B; p.H = H; p.Nc = Nc; p.Ns = Ns;
-  p.prio = tuning().attn_prio;
   p.ldt = (Ns + 63) / 64 * 64;
   if (384LL * p.ldt >= (1LL << 31)) return fail("mhada_attn_split3: Ns too large for 32-bit plane offsets");
   // waves per block as mhada_attn: tuning attn_waves, 0 = 8, or 4 when the 8-wave grid has fewer
@@ -629,7 +630,6 @@ extern "C" int mhada_attn_train_fwd_split3(const float* q, const float* k, const
   AttnP p = {};
   p.q = q; p.kv = img; p.vt = img; p.fcs = x; p.out = out; p.mo = mo; p.lse = lse;
   p.B = BH; p.H = 1; p.Nc = Nc; p.Ns = Ns; p.ldk = 64;
-  p.prio = tuning().attn_prio;
   p.ldt = (Ns + 63) / 64 * 64;
   if (384LL * p.ldt >= (1LL << 31)) return fail("mhada_attn_train_fwd_split3: Ns too large for 32-bit plane offsets");
   int nw = tuning().attn_waves;

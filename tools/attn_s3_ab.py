@@ -4,6 +4,7 @@ interleaved rounds, median of rounds, at the bench shapes.  Also the one-time pl
 (mhada_split3_kv) and each kernel's error against fp64 on a row subset.
 
     python tools/attn_s3_ab.py [waves...]      (waves: 0 = auto, 4, 8)
+    S3_VARIANTS="base: inter:xknob=1 noprio:attn_prio=0" python tools/attn_s3_ab.py   (tuning A/B)
 """
 import math
 import os
@@ -54,6 +55,10 @@ def ref_rows(q, kv, fcs, mu, rs, vmu, rows):
 
 def main():
     waves = [int(x) for x in sys.argv[1:]] or [0]
+    variants = []
+    for item in os.environ.get("S3_VARIANTS", "base:").split():
+        name, _, kv = item.partition(":")
+        variants.append((name, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
     torch.manual_seed(0)
     H = 8
     for name, B, nc, ns in SHAPES:
@@ -73,14 +78,15 @@ def main():
         tsp = timeit(lambda: ops.split3_kv(kv, vt))
         line = f"{name:18s} f32 {t32:.3f} ms {fl / t32 / 1e9:.1f} TF (err {e32:.2e}) | split3_kv {tsp * 1e3:.1f} us"
         for w in waves:
-            with _lib.tuning(attn_waves=w):
-                y = ops.attn_split3(q, img, ns, fcs, mu, rs, vmu)
-                es = ((y[:, rows].double() - ref).norm() / ref.norm()).item()
-                ts = timeit(lambda: ops.attn_split3(q, img, ns, fcs, mu, rs, vmu))
-            # bf16 MFMA FLOP per (query, key, head): 6 x 128 (QK) + 6 x 256 (PV) + 3 x 32 (row sum)
-            mf = fl / 384 * (6 * 128 + 6 * 256 + 96) / 1e9  # GFLOP
-            line += (f" | s3 w{w} {ts:.3f} ms {fl / ts / 1e9:.1f} TF-fp32eq, bf16 pipe {mf / ts:.0f} TF ="
-                     f" {mf / ts / 2500:.3f} (err {es:.2e}) x{t32 / ts:.2f}")
+            for vname, knobs in variants:
+                with _lib.tuning(attn_waves=w, **knobs):
+                    y = ops.attn_split3(q, img, ns, fcs, mu, rs, vmu)
+                    es = ((y[:, rows].double() - ref).norm() / ref.norm()).item()
+                    ts = timeit(lambda: ops.attn_split3(q, img, ns, fcs, mu, rs, vmu))
+                # bf16 MFMA FLOP per (query, key, head): 6 x 128 (QK) + 6 x 256 (PV) + 3 x 32 (row sum)
+                mf = fl / 384 * (6 * 128 + 6 * 256 + 96) / 1e9  # GFLOP
+                line += (f" | s3 {vname} w{w} {ts:.3f} ms {fl / ts / 1e9:.1f} TF-fp32eq, bf16 pipe {mf / ts:.0f} TF ="
+                         f" {mf / ts / 2500:.3f} (err {es:.2e}) x{t32 / ts:.2f}")
         print(line, flush=True)
 
 
