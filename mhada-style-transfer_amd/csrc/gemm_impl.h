@@ -126,8 +126,9 @@ constexpr int kRowsCentred = 100;
 // an fp32 matrix (8 + 8 + 8 mantissa bits), the GEMM's K = 6 K0 is virtual: K-tile 6 kk + t reads
 // columns 64 kk .. of plane kSplitPlanes[t] = 1, 2, 0, 1, 0, 0, and W holds the matching [N][6 K0]
 // interleave (chunk kk of q1, q0, q2, q0, q1, q0), so the fp32 accumulators sum p1 q1 + p2 q0 +
-// p0 q2 + p1 q0 + p0 q1 + p0 q0 chunk by chunk — the six cross products above 2^-24 (the three
-// dropped are < 2^-32).
+// p0 q2 + p1 q0 + p0 q1 + p0 q0 chunk by chunk: every cross product p_i q_j with i + j <= 2.  With
+// round-to-nearest planes |p1| <= 2^-8 |x|, |p2| <= 2^-16 |x| (likewise q), so the three dropped
+// terms are below 2^-24 |x w| (p1 q2 and p2 q1) and 2^-32 |x w| (p2 q2) per product.
 constexpr int kRowsSplit3 = 101;
 constexpr int kSplitPlanes = 0x001021;  // nibble t = plane of K-block t
 

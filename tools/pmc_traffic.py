@@ -19,11 +19,15 @@ from bench import attn_source_sha  # noqa: E402
 CONFIGS = {"512x512_b8_f32": 8 * 8 * (4096 // 256) * 512, "1024x1024_b4_bf16": 4 * 8 * (16384 // 256) * 512}
 
 
+NAMES = {}  # grid size -> the attention kernel's name (attn_s3_kernel for the fp32 SPLIT3 path, round 6)
+
+
 def load(fn, counter):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(fn)):
         if "attn_" in r["Kernel_Name"] and "vit" not in r["Kernel_Name"] and r["Counter_Name"] == counter:
             d[int(r["Grid_Size"])].append(float(r["Counter_Value"]))
+            NAMES[int(r["Grid_Size"])] = r["Kernel_Name"].split("(")[0].replace("void ", "")
     return d
 
 
@@ -36,7 +40,7 @@ def main():
             continue
         fetch = 2.0 * 1024 * sum(f[grid]) / len(f[grid])
         write = 1024.0 * sum(w[grid]) / len(w[grid])
-        out[name] = {"kernel": "mhada_attn", "launches": len(f[grid]), "fetch_bytes_corrected": fetch,
+        out[name] = {"kernel": NAMES.get(grid, "mhada_attn"), "launches": len(f[grid]), "fetch_bytes_corrected": fetch,
                      "write_bytes": write, "traffic_bytes_per_launch": fetch + write,
                      "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; separate --pmc passes"}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
