@@ -108,7 +108,7 @@ typedef struct mhada_gemm_args {
   const float* bias; long long sb1, sb2;
   const void* r; int r_dtype; long long ldr, sr1, sr2;
   void* c; int c_dtype; long long ldc, sc1, sc2;
-  /* 1: ReLU after the bias (before a residual).  2 (ABI 10): ReLU-adjoint mask — r is not added
+  /* 1: ReLU after the bias (before a residual).  2 (ABI 10; SPLIT3 too since ABI 16): ReLU-adjoint mask — r is not added
    * but read as a mask of C's layout: C = 0 where r <= 0 (a gradient GEMM whose input was a ReLU
    * output consumed only by the forward of this layer; fp32 C and r, ROWS mode). */
   int relu;
@@ -205,6 +205,10 @@ int mhada_attn(const void* q, const void* kv, const void* vt, const float* fcs,
  * mhada_attn_split3: q fp32 [B][H][Nc][64] (split on load) and img -> out fp32 [B][Nc][64H]; the other
  *   arguments as mhada_attn. */
 int mhada_split3_kv(const float* kv, const float* vt, void* img, int B, int H, int Ns, mhada_stream_t stream);
+/* x fp32 [n] -> planes bf16 [3][n]: p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 - p1) (the
+ * MHADA_A_SPLIT3 operand of any fp32 matrix, e.g. the training step's activations and gradients;
+ * ABI 16).  n % 4 == 0 and n * 2 % 16 == 0, 16-byte aligned pointers. */
+int mhada_split3_rows(const float* x, void* planes, long long n, mhada_stream_t stream);
 /* The block's K|V' projection written straight as that plane image (the engine's fp32 softmax path:
  * replaces mhada_gemm with the vt epilogue plus mhada_split3_kv, adaDecoder.py:178,182):
  *   Y[n][o] = sum_c (fs[b][n][64h+c] - mu_s[b][64h+c]) wkv[b][h][o][c] + bkv[h][o]  (fp32 MFMA),

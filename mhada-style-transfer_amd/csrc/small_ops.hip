@@ -786,6 +786,26 @@ __global__ void __launch_bounds__(256) upsample2x_vec_kernel(const T* __restrict
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// fp32 [n] -> three bf16 planes [3][n] (p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 - p1), the
+// SPLIT3 GEMM operand); four elements per thread, n % 4 == 0, 16-B aligned.
+__global__ void __launch_bounds__(256) split3_rows_kernel(const float* __restrict__ x, bf16* __restrict__ y,
+                                                          long long n) {
+  const long long i = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (i >= n) return;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+  bf16x4 a, b, c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = (bf16)v[e];
+    const float r = v[e] - (float)a[e];
+    b[e] = (bf16)r;
+    c[e] = (bf16)(r - (float)b[e]);
+  }
+  *reinterpret_cast<bf16x4*>(y + i) = a;
+  *reinterpret_cast<bf16x4*>(y + n + i) = b;
+  *reinterpret_cast<bf16x4*>(y + 2 * n + i) = c;
+}
+
 }  // namespace mhada
 
 using namespace mhada;
@@ -1111,4 +1131,14 @@ extern "C" int mhada_upsample2x(const void* x, void* y, int dtype, int B, int H,
     hipLaunchKernelGGL((upsample2x_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)s_, (const bf16*)x, (bf16*)y, B,
                        H, W, C);
   return check_launch("mhada_upsample2x");
+}
+
+extern "C" int mhada_split3_rows(const float* x, void* planes, long long n, mhada_stream_t s_) {
+  if (!x || !planes || n < 0 || n % 4) return fail("mhada_split3_rows: bad args (n % 4 == 0)");
+  if (!aligned16(x) || !aligned16(planes) || (n * 2) % 16) return fail("mhada_split3_rows: 16-byte aligned operands");
+  if (n == 0) return MHADA_OK;
+  const long long nb = (n / 4 + 255) / 256;
+  if (nb > 0x7fffffffLL) return fail("mhada_split3_rows: too large");
+  hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)s_, x, (bf16*)planes, n);
+  return check_launch("mhada_split3_rows");
 }

@@ -330,13 +330,25 @@ def split3_weight(w: torch.Tensor) -> torch.Tensor:
     return terms.reshape(N, 6 * K0).contiguous()
 
 
+def split3_rows(x: torch.Tensor) -> torch.Tensor:
+    """``mhada_split3_rows``: a contiguous fp32 matrix [M][K0] as its three bf16 planes [3][M][K0] (the
+    ``linear_split3`` A operand of an activation or gradient that no LayerNorm produced)."""
+    _need_gpu(x)
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 2:
+        raise ValueError("split3_rows needs a contiguous float32 [M][K0] matrix")
+    y = torch.empty(3, *x.shape, device=x.device, dtype=torch.bfloat16)
+    _call("mhada_split3_rows", x, x.data_ptr(), y.data_ptr(), x.numel())
+    return y
+
+
 def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
                   residual: Optional[torch.Tensor] = None, relu: bool = False,
-                  out_planes: bool = False) -> torch.Tensor:
+                  out_planes: bool = False, relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp32-accurate x @ w^T (+bias, relu, residual) from x's bf16 planes [3][M][K0] and
     ``split3_weight(w)`` [N][6 K0]: the six significant cross products summed in fp32 accumulators
     on the bf16 MFMA (mhada_gemm MHADA_A_SPLIT3).  ``out_planes``: return the fp32 result as its
-    three bf16 planes [3][M][N] (the next SPLIT3 GEMM's operand) instead of an fp32 [M][N]."""
+    three bf16 planes [3][M][N] (the next SPLIT3 GEMM's operand) instead of an fp32 [M][N].
+    ``relu_mask`` (fp32 [M][N], as ``linear``'s): the result zeroed where relu_mask <= 0."""
     if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_contiguous():
         raise ValueError("linear_split3: planes must be contiguous bf16 [3][M][K0]")
     _, M, K0 = planes.shape
@@ -351,6 +363,12 @@ def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.T
                     ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu,
                     c2=c2, ldc2=N, c2_planes=True)
     c = torch.empty(M, N, device=planes.device, dtype=out_dtype)
+    if relu_mask is not None:
+        if residual is not None or relu or out_dtype != torch.float32 or relu_mask.dtype != torch.float32 \
+                or relu_mask.shape != (M, N) or not relu_mask.is_contiguous():
+            raise ValueError("linear_split3: relu_mask needs fp32 output, a contiguous fp32 [M][N] mask, no residual / relu")
+        return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
+                    ldw=6 * K0, bias=bias, r=relu_mask, ldr=N, ldc=N, relu=2)
     return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
                 ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)
 

@@ -170,10 +170,39 @@ class Conv3x3Fn(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None
 
 
+# The training linears' forward and input-gradient GEMMs as SPLIT3 products on the bf16 MFMA (round 6):
+# fp32-accurate (ops.linear_split3; against fp64 at or below the fp32-MFMA GEMM's error without a
+# residual, <= 1.75x with one, tests/test_gpu_kernels.py) where the 256 x 256 tiles fill the chip
+# (engine._split3_fills); the operand is split by one mhada_split3_rows pass, the weights once per
+# parameter version.  False: the fp32-MFMA GEMMs.
+TRAIN_SPLIT3 = True
+
+
+def _split3_w(weight: torch.Tensor, transposed: bool) -> torch.Tensor:
+    """ops.split3_weight of W (forward, [N][6 K0]) or of W^T (input gradient, [K0][6 N]), cached per
+    weight tensor (_pack_slot) and rebuilt when its version changes (every optimizer step)."""
+    cache = _pack_slot(weight)
+    key = ("s3t",) if transposed else ("s3",)
+    hit = cache.get(key)
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    with torch.no_grad():
+        w = weight.detach().float()
+        w6 = ops.split3_weight(w.t().contiguous() if transposed else w.contiguous())
+    cache[key] = (weight._version, w6)
+    return w6
+
+
+def _split3_ok(M: int, N: int, K0: int, dev: torch.device) -> bool:
+    from .engine import _split3_fills
+    return TRAIN_SPLIT3 and N > 128 and K0 % 64 == 0 and _split3_fills(M, N, dev)
+
+
 class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) (+ residual) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear
     layout).  ``residual`` [M][N] (no ReLU with it): the add of a residual stream fused into the
-    GEMM epilogue (the reference's ``t + f(t)``); its gradient is gy itself."""
+    GEMM epilogue (the reference's ``t + f(t)``); its gradient is gy itself.  Forward and input
+    gradient run as SPLIT3 GEMMs where TRAIN_SPLIT3 and the shape allow (_split3_ok)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, relu: bool, grad_masked: bool = False, relu_input: bool = False,
@@ -181,8 +210,14 @@ class LinearFn(torch.autograd.Function):
         x = x.contiguous()
         if residual is not None and relu:
             raise ValueError("LinearFn: a fused residual follows a ReLU-free linear")
-        y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu,
-                       residual=None if residual is None else residual.detach().contiguous())
+        M, K0 = x.shape
+        N = weight.shape[0]
+        res = None if residual is None else residual.detach().contiguous()
+        if x.dtype == torch.float32 and _split3_ok(M, N, K0, x.device):
+            y = ops.linear_split3(ops.split3_rows(x), _split3_w(weight, False), bias.detach().contiguous(), F32,
+                                  residual=res, relu=relu)
+        else:
+            y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu, residual=res)
         ctx.save_for_backward(x, weight, y if (relu and not grad_masked) else None)
         # grad_masked: y's only consumer is a LinearFn(relu_input=True), whose input-gradient GEMM
         # applies this ReLU's adjoint in its epilogue (mhada_gemm relu = 2): no relu_bwd pass here
@@ -197,7 +232,13 @@ class LinearFn(torch.autograd.Function):
             g = ops.relu_bwd(g, y)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = ops.linear(g, weight.detach().t().contiguous(), None, F32, relu_mask=x if ctx.relu_input else None)
+            M, N = g.shape
+            K0 = weight.shape[1]
+            if _split3_ok(M, K0, N, g.device):
+                gx = ops.linear_split3(ops.split3_rows(g), _split3_w(weight, True), None, F32,
+                                       relu_mask=x if ctx.relu_input else None)
+            else:
+                gx = ops.linear(g, weight.detach().t().contiguous(), None, F32, relu_mask=x if ctx.relu_input else None)
         if ctx.needs_input_grad[1]:
             M, N = g.shape
             gw, cs = ops.gemm_tn(g, x, M=N, N=x.shape[1], K=M, lda=N, ldb=x.shape[1], b_mode=A_ROWS, colsum=True)

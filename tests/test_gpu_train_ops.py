@@ -351,6 +351,74 @@ def test_linear_fn_fused_residual(M, K, N):
         assert rel(a, b_) < 1e-5
 
 
+@pytest.mark.parametrize("M,K,N,mode", [(32768, 512, 1536, "plain"), (32768, 512, 2048, "relu"), (32768, 2048, 512, "residual"),
+                                         (65536, 512, 512, "residual"), (40000, 512, 2048, "mlp_fold")])
+def test_linear_fn_split3_vs_fp64(monkeypatch, M, K, N, mode):
+    """LinearFn at the 512^2 training shapes, where its forward and input-gradient GEMMs run as SPLIT3
+    products (train_fns.TRAIN_SPLIT3, round 6): output and all gradients against fp64 autograd at an
+    fp32-class error (< 2e-6) and within 1.75x of the fp32-MFMA GEMMs' error (TRAIN_SPLIT3 = False) on
+    the same operands; ReLU, a fused residual, and the MLP pair with its ReLU adjoint folded into the
+    second layer's input-gradient epilogue (relu = 2 on the SPLIT3 kernel), bit-identical to the
+    unfolded pair."""
+    from mhada_hip.engine import _split3_fills
+    assert _split3_fills(M, min(N, K), torch.device(DEV))  # the shapes take the SPLIT3 path
+    errs = {}
+    for s3 in (True, False):
+        monkeypatch.setattr(train_fns, "TRAIN_SPLIT3", s3)
+        x = rnd(M, K, seed=21).requires_grad_(True)
+        w = rnd(N, K, seed=22, scale=K ** -0.5).requires_grad_(True)
+        b = rnd(N, seed=23, scale=0.1).requires_grad_(True)
+        gy = rnd(M, N if mode != "mlp_fold" else K, seed=24)
+        ps = [x, w, b]
+        if mode == "mlp_fold":
+            w2 = rnd(K, N, seed=25, scale=N ** -0.5).requires_grad_(True)
+            b2 = rnd(K, seed=26, scale=0.1).requires_grad_(True)
+            ps += [w2, b2]
+            grads = []
+            for fold in (True, False):
+                for t in ps:
+                    t.grad = None
+                h = train_fns.linear(x, w, b, relu=True, grad_masked=fold)
+                y = train_fns.linear(h, w2, b2, relu_input=fold)
+                y.backward(gy)
+                grads.append([t.grad.clone() for t in ps])
+            for a, c in zip(*grads):
+                assert torch.equal(a, c)
+        elif mode == "residual":
+            r = rnd(M, N, seed=27).requires_grad_(True)
+            ps.append(r)
+            y = train_fns.linear(x, w, b, residual=r)
+            y.backward(gy)
+        else:
+            y = train_fns.linear(x, w, b, relu=(mode == "relu"))
+            y.backward(gy)
+        p64 = [t.detach().double().requires_grad_(True) for t in ps]
+        if mode == "mlp_fold":
+            ref = F.linear(F.relu(F.linear(p64[0], p64[1], p64[2])), p64[3], p64[4])
+        elif mode == "residual":
+            ref = F.linear(p64[0], p64[1], p64[2]) + p64[3]
+        else:
+            ref = F.linear(p64[0], p64[1], p64[2])
+            if mode == "relu":
+                ref = F.relu(ref)
+        ref.backward(gy.double())
+        errs[s3] = [rel(y, ref)] + [rel(t.grad, t64.grad) for t, t64 in zip(ps, p64)]
+    for e3, e32 in zip(errs[True], errs[False]):
+        assert e3 < 2e-6 and e3 <= 1.75 * e32 + 1e-8, (errs[True], errs[False])
+
+
+def test_split3_rows_planes_are_exact():
+    """mhada_split3_rows: plane 0 is the bf16 rounding, each plane the rounding of what the planes before
+    leave, and the three sum to the fp32 input exactly."""
+    x = rnd(1000, 384, seed=31) * 7
+    pl = ops.split3_rows(x)
+    assert pl.shape == (3, 1000, 384) and pl.dtype == torch.bfloat16
+    assert torch.equal(pl[0], x.bfloat16())
+    r1 = x.double() - pl[0].double()
+    assert torch.equal(pl[1], r1.float().bfloat16())
+    assert torch.equal(pl[0].double() + pl[1].double() + pl[2].double(), x.double())
+
+
 @pytest.mark.parametrize("B,H,W,C", [(2, 5, 7, 64), (3, 33, 20, 128), (1, 1, 2, 4), (2, 64, 64, 512), (8, 128, 128, 64),
                                      (2, 1, 1, 8)])
 def test_feat_stats_vs_fp64(B, H, W, C):
