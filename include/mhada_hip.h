@@ -209,6 +209,11 @@ int mhada_split3_kv(const float* kv, const float* vt, void* img, int B, int H, i
  * MHADA_A_SPLIT3 operand of any fp32 matrix, e.g. the training step's activations and gradients;
  * ABI 16).  n % 4 == 0 and n * 2 % 16 == 0, 16-byte aligned pointers. */
 int mhada_split3_rows(const float* x, void* planes, long long n, mhada_stream_t stream);
+/* The SPLIT3 GEMM's weight operand in one launch (ABI 16): W fp32 [N][K0] (transposed = 0) or the W
+ * of W^T (transposed = 1: w is [K0][N], the operand is W^T's [N][K0]) -> out bf16 [N][6 K0], per
+ * 64-column chunk the planes q1 | q0 | q2 | q0 | q1 | q0 (q0 = bf16(x), q1 = bf16(x - q0),
+ * q2 = bf16(x - q0 - q1)).  K0 % 64 == 0. */
+int mhada_split3_weight(const float* w, void* out, int N, int K0, int transposed, mhada_stream_t stream);
 /* The block's K|V' projection written straight as that plane image (the engine's fp32 softmax path:
  * replaces mhada_gemm with the vt epilogue plus mhada_split3_kv, adaDecoder.py:178,182):
  *   Y[n][o] = sum_c (fs[b][n][64h+c] - mu_s[b][64h+c]) wkv[b][h][o][c] + bkv[h][o]  (fp32 MFMA),

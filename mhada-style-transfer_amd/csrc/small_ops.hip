@@ -806,9 +806,39 @@ __global__ void __launch_bounds__(256) split3_rows_kernel(const float* __restric
   *reinterpret_cast<bf16x4*>(y + 2 * n + i) = c;
 }
 
+// The SPLIT3 GEMM's W operand in one pass: element (n, k) of W [N][K0] (or of W^T when
+// transposed, W then [K0][N]) -> its planes q0, q1, q2 at out[n][(6 (k / 64) + t) 64 + k % 64] for the
+// term order t = q1, q0, q2, q0, q1, q0 (ops.split3_weight's layout).  One thread per element.
+__global__ void __launch_bounds__(256) split3_weight_kernel(const float* __restrict__ w, bf16* __restrict__ out,
+                                                            int N, int K0, int transposed) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * K0) return;
+  const int n = (int)(i / K0), k = (int)(i - (long long)n * K0);
+  const float x = transposed ? w[(long long)k * N + n] : w[i];
+  const bf16 q0 = (bf16)x;
+  const float r = x - (float)q0;
+  const bf16 q1 = (bf16)r;
+  const bf16 q2 = (bf16)(r - (float)q1);
+  bf16* o = out + (long long)n * 6 * K0 + 6 * 64 * (k >> 6) + (k & 63);
+  o[0] = q1;
+  o[64] = q0;
+  o[128] = q2;
+  o[192] = q0;
+  o[256] = q1;
+  o[320] = q0;
+}
+
 }  // namespace mhada
 
 using namespace mhada;
+
+extern "C" int mhada_split3_weight(const float* w, void* out, int N, int K0, int transposed, mhada_stream_t s_) {
+  if (!w || !out || N <= 0 || K0 <= 0 || K0 % 64) return fail("mhada_split3_weight: bad args (K0 % 64 == 0)");
+  const long long n = (long long)N * K0;
+  hipLaunchKernelGGL(split3_weight_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s_, w,
+                     (bf16*)out, N, K0, transposed);
+  return check_launch("mhada_split3_weight");
+}
 
 extern "C" int mhada_layernorm(const float* x, void* y, int y_dtype, const float* gamma, const float* beta,
                                int rows, int cols, float eps, mhada_stream_t s_) {

@@ -75,6 +75,7 @@ SIGNATURES = {
     "mhada_split3_kv": (_I, [_vp, _vp, _vp, _I, _I, _I, _vp]),
     "mhada_kv_proj_split3": (_I, [_vp] * 5 + [_I, _I, _I, _vp]),
     "mhada_split3_rows": (_I, [_vp, _vp, _c_ll, _vp]),
+    "mhada_split3_weight": (_I, [_vp, _vp, _I, _I, _I, _vp]),
     "mhada_attn_split3": (_I, [_vp] * 7 + [_I, _I, _I, _I, _vp]),
     "mhada_attn_train_fwd": (_I, [_vp] * 7 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),

@@ -330,6 +330,20 @@ def split3_weight(w: torch.Tensor) -> torch.Tensor:
     return terms.reshape(N, 6 * K0).contiguous()
 
 
+def split3_weight_dev(w: torch.Tensor, transposed: bool = False) -> torch.Tensor:
+    """``mhada_split3_weight``: split3_weight(w) (or of w.t()) in one device launch, bit-identical to
+    split3_weight — the training step re-splits its weights after every optimizer step."""
+    _need_gpu(w)
+    if w.dtype != torch.float32 or not w.is_contiguous() or w.dim() != 2:
+        raise ValueError("split3_weight_dev needs a contiguous float32 matrix")
+    N, K0 = (w.shape[1], w.shape[0]) if transposed else w.shape
+    if K0 % 64:
+        raise ValueError("split3_weight_dev: K0 must be a multiple of 64")
+    out = torch.empty(N, 6 * K0, device=w.device, dtype=torch.bfloat16)
+    _call("mhada_split3_weight", w, w.data_ptr(), out.data_ptr(), N, K0, int(transposed))
+    return out
+
+
 def split3_rows(x: torch.Tensor) -> torch.Tensor:
     """``mhada_split3_rows``: a contiguous fp32 matrix [M][K0] as its three bf16 planes [3][M][K0] (the
     ``linear_split3`` A operand of an activation or gradient that no LayerNorm produced)."""

@@ -186,9 +186,7 @@ def _split3_w(weight: torch.Tensor, transposed: bool) -> torch.Tensor:
     hit = cache.get(key)
     if hit is not None and hit[0] == weight._version:
         return hit[1]
-    with torch.no_grad():
-        w = weight.detach().float()
-        w6 = ops.split3_weight(w.t().contiguous() if transposed else w.contiguous())
+    w6 = ops.split3_weight_dev(weight.detach().contiguous(), transposed)
     cache[key] = (weight._version, w6)
     return w6
 

@@ -356,8 +356,9 @@ def test_linear_fn_fused_residual(M, K, N):
 def test_linear_fn_split3_vs_fp64(monkeypatch, M, K, N, mode):
     """LinearFn at the 512^2 training shapes, where its forward and input-gradient GEMMs run as SPLIT3
     products (train_fns.TRAIN_SPLIT3, round 6): output and all gradients against fp64 autograd at an
-    fp32-class error (< 2e-6) and within 1.75x of the fp32-MFMA GEMMs' error (TRAIN_SPLIT3 = False) on
-    the same operands; ReLU, a fused residual, and the MLP pair with its ReLU adjoint folded into the
+    fp32-class error (< 2e-6, or 1.25x the fp32 path's where ReLU mask flips dominate) and within 1.75x
+    of the fp32-MFMA GEMMs' error (TRAIN_SPLIT3 = False) on the same operands; ReLU, a fused residual,
+    and the MLP pair with its ReLU adjoint folded into the
     second layer's input-gradient epilogue (relu = 2 on the SPLIT3 kernel), bit-identical to the
     unfolded pair."""
     from mhada_hip.engine import _split3_fills
@@ -404,7 +405,20 @@ def test_linear_fn_split3_vs_fp64(monkeypatch, M, K, N, mode):
         ref.backward(gy.double())
         errs[s3] = [rel(y, ref)] + [rel(t.grad, t64.grad) for t, t64 in zip(ps, p64)]
     for e3, e32 in zip(errs[True], errs[False]):
-        assert e3 < 2e-6 and e3 <= 1.75 * e32 + 1e-8, (errs[True], errs[False])
+        # behind a ReLU the gradients carry the mask flips of outputs within rounding of 0 (any fp32
+        # evaluation against fp64: ~3e-4 here), so the absolute bound is relative to the fp32 path's
+        assert e3 < max(2e-6, 1.25 * e32) and e3 <= 1.75 * e32 + 1e-8, (errs[True], errs[False])
+
+
+@pytest.mark.parametrize("N,K0", [(1536, 512), (512, 2048), (700, 64)])
+def test_split3_weight_dev_matches_host_split(N, K0):
+    """mhada_split3_weight (the training step's per-step weight split) is bit-identical to
+    ops.split3_weight, for W and for W^T."""
+    w = rnd(N, K0, seed=5)
+    assert torch.equal(ops.split3_weight_dev(w), ops.split3_weight(w))
+    wt = rnd(K0, N, seed=6)
+    if N % 64 == 0:
+        assert torch.equal(ops.split3_weight_dev(wt, transposed=True), ops.split3_weight(wt.t().contiguous()))
 
 
 def test_split3_rows_planes_are_exact():
