@@ -209,8 +209,10 @@ MHADA_DEV f32x4 mfma6(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, cons
 
 // Exact two-pass recompute of one wave's 2 x 16 queries (the rare path when a row sum trips
 // kShiftSumThr): the true row max over all keys, then the full pass, planes read from L2.
+template <bool QK32>
 MHADA_DEV void attn_exact_q3(const AttnP& p, const bf16* kp, const bf16* vp, const bf16x8 (&qf)[3][2][2],
-                             f32x4 (&O)[2][8], float (&lt)[2], float (&mx)[2], int g, int r16) {
+                             const float (&qreg)[2][16], f32x4 (&O)[2][8], float (&lt)[2], float (&mx)[2], int g,
+                             int r16) {
   const int Ns = p.Ns;
   const long long kps = 64LL * p.ldt, vps = 128LL * p.ldt;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
@@ -220,8 +222,15 @@ MHADA_DEV void attn_exact_q3(const AttnP& p, const bf16* kp, const bf16* vp, con
       const bf16* kr = kp + (long long)(k0 + fsq_key(r16, t)) * 64 + 8 * g;  // k0 + 31 < ldt
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg) S[qg][t] = z4;
+      if constexpr (QK32) {  // fp32 K rows, d permuted to 16 g + s
+        const float* kf = reinterpret_cast<const float*>(kp) + (long long)(k0 + fsq_key(r16, t)) * 64 + 16 * g;
 #pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
+        for (int st = 0; st < 16; ++st)
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg) S[qg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[st], qreg[qg][st], S[qg][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int dh = 0; dh < (QK32 ? 0 : 2); ++dh) {
         const bf16x8 k0f = *reinterpret_cast<const bf16x8*>(kr + 32 * dh);
         const bf16x8 k1f = *reinterpret_cast<const bf16x8*>(kr + kps + 32 * dh);
         const bf16x8 k2f = *reinterpret_cast<const bf16x8*>(kr + 2 * kps + 32 * dh);
@@ -295,8 +304,9 @@ MHADA_DEV void s3_mask(f32x4 (&S)[2][2][2], int key0, int Ns, int g) {
 }
 
 // Training forward (mhada_attn_train_fwd_split3): k [BH][Ns][64] and the centred v [BH][Ns][64] rows
-// of the training attention -> the plane image (K planes from k; V'^T | V'^2^T planes from v, its fp32
-// square, key positions permuted as split3_kv_kernel's).  One workgroup per (64 keys, b h).
+// of the training attention -> the QK32 image: fp32 K rows [ldt][64] (d = 4 s + g at 16 g + s; in the
+// K-plane region) and the V'^T | V'^2^T planes from v (its fp32 square, key positions permuted as
+// split3_kv_kernel's).  One workgroup per (64 keys, b h).
 __global__ void __launch_bounds__(256) train_s3_prep_kernel(const float* __restrict__ k, const float* __restrict__ v,
                                                             bf16* __restrict__ img, int Ns, int ldt) {
   __shared__ float sv[64 * 65];  // [key][o]
@@ -305,20 +315,17 @@ __global__ void __launch_bounds__(256) train_s3_prep_kernel(const float* __restr
   bf16* vp = kp + 192LL * ldt;
   const float* kb = k + (long long)bh * Ns * 64;
   const float* vb = v + (long long)bh * Ns * 64;
-  const long long kps = 64LL * ldt, vps = 128LL * ldt;
+  const long long vps = 128LL * ldt;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = tid + 256 * i, n = idx >> 4, d = (idx & 15) * 4;
     const bool ok = n0 + n < Ns;
     const f32x4 x = ok ? *reinterpret_cast<const f32x4*>(kb + (long long)(n0 + n) * 64 + d) : f32x4{0.f, 0.f, 0.f, 0.f};
     const f32x4 y = ok ? *reinterpret_cast<const f32x4*>(vb + (long long)(n0 + n) * 64 + d) : f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x4 a, b, c;
+    // fp32 K rows for the QK32 kernel: d = 4 s + g stored at 16 g + s
+    float* kf = reinterpret_cast<float*>(kp) + (long long)(n0 + n) * 64 + d / 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) split3_into(x[e], a, b, c, e);
-    bf16* dst = kp + (long long)(n0 + n) * 64 + d;
-    *reinterpret_cast<bf16x4*>(dst) = a;
-    *reinterpret_cast<bf16x4*>(dst + kps) = b;
-    *reinterpret_cast<bf16x4*>(dst + 2 * kps) = c;
+    for (int e = 0; e < 4; ++e) kf[16 * e] = x[e];
 #pragma unroll
     for (int e = 0; e < 4; ++e) sv[n * 65 + d + e] = y[e];
   }
@@ -381,14 +388,24 @@ MHADA_DEV void attn_train_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], con
 
 // TRAIN: the training forward — Q in natural units (log2 e applied in fp32 on load, as attn_f32_kernel's
 // TRAIN form), the training epilogue (out', [M' | E2'], lse2).
-template <int NW, bool TRAIN = false>
+// QK32 (the training forward): S = Q K^T on the fp32 MFMA (v_mfma_f32_16x16x4f32, the S^T tile layout of
+// the bf16 16x16x32 MFMA) from fp32 K rows, P V' / P V'^2 SPLIT3 as above.  The backward recomputes S
+// on the fp32 MFMA against this kernel's lse2: a SPLIT3 S (whose bf16 MFMA sums truncate) put the two
+// apart by ~1e-5 |S| at large logits — enough to move gradient norms of the 64^2 video golden by 6e-3
+// (ops.TRAIN_FWD_S3).  K image: fp32 rows [ldt][64] with d permuted to 16 g + s (= d 4 s + g: lane
+// group g's 16 MFMA steps are 64 contiguous bytes) in the K-plane region of the plane image; in LDS the
+// 16-B chunk c of key row k at slot c ^ f(k & 7), f(k) = (k & 3) | (k >> 2) << 3 (the 16 lanes of a
+// ds_read_b128 group then hit 16 distinct slots).
+template <int NW, bool TRAIN = false, bool QK32 = false>
 __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   constexpr int TK = kS3Tk;
-  constexpr int KPL = TK * 64, VPL = 128 * TK, SLOT = 3 * (KPL + VPL);  // bf16 elements
-  constexpr int KPC = 3 * KPL / 512, VPC = 3 * VPL / 512;                // 1-KiB DMA pieces per slot: 24 + 48
+  constexpr int KPL = TK * 64, VPL = 128 * TK;                // bf16 elements per plane
+  constexpr int KREG = QK32 ? 2 * TK * 64 : 3 * KPL;          // bf16 elements of the slot's K region
+  constexpr int SLOT = KREG + 3 * VPL;
+  constexpr int KPC = KREG / 512, VPC = 3 * VPL / 512;        // 1-KiB DMA pieces per slot: 24 (16) + 48
   static_assert(KPC % NW == 0 && VPC % NW == 0, "tile config");
   constexpr int KPW = KPC / NW, VPW = VPC / NW;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * SLOT];  // 144 KiB
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * SLOT];  // 144 KiB (QK32: 128 KiB)
   int b, hh, qb;
   decode_block(p, b, hh, qb);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -399,9 +416,16 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
   bf16x8 qf[3][2][2];  // Q^T planes: query q0 + 16 qg + r16, d = 32 dh + 8 g .. + 8
+  float qreg[2][16];   // QK32: Q[q][4 s + g] (x log2 e) for MFMA step s
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q0 + 16 * qg + r16;
+    if constexpr (QK32) {
+      const float* qr = reinterpret_cast<const float*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + g;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) qreg[qg][st] = q < p.Nc ? qr[4 * st] * 1.4426950408889634f : 0.f;
+      continue;
+    }
     const float* qp = reinterpret_cast<const float*>(p.q) + (bh * p.Nc + (q < p.Nc ? q : 0)) * 64 + 8 * g;
 #pragma unroll
     for (int dh = 0; dh < 2; ++dh) {
@@ -420,8 +444,14 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   int ksrc[KPW], vsrc[VPW];
 #pragma unroll
   for (int i = 0; i < KPW; ++i) {
-    const int pc = NW * i + wave, pl = pc >> 3, row = 8 * (pc & 7) + (lane >> 3), slot = lane & 7;
-    ksrc[i] = pl * 64 * ldt + row * 64 + 8 * (slot ^ (row & 7));
+    if constexpr (QK32) {  // 4 fp32 rows of 256 B per piece; bf16-element offsets
+      const int pc = NW * i + wave, row = 4 * pc + (lane >> 4), slot = lane & 15;
+      const int f = (row & 3) | (((row >> 2) & 1) << 3);
+      ksrc[i] = 2 * (row * 64 + 4 * (slot ^ f));
+    } else {
+      const int pc = NW * i + wave, pl = pc >> 3, row = 8 * (pc & 7) + (lane >> 3), slot = lane & 7;
+      ksrc[i] = pl * 64 * ldt + row * 64 + 8 * (slot ^ (row & 7));
+    }
   }
 #pragma unroll
   for (int i = 0; i < VPW; ++i) {
@@ -430,8 +460,8 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   }
   auto stage = [&](int key0, int sl) {
     bf16* kd = smem + sl * SLOT;
-    bf16* vd = kd + 3 * KPL;
-    const bf16* ks = kp + (long long)key0 * 64;
+    bf16* vd = kd + KREG;
+    const bf16* ks = kp + (long long)key0 * (QK32 ? 128 : 64);
     const bf16* vs = vp + key0;
 #pragma unroll
     for (int i = 0; i < KPW; ++i) attn_glds16(ks + ksrc[i], kd + 512 * (NW * i + wave));
@@ -442,6 +472,26 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) krow[t] = fsq_key(r16, t) * 64;
   auto qk = [&](int sl, f32x4 (&S)[2][2][2], const f32x4 (&init)[2]) {
+    if constexpr (QK32) {
+      const float* ck = reinterpret_cast<const float*>(smem + sl * SLOT);
+      const int f = (r16 & 3) | (((r16 >> 2) & 1) << 3);  // f(key & 7), key & 7 == r16 & 7
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float* kr = ck + (kg * 32 + fsq_key(r16, t)) * 64;
+          f32x4 kf[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) kf[j] = *reinterpret_cast<const f32x4*>(kr + 4 * ((4 * g + j) ^ f));
+#pragma unroll
+          for (int st = 0; st < 16; ++st)
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg)
+              S[qg][kg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[st >> 2][st & 3], qreg[qg][st],
+                                                                  st == 0 ? init[qg] : S[qg][kg][t], 0, 0, 0);
+        }
+      return;
+    }
     const bf16* ck = smem + sl * SLOT;
 #pragma unroll
     for (int kg = 0; kg < 2; ++kg)
@@ -472,7 +522,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
   auto finish = [&](int sl, const f32x4 (&S)[2][2][2]) {
-    const bf16* cv = smem + sl * SLOT + 3 * KPL;
+    const bf16* cv = smem + sl * SLOT + KREG;
 #pragma unroll
     for (int kg = 0; kg < 2; ++kg) {
       bf16x8 pf[3][2];
@@ -553,7 +603,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
     lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
     mx[qg] = -Cm[qg][0];
   }
-  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3(p, kp, vp, qf, O, lt, mx, g, r16);
+  if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3<QK32>(p, kp, vp, qf, qreg, O, lt, mx, g, r16);
   if constexpr (TRAIN) attn_train_epilogue_q(p, O, lt, mx, bh, q0, g, r16);
   else attn_epilogue_q<float>(p, O, lt, b, hh, q0, g, r16);
 }
@@ -640,7 +690,7 @@ extern "C" int mhada_attn_train_fwd_split3(const float* q, const float* k, const
   p.nblk = (int)nblk;
   hipLaunchKernelGGL(train_s3_prep_kernel, dim3(p.ldt / 64, BH), dim3(256), 0, s, k, v, reinterpret_cast<bf16*>(img),
                      Ns, p.ldt);
-  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, true>), dim3(p.nblk), dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((attn_s3_kernel<4, true>), dim3(p.nblk), dim3(256), 0, s, p);
+  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, true, true>), dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((attn_s3_kernel<4, true, true>), dim3(p.nblk), dim3(256), 0, s, p);
   return check_launch("mhada_attn_train_fwd_split3");
 }
