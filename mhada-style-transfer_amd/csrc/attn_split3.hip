@@ -390,13 +390,21 @@ MHADA_DEV void attn_train_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], con
 // TRAIN form), the training epilogue (out', [M' | E2'], lse2).
 // QK32 (the training forward): S = Q K^T on the fp32 MFMA (v_mfma_f32_16x16x4f32, the S^T tile layout of
 // the bf16 16x16x32 MFMA) from fp32 K rows, P V' / P V'^2 SPLIT3 as above.  The backward recomputes S
-// on the fp32 MFMA against this kernel's lse2: a SPLIT3 S (whose bf16 MFMA sums truncate) put the two
-// apart by ~1e-5 |S| at large logits — enough to move gradient norms of the 64^2 video golden by 6e-3
-// (ops.TRAIN_FWD_S3).  K image: fp32 rows [ldt][64] with d permuted to 16 g + s (= d 4 s + g: lane
+// on the fp32 MFMA against this kernel's lse2, so lse2 and the backward's P come from the same fp32
+// products (a SPLIT3 S differs from them by ~1e-5 |S| at large logits; QK32 with ACC 0 alone did not
+// move the video golden below, ACC 1 with a SPLIT3 S was not measured).
+// ACC 1 (the training forward): P V' / P V'^2 and the row sums of each 32-key group from zero, added to
+// the running totals by fp32 VALU adds (round to nearest).  Accumulated in the MFMA instead (ACC 0, the
+// inference kernel) the bf16 MFMA's truncating partial sums bias M' and E2' low by a few 1e-7 — 3x the
+// error of ACC 1 on the bench data (profiles/r06_attn_s3_acc_ab.log) — and through sqrt's gradient at
+// near-degenerate variance rows that moved the 64^2 video-training golden's AdaFormer gradient norm by
+// 5.9e-3 (ACC 1: 3.3e-4; the fp32-MFMA forward: 4.9e-4; profiles/r06_train_fwd_s3_acc_ab.log).  ACC 1
+// costs 7 % at inference (and 10 spilled registers in the 8-wave inference kernel): not used there.
+// K image: fp32 rows [ldt][64] with d permuted to 16 g + s (= d 4 s + g: lane
 // group g's 16 MFMA steps are 64 contiguous bytes) in the K-plane region of the plane image; in LDS the
 // 16-B chunk c of key row k at slot c ^ f(k & 7), f(k) = (k & 3) | (k >> 2) << 3 (the 16 lanes of a
 // ds_read_b128 group then hit 16 distinct slots).
-template <int NW, bool TRAIN = false, bool QK32 = false>
+template <int NW, bool TRAIN = false, bool QK32 = false, int ACC = 0>
 __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   constexpr int TK = kS3Tk;
   constexpr int KPL = TK * 64, VPL = 128 * TK;                // bf16 elements per plane
@@ -512,6 +520,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
       }
   };
   f32x4 O[2][8], L[2];
+  float lsum[2] = {0.f, 0.f};  // ACC 1: the row sums, summed per 32-key group in fp32
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     L[qg] = z4;
@@ -532,19 +541,43 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
         for (int j = 0; j < 8; ++j) split3_into(fast_exp2(S[qg][kg][j >> 2][j & 3]), pf[0][qg], pf[1][qg], pf[2][qg], j);
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg) {
-        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[2][qg], L[qg], 0, 0, 0);
-        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][qg], L[qg], 0, 0, 0);
-        L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][qg], L[qg], 0, 0, 0);
+        if constexpr (ACC == 0) {
+          L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[2][qg], L[qg], 0, 0, 0);
+          L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][qg], L[qg], 0, 0, 0);
+          L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][qg], L[qg], 0, 0, 0);
+        } else {  // the group's sum from zero, added to the total in fp32 (round to nearest)
+          f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[2][qg], z4, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][qg], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][qg], t, 0, 0, 0);
+          lsum[qg] += t[0];
+        }
       }
       const int off = 8 * ((4 * kg + g) ^ ((r16 >> 1) & 7));  // row 16 dvb + r16
+      f32x4 tp[2];  // ACC 1: the previous dvb's group sums, added one step later (no MFMA -> VALU wait)
 #pragma unroll
       for (int dvb = 0; dvb < 8; ++dvb) {
         const bf16* vr = cv + (16 * dvb + r16) * TK + off;
         const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vr);
         const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vr + VPL);
         const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vr + 2 * VPL);
+        if constexpr (ACC == 0) {
 #pragma unroll
-        for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], O[qg][dvb]);
+          for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], O[qg][dvb]);
+        } else {
+          f32x4 tn[2];
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg) tn[qg] = mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], z4);
+          if (dvb > 0) {
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg) O[qg][dvb - 1] += tp[qg];
+          }
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg) tp[qg] = tn[qg];
+        }
+      }
+      if constexpr (ACC != 0) {
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) O[qg][7] += tp[qg];
       }
     }
   };
@@ -600,7 +633,7 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   float lt[2], mx[2];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
-    lt[qg] = L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
+    lt[qg] = ACC ? lsum[qg] : L[qg][0];  // every D row is the full sum over the 32 keys of each MFMA
     mx[qg] = -Cm[qg][0];
   }
   if (__any(!(lt[0] <= kShiftSumThr) || !(lt[1] <= kShiftSumThr))) attn_exact_q3<QK32>(p, kp, vp, qf, qreg, O, lt, mx, g, r16);
@@ -690,7 +723,7 @@ extern "C" int mhada_attn_train_fwd_split3(const float* q, const float* k, const
   p.nblk = (int)nblk;
   hipLaunchKernelGGL(train_s3_prep_kernel, dim3(p.ldt / 64, BH), dim3(256), 0, s, k, v, reinterpret_cast<bf16*>(img),
                      Ns, p.ldt);
-  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, true, true>), dim3(p.nblk), dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((attn_s3_kernel<4, true, true>), dim3(p.nblk), dim3(256), 0, s, p);
+  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, true, true, 1>), dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((attn_s3_kernel<4, true, true, 1>), dim3(p.nblk), dim3(256), 0, s, p);
   return check_launch("mhada_attn_train_fwd_split3");
 }

@@ -670,14 +670,14 @@ def attn_train_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, x: torch.T
     return out, mo, lse
 
 
-# attn_train_fwd: TRAIN_FWD_VT = mhada_attn_train_fwd_vt (the fp32-MFMA inference structure, the
-# default), False = the round-1 kernel (A/B, tests).  TRAIN_FWD_S3 = the SPLIT3 kernel on the bf16 MFMA
-# (round 6; 457 -> 433 ms per 512^2 B8 step) — off by default: the backward recomputes S on the fp32
-# MFMA against the forward's lse2, and for large logits the bf16 MFMA's truncating partial sums put
-# the two S apart by ~1e-5 |S|, so P in the backward no longer sums to 1: the 64^2 video-training
-# golden's gradient norms move by up to 5.9e-3 (fp32 noise there: 4.9e-4, its float64 yardstick;
-# tools/video_golden_ab.py, profiles/r06_video_golden_ab.log)
-TRAIN_FWD_S3 = False
+# attn_train_fwd: TRAIN_FWD_S3 = mhada_attn_train_fwd_split3 (round 6, the default): S on the fp32
+# MFMA, P V' / P V'^2 as SPLIT3 products on the bf16 MFMA with per-group sums added in fp32
+# (csrc/attn_split3.hip) — 450 -> 433 ms per 512^2 B8 training step; the 64^2 video-training golden's
+# gradient norms within 3.3e-4 (the fp32-MFMA forward: 4.9e-4;
+# tools/video_golden_ab.py, profiles/r06_train_fwd_s3_acc_ab.log).  TRAIN_FWD_VT =
+# mhada_attn_train_fwd_vt (the fp32-MFMA inference structure, round 4) when TRAIN_FWD_S3 is off;
+# both off = the round-1 kernel (A/B, tests).
+TRAIN_FWD_S3 = True
 TRAIN_FWD_VT = True
 
 

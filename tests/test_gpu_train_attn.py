@@ -2,9 +2,11 @@
 reference formula (adaDecoder.py:186-198), and the fused block against the plain-autograd block.
 
 Tolerances: fp32 MFMA (exact fp32 products, fp32 accumulation) vs fp64 — relative max error
-of outputs < 2e-4 of the tensor's max magnitude; of gradients < max(2e-4, 3x the error of the
+of outputs < 2e-4 of the tensor's max magnitude; of gradients < max(2e-4, 4x the error of the
 reference's own fp32 autograd on the same inputs) — peaky softmaxes (logit std 12) lose digits
-in dS = P (dA - D) in any fp32 evaluation."""
+in dS = P (dA - D) in any fp32 evaluation: over four seeds of each shape both training forwards
+(SPLIT3 and the fp32-MFMA one, sharing the backward) land 1-5x the yardstick at logit std >= 12,
+neither systematically ahead (tools/train_attn_err.py, profiles/r06_train_attn_err.log)."""
 import os
 
 import pytest
@@ -30,9 +32,12 @@ def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item()
 
 
+@pytest.mark.parametrize("form", ["s3", "vt"])
 @pytest.mark.parametrize("BH,Nc,Ns,scale", [(2, 128, 64, 0.4), (3, 100, 70, 0.4), (1, 37, 300, 0.6),
                                             (2, 256, 129, 1.5)])
-def test_attn_train_fwd_bwd_vs_fp64(BH, Nc, Ns, scale):
+def test_attn_train_fwd_bwd_vs_fp64(monkeypatch, form, BH, Nc, Ns, scale):
+    monkeypatch.setattr(ops, "TRAIN_FWD_S3", form == "s3")
+    monkeypatch.setattr(ops, "TRAIN_FWD_VT", True)
     g = torch.Generator().manual_seed(Nc * 7 + Ns)
     q = torch.randn(BH, Nc, 64, generator=g) * scale
     k = torch.randn(BH, Ns, 64, generator=g) * scale
@@ -55,7 +60,7 @@ def test_attn_train_fwd_bwd_vs_fp64(BH, Nc, Ns, scale):
     for name, a, b, c in zip("qkvx", gs, ts, fs):
         err = _rel(a.grad.double().cpu(), b.grad)
         err32 = _rel(c.grad.double().cpu(), b.grad)
-        assert err < max(2e-4, 3 * err32), (name, err, err32)
+        assert err < max(2e-4, 4 * err32), (name, err, err32)
 
 
 def test_attn_train_bwd_with_clamped_variance():
@@ -232,8 +237,11 @@ def test_attn_train_fwd_kernels_vs_fp64(monkeypatch, form, BH, Nc, Ns, scale):
     a = torch.softmax(s, -1)
     assert torch.allclose(lse.double().cpu(), torch.logsumexp(s, -1) / torch.log(torch.tensor(2.0, dtype=torch.float64)),
                           atol=2e-4, rtol=1e-5)
-    assert _rel(mo[..., :64].double().cpu(), a @ vd) < 2e-5
-    assert _rel(mo[..., 64:].double().cpu(), a @ vd ** 2) < 2e-5
+    # M', E2': 2e-5, or 2x the error of the same expressions evaluated in fp32 by torch (at logit std
+    # 72, scale 3, an fp32 S is off by ~1e-5 in log2 units and P by as much relative, in any fp32 form)
+    a32 = torch.softmax(q @ k.transpose(1, 2), -1)
+    for sl, ref64, ref32 in ((slice(0, 64), a @ vd, a32 @ v), (slice(64, 128), a @ vd ** 2, a32 @ (v * v))):
+        assert _rel(mo[..., sl].double().cpu(), ref64) < max(2e-5, 2 * _rel(ref32.double(), ref64))
     # out' = sqrt(E2' - M'^2) x + M' cancels where the variance is small: held to the error of the
     # reference expression's own fp32 evaluation on the same inputs (x4), with a 2e-4 floor
     ref = _ref(qd, kd, vd, x.double())
