@@ -95,12 +95,19 @@ SPLIT3_MFMA_PER_FP32 = (6 * 128 + 6 * 256 + 3 * 32) / 384
 
 
 def attn_source_sha() -> str:
-    """sha256 (16 hex) of the attention kernel's sources: ties a PMC measurement to this build."""
+    """sha256 (16 hex) of the attention kernel's sources: ties a PMC measurement to this build.
+    Comments and blank lines are left out (round 6), so a comment edit keeps a measurement valid;
+    any change to the code itself makes it stale."""
     import hashlib
+    import re
     h = hashlib.sha256()
     for rel in ATTN_SOURCES:
-        with open(os.path.join(REPO, rel), "rb") as f:
-            h.update(f.read())
+        with open(os.path.join(REPO, rel), encoding="utf-8") as f:
+            text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+        for line in text.splitlines():
+            line = line.split("//", 1)[0].rstrip()
+            if line:
+                h.update(line.encode() + b"\n")
     return h.hexdigest()[:16]
 
 

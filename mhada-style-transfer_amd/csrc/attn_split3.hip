@@ -391,8 +391,10 @@ MHADA_DEV void attn_train_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], con
 // QK32 (the training forward): S = Q K^T on the fp32 MFMA (v_mfma_f32_16x16x4f32, the S^T tile layout of
 // the bf16 16x16x32 MFMA) from fp32 K rows, P V' / P V'^2 SPLIT3 as above.  The backward recomputes S
 // on the fp32 MFMA against this kernel's lse2, so lse2 and the backward's P come from the same fp32
-// products (a SPLIT3 S differs from them by ~1e-5 |S| at large logits; QK32 with ACC 0 alone did not
-// move the video golden below, ACC 1 with a SPLIT3 S was not measured).
+// products: a SPLIT3 S (the bf16 MFMA's truncating sums, ~1e-5 |S| at large logits) needs neither fp32
+// pipe nor K rows and is 2 % faster per training step (424.6 vs 433.1 ms), but with ACC 1 it leaves the
+// 64^2 video golden's AdaFormer gradient norm at 5.8e-3 — both changes are needed
+// (profiles/r06_train_fwd_s3_acc_ab.log).
 // ACC 1 (the training forward): P V' / P V'^2 and the row sums of each 32-key group from zero, added to
 // the running totals by fp32 VALU adds (round to nearest).  Accumulated in the MFMA instead (ACC 0, the
 // inference kernel) the bf16 MFMA's truncating partial sums bias M' and E2' low by a few 1e-7 — 3x the
