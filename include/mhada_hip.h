@@ -257,9 +257,11 @@ int mhada_attn_train_fwd(const float* q, const float* k, const float* v, const f
  * that this call fills from v.  Same outputs as mhada_attn_train_fwd (ABI 10). */
 int mhada_attn_train_fwd_vt(const float* q, const float* k, const float* v, float* vt, const float* x,
                             float* out, float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
-/* The same forward as fp32-accurate SPLIT3 products on the bf16 MFMA (ABI 16; csrc/attn_split3.hip,
- * mhada_attn_split3's arithmetic): img is caller-provided workspace of BH * 576 * ceil64(Ns) bf16 that
- * this call fills with the plane image of k and v.  Same outputs as mhada_attn_train_fwd_vt. */
+/* The same forward with P V' / P V'^2 as fp32-accurate SPLIT3 products on the bf16 MFMA (ABI 16;
+ * csrc/attn_split3.hip): S = Q K^T on the fp32 MFMA (as the backward recomputes it, so lse2 matches),
+ * the PV products and row sums summed per 32-key group and added in fp32.  img is caller-provided
+ * workspace of BH * 576 * ceil64(Ns) bf16 that this call fills from k (fp32 rows) and v (planes).
+ * Same outputs as mhada_attn_train_fwd_vt. */
 int mhada_attn_train_fwd_split3(const float* q, const float* k, const float* v, void* img, const float* x,
                                 float* out, float* mo, float* lse, int BH, int Nc, int Ns, mhada_stream_t stream);
 /* dst [BH][64][ldt] = src [BH][N][64] transposed per problem (columns N..ldt-1 zero; ldt % 64 == 0,
