@@ -268,6 +268,18 @@ int mhada_attn_train_fwd_split3(const float* q, const float* k, const float* v, 
  * ldt >= N): K^T, the W operand of the dQ = dS K GEMM after mhada_attn_train_dkv's dS spill
  * (replaces the strided aten copy k.transpose(1, 2).contiguous()) (ABI 11). */
 int mhada_transpose64(const float* src, float* dst, int BH, int N, int ldt, mhada_stream_t stream);
+/* dQ = dS K of the dS-spill backward as fp32-accurate SPLIT3 products on the bf16 MFMA (ABI 16;
+ * csrc/gemm_n64_split3.hip): c[z][m][n] = sum_k a[z][m][k] w[z][n][k], n < 64, for z < nz.  a fp32
+ * rows (dS [BH][Nc][Ns]: M = Nc, K = Ns, lda, problem stride sa), split into three bf16 planes in
+ * registers; w_planes = mhada_split3_rows of K^T (mhada_transpose64): three bf16 planes of stride wps
+ * elements, each [nz][64][ldw] (problem stride sw); c fp32 [nz][M][ldc] (problem stride sc).
+ * K % 32 == 0, 16-byte aligned rows and problems.  Replaces mhada_gemm(a = dS, w = K^T, N = 64, fp32). */
+int mhada_gemm_n64_split3(const float* a, const void* w_planes, float* c, int nz, int M, int K, int lda,
+                          long long sa, int ldw, long long sw, long long wps, int ldc, long long sc,
+                          mhada_stream_t stream);
+/* Its W operand in one pass (ABI 16): k fp32 [BH][N][64] -> planes bf16 [3][BH][64][ldt], the three
+ * planes of K^T (= mhada_split3_rows(mhada_transpose64(k))), key columns >= N zero; ldt % 64 == 0. */
+int mhada_transpose64_split3(const float* k, void* planes, int BH, int N, int ldt, mhada_stream_t stream);
 int mhada_attn_train_bwd(const float* q, const float* k, const float* v, const float* lse,
                          const float* dmo, const float* dd, float* dq, float* dk, float* dv,
                          int BH, int Nc, int Ns, mhada_stream_t stream);

@@ -81,6 +81,8 @@ SIGNATURES = {
     "mhada_attn_train_fwd_vt": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
     "mhada_attn_train_fwd_split3": (_I, [_vp] * 8 + [_I, _I, _I, _vp]),
     "mhada_transpose64": (_I, [_vp, _vp, _I, _I, _I, _vp]),
+    "mhada_gemm_n64_split3": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _c_ll, _I, _c_ll, _c_ll, _I, _c_ll, _vp]),
+    "mhada_transpose64_split3": (_I, [_vp, _vp, _I, _I, _I, _vp]),
     "mhada_attn_train_bwd": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_attn_train_dkv": (_I, [_vp] * 9 + [_I, _I, _I, _vp]),
     "mhada_conv3x3_out3": (_I, [_vp, _I, _vp, _vp, _vp, _I, _I, _I, _I, _I, _vp]),

@@ -747,11 +747,48 @@ def attn_train_bwd(q, k, v, lse, dmo, dd, spill: Optional[bool] = None):
         raise ValueError("attn_train_bwd: the dS spill needs Ns % 4 == 0")
     _call("mhada_attn_train_dkv", q, q.data_ptr(), k.data_ptr(), v.data_ptr(), lse.data_ptr(), dmo.data_ptr(),
           dd.data_ptr(), dk.data_ptr(), dv.data_ptr(), ds.data_ptr(), BH, Nc, Ns)
-    kt = transpose64(k)  # W[n = d][k = key] of the NT GEMM, rows padded to ceil64(Ns)
-    ldt = kt.shape[-1]
-    gemm(a=ds, w=kt, c=dq, M=Nc, N=64, K=Ns, compute=torch.float32, lda=Ns, sa=(Nc * Ns, 0), nb=(BH, 1),
-         ldw=ldt, sw=(64 * ldt, 0), ldc=64, sc=(Nc * 64, 0))
+    if TRAIN_DQ_S3 and Ns % 32 == 0:
+        ldt = (Ns + 63) // 64 * 64
+        gemm_n64_split3(ds, transpose64_split3(k), dq, BH, Nc, Ns, ldt)
+    else:
+        kt = transpose64(k)  # W[n = d][k = key] of the NT GEMM, rows padded to ceil64(Ns)
+        ldt = kt.shape[-1]
+        gemm(a=ds, w=kt, c=dq, M=Nc, N=64, K=Ns, compute=torch.float32, lda=Ns, sa=(Nc * Ns, 0), nb=(BH, 1),
+             ldw=ldt, sw=(64 * ldt, 0), ldc=64, sc=(Nc * 64, 0))
     return dq, dk, dv
+
+
+# dQ = dS K of the dS-spill backward as SPLIT3 products on the bf16 MFMA (csrc/gemm_n64_split3.hip,
+# round 6) where Ns % 32 == 0; False: the fp32-MFMA N <= 64 GEMM (gemm_n64_kernel)
+TRAIN_DQ_S3 = True
+
+
+def transpose64_split3(k: torch.Tensor) -> torch.Tensor:
+    """``mhada_transpose64_split3``: fp32 [BH][N][64] -> the bf16 planes of its transpose [3][BH * 64][ldt]
+    (ldt = ceil64(N), columns >= N zero) = ``split3_rows(transpose64(k))`` in one pass."""
+    _need_gpu(k)
+    if k.dtype != torch.float32 or k.dim() != 3 or k.shape[-1] != 64:
+        raise ValueError("transpose64_split3: fp32 [BH][N][64]")
+    k = k.contiguous()
+    BH, N, _ = k.shape
+    ldt = (N + 63) // 64 * 64
+    out = torch.empty(3, BH * 64, ldt, device=k.device, dtype=torch.bfloat16)
+    _call("mhada_transpose64_split3", k, k.data_ptr(), out.data_ptr(), BH, N, ldt)
+    return out
+
+
+def gemm_n64_split3(ds: torch.Tensor, kt_planes: torch.Tensor, dq: torch.Tensor, BH: int, Nc: int, Ns: int,
+                    ldt: int):
+    """``mhada_gemm_n64_split3``: dq [BH][Nc][64] = ds [BH][Nc][Ns] @ K where kt_planes = the three bf16
+    planes [3][BH * 64][ldt] of K^T (``split3_rows(transpose64(k))``)."""
+    if ds.dtype != torch.float32 or not ds.is_contiguous() or ds.shape != (BH, Nc, Ns):
+        raise ValueError("gemm_n64_split3: ds must be contiguous float32 [BH][Nc][Ns]")
+    if kt_planes.dtype != torch.bfloat16 or kt_planes.shape != (3, BH * 64, ldt) or not kt_planes.is_contiguous():
+        raise ValueError("gemm_n64_split3: kt_planes must be contiguous bf16 [3][BH*64][ldt]")
+    if dq.dtype != torch.float32 or not dq.is_contiguous() or dq.shape != (BH, Nc, 64):
+        raise ValueError("gemm_n64_split3: dq must be contiguous float32 [BH][Nc][64]")
+    _call("mhada_gemm_n64_split3", ds, ds.data_ptr(), kt_planes.data_ptr(), dq.data_ptr(), BH, Nc, Ns, Ns, Nc * Ns,
+          ldt, 64 * ldt, BH * 64 * ldt, 64, Nc * 64)
 
 
 # ---- video path: optical-flow warping (NCHW fp32) ---------------------------------------

@@ -259,3 +259,38 @@ def test_transpose64_is_the_exact_transpose(BH, N):
     assert t.shape == (BH, 64, ldt)
     assert torch.equal(t[..., :N], x.transpose(1, 2))
     assert bool((t[..., N:] == 0).all())
+
+
+@pytest.mark.parametrize("BH,Nc,Ns,scale", [(2, 300, 128, 1.0), (8, 256, 1024, 1.0), (3, 1000, 96, 30.0),
+                                            (1, 37, 32, 1.0), (16, 520, 4096, 0.01)])
+def test_dq_split3_vs_fp64(monkeypatch, BH, Nc, Ns, scale):
+    """dQ = dS K of the dS-spill backward on the SPLIT3 GEMM (mhada_gemm_n64_split3: dS split into bf16
+    planes in registers, K^T as planes, 6 cross products per K-tile summed from zero and added in fp32)
+    against fp64 and against the fp32-MFMA N <= 64 GEMM it replaces: ragged row tiles, 1 .. 128
+    K-tiles, problem counts with and without the per-XCD grouping (BH % 8), dS of mixed sign and
+    magnitude (as P (dA - D) is)."""
+    g = torch.Generator().manual_seed(BH * 7 + Nc + Ns)
+    ds = (torch.randn(BH, Nc, Ns, generator=g) * torch.rand(BH, Nc, 1, generator=g) * scale).cuda()
+    k = torch.randn(BH, Ns, 64, generator=g).cuda()
+    ref = ds.double() @ k.double()
+    kt = ops.transpose64(k)
+    ldt = kt.shape[-1]
+    dq = torch.full((BH, Nc, 64), float("nan"), device="cuda")
+    ops.gemm_n64_split3(ds, ops.split3_rows(kt.view(BH * 64, ldt)), dq, BH, Nc, Ns, ldt)
+    dq32 = torch.empty_like(dq)
+    ops.gemm(a=ds, w=kt, c=dq32, M=Nc, N=64, K=Ns, compute=torch.float32, lda=Ns, sa=(Nc * Ns, 0), nb=(BH, 1),
+             ldw=ldt, sw=(64 * ldt, 0), ldc=64, sc=(Nc * 64, 0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(dq).all()
+    e3, e32 = _rel(dq.double(), ref), _rel(dq32.double(), ref)
+    assert e3 < 2e-6 and e3 <= 1.5 * e32 + 1e-8, (e3, e32)
+
+
+@pytest.mark.parametrize("BH,N", [(3, 300), (2, 64), (1, 4096), (4, 7)])
+def test_transpose64_split3_is_split_of_transpose(BH, N):
+    """mhada_transpose64_split3 (the SPLIT3 dQ GEMM's W operand in one pass) = split3_rows of
+    mhada_transpose64 bit for bit, padding columns zero in every plane."""
+    x = torch.randn(BH, N, 64, generator=torch.Generator().manual_seed(N + 1)).cuda()
+    kt = ops.transpose64(x)
+    ldt = kt.shape[-1]
+    assert torch.equal(ops.transpose64_split3(x), ops.split3_rows(kt.view(BH * 64, ldt)))
