@@ -20,6 +20,11 @@
 // are added to the fp32 accumulators by VALU adds (round to nearest) — the bf16 MFMA's truncating sums
 // then never accumulate over the 128 K-tiles of a row (the training forward's lesson, attn_split3.hip).
 //
+// Measured at the 512^2 B8 step's shape (tools/dq_ab.py, profiles/r06_dq_split3_ab.log): 3.23-3.29 vs
+// 3.70-3.75 ms for gemm_n64_kernel, 4.0 TB/s of A, error against fp64 4.6e-7 vs 2.2e-6.  A form with A
+// loaded straight into registers (four-deep register ring, W alone in a four-slot LDS ring) measured
+// 3.205 vs 3.228 ms in the same run — within noise, not kept.
+//
 // LDS images: A row r (128 B = 8 chunks of 4 floats): chunk c at slot c ^ ((r >> 1) & 7); W plane
 // row n (64 B = 4 chunks of 8 bf16): chunk c at slot c ^ ((n >> 2) & 3) — the ds_read_b128 lane
 // groups (32 rows x one chunk) hit distinct (bank, slot) pairs.
