@@ -46,9 +46,12 @@ extern "C" int mhada_gemm(const mhada_gemm_args* a, mhada_stream_t stream_) {
   p.r = a->r; p.ldr = a->ldr; p.sr1 = a->sr1; p.sr2 = a->sr2;
   p.c = a->c; p.ldc = a->ldc; p.sc1 = a->sc1; p.sc2 = a->sc2;
   if (a->relu < 0 || a->relu > 2) return fail("mhada_gemm: relu must be 0, 1 or 2");
-  if (a->relu == 2 && (!a->r || a->r_dtype != MHADA_F32 || a->c_dtype != MHADA_F32 || a->c2 || a->vt ||
+  // (a SPLIT3 GEMM may also write the masked result's planes: c2_planes with C, round 6)
+  if (a->relu == 2 && (!a->r || a->r_dtype != MHADA_F32 || a->c_dtype != MHADA_F32 || !a->c ||
+                       (a->c2 && !(a->c2_planes && a->a_mode == MHADA_A_SPLIT3)) || a->vt ||
                        (a->a_mode != MHADA_A_ROWS && a->a_mode != MHADA_A_SPLIT3)))
-    return fail("mhada_gemm: relu = 2 (ReLU-adjoint mask) needs fp32 C, an fp32 mask in r, ROWS or SPLIT3 mode, no c2 / vt");
+    return fail("mhada_gemm: relu = 2 (ReLU-adjoint mask) needs fp32 C, an fp32 mask in r, ROWS or SPLIT3 mode, "
+                "no vt, c2 only as SPLIT3 planes");
   p.relu = a->relu;
   p.c2 = a->c2; p.ldc2 = a->ldc2; p.sc21 = a->sc21; p.sc22 = a->sc22;
   p.c2planes = a->c2_planes ? 1 : 0;

@@ -73,7 +73,7 @@ def _vit_forward_hip(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor
         t = train_fns.linear(o, att.out_proj.weight, att.out_proj.bias, residual=t.reshape(B * N, C)).view(B, N, C)
         y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2) if ln_hip else blk.ln2(t).reshape(B * N, C)
         # MLP1's ReLU adjoint is applied by MLP2's input-gradient GEMM (its only consumer)
-        m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True, grad_masked=True)
+        m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True, grad_masked=True, planes_out=True)
         t = train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias, relu_input=True,
                              residual=t.reshape(B * N, C)).view(B, N, C)
         outs.append(t.permute(0, 2, 1).reshape(B, C, h, w))

@@ -357,12 +357,14 @@ def split3_rows(x: torch.Tensor) -> torch.Tensor:
 
 def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.Tensor], out_dtype: torch.dtype,
                   residual: Optional[torch.Tensor] = None, relu: bool = False,
-                  out_planes: bool = False, relu_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out_planes: bool = False, relu_mask: Optional[torch.Tensor] = None, both: bool = False):
     """fp32-accurate x @ w^T (+bias, relu, residual) from x's bf16 planes [3][M][K0] and
     ``split3_weight(w)`` [N][6 K0]: the six significant cross products summed in fp32 accumulators
     on the bf16 MFMA (mhada_gemm MHADA_A_SPLIT3).  ``out_planes``: return the fp32 result as its
     three bf16 planes [3][M][N] (the next SPLIT3 GEMM's operand) instead of an fp32 [M][N].
-    ``relu_mask`` (fp32 [M][N], as ``linear``'s): the result zeroed where relu_mask <= 0."""
+    ``relu_mask`` (fp32 [M][N], as ``linear``'s): the result zeroed where relu_mask <= 0.  ``both``: return
+    (the fp32 result, its three bf16 planes) from the one epilogue — for a result that is kept in fp32
+    (saved for a backward) and also feeds a SPLIT3 GEMM."""
     if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_contiguous():
         raise ValueError("linear_split3: planes must be contiguous bf16 [3][M][K0]")
     _, M, K0 = planes.shape
@@ -377,14 +379,22 @@ def linear_split3(planes: torch.Tensor, w6: torch.Tensor, bias: Optional[torch.T
                     ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu,
                     c2=c2, ldc2=N, c2_planes=True)
     c = torch.empty(M, N, device=planes.device, dtype=out_dtype)
+    c2 = None
+    if both:
+        if out_dtype != torch.float32:
+            raise ValueError("linear_split3: both splits an fp32 result")
+        c2 = torch.empty(3, M, N, device=planes.device, dtype=torch.bfloat16)
     if relu_mask is not None:
         if residual is not None or relu or out_dtype != torch.float32 or relu_mask.dtype != torch.float32 \
                 or relu_mask.shape != (M, N) or not relu_mask.is_contiguous():
             raise ValueError("linear_split3: relu_mask needs fp32 output, a contiguous fp32 [M][N] mask, no residual / relu")
-        return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
-                    ldw=6 * K0, bias=bias, r=relu_mask, ldr=N, ldc=N, relu=2)
-    return gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
-                ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu)
+        gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
+             ldw=6 * K0, bias=bias, r=relu_mask, ldr=N, ldc=N, relu=2, c2=c2, ldc2=N if both else 0, c2_planes=both)
+    else:
+        gemm(a=planes, w=w6, c=c, M=M, N=N, K=6 * K0, compute=torch.bfloat16, a_mode=A_SPLIT3, lda=K0,
+             ldw=6 * K0, bias=bias, r=residual, ldr=N if residual is not None else 0, ldc=N, relu=relu,
+             c2=c2, ldc2=N if both else 0, c2_planes=both)
+    return (c, c2) if both else c
 
 
 def vit_batch_attn(qkv: torch.Tensor, L: int, ntok: int, heads: int, groups: int = 1) -> torch.Tensor:

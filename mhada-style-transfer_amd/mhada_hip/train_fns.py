@@ -196,6 +196,30 @@ def _split3_ok(M: int, N: int, K0: int, dev: torch.device) -> bool:
     return TRAIN_SPLIT3 and N > 128 and K0 % 64 == 0 and _split3_fills(M, N, dev)
 
 
+# A tensor that the producing SPLIT3 GEMM also wrote as its three bf16 planes (ops.linear_split3(both=True))
+# carries them here, with the tensor's _version at the time: the consuming LinearFn then skips its
+# mhada_split3_rows pass.  Forward: MLP1's ReLU output for MLP2; backward: MLP2's input gradient (MLP1's
+# output gradient, the ReLU mask applied) for MLP1's input-gradient GEMM.  Missing or stale: split again.
+PLANES_HANDOFF_ON = True  # False: every SPLIT3 LinearFn splits its operand itself (A/B)
+_PLANES_ATTR = "_mhada_split3_planes"
+PLANES_HANDOFF = {"used": 0, "split": 0}
+
+
+def _attach_planes(t: torch.Tensor, planes: torch.Tensor) -> None:
+    setattr(t, _PLANES_ATTR, (planes, t._version))
+
+
+def _planes_of(t: torch.Tensor) -> torch.Tensor:
+    hit = getattr(t, _PLANES_ATTR, None)
+    if hit is not None:
+        delattr(t, _PLANES_ATTR)  # one consumer; do not keep the planes alive with a saved tensor
+        if hit[1] == t._version and hit[0].shape == (3, *t.shape):
+            PLANES_HANDOFF["used"] += 1
+            return hit[0]
+    PLANES_HANDOFF["split"] += 1
+    return ops.split3_rows(t)
+
+
 class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) (+ residual) on contiguous fp32 rows x [M][K], W [N][K] (nn.Linear
     layout).  ``residual`` [M][N] (no ReLU with it): the add of a residual stream fused into the
@@ -204,16 +228,21 @@ class LinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, relu: bool, grad_masked: bool = False, relu_input: bool = False,
-                residual=None):
+                residual=None, planes_out: bool = False):
         x = x.contiguous()
         if residual is not None and relu:
             raise ValueError("LinearFn: a fused residual follows a ReLU-free linear")
         M, K0 = x.shape
         N = weight.shape[0]
         res = None if residual is None else residual.detach().contiguous()
-        if x.dtype == torch.float32 and _split3_ok(M, N, K0, x.device):
-            y = ops.linear_split3(ops.split3_rows(x), _split3_w(weight, False), bias.detach().contiguous(), F32,
-                                  residual=res, relu=relu)
+        # planes_out: y's consumer is a SPLIT3 LinearFn — write y's planes from this epilogue as well
+        ctx.s3_in = x.dtype == torch.float32 and _split3_ok(M, N, K0, x.device)
+        if ctx.s3_in:
+            y = ops.linear_split3(_planes_of(x), _split3_w(weight, False), bias.detach().contiguous(), F32,
+                                  residual=res, relu=relu, both=planes_out and PLANES_HANDOFF_ON)
+            if planes_out and PLANES_HANDOFF_ON:
+                y, yp = y
+                _attach_planes(y, yp)
         else:
             y = ops.linear(x, weight.detach().contiguous(), bias.detach().contiguous(), F32, relu=relu, residual=res)
         ctx.save_for_backward(x, weight, y if (relu and not grad_masked) else None)
@@ -233,8 +262,14 @@ class LinearFn(torch.autograd.Function):
             M, N = g.shape
             K0 = weight.shape[1]
             if _split3_ok(M, K0, N, g.device):
-                gx = ops.linear_split3(ops.split3_rows(g), _split3_w(weight, True), None, F32,
-                                       relu_mask=x if ctx.relu_input else None)
+                # relu_input with a SPLIT3 forward: x came from a SPLIT3 LinearFn(planes_out) whose
+                # input-gradient GEMM is SPLIT3 too (same M, N) — hand it gx's planes
+                both = PLANES_HANDOFF_ON and ctx.relu_input and ctx.s3_in and _split3_ok(M, N, K0, g.device)
+                gx = ops.linear_split3(_planes_of(g), _split3_w(weight, True), None, F32,
+                                       relu_mask=x if ctx.relu_input else None, both=both)
+                if both:
+                    gx, gp = gx
+                    _attach_planes(gx, gp)
             else:
                 gx = ops.linear(g, weight.detach().t().contiguous(), None, F32, relu_mask=x if ctx.relu_input else None)
         if ctx.needs_input_grad[1]:
@@ -244,12 +279,13 @@ class LinearFn(torch.autograd.Function):
                 gb = cs
         elif ctx.needs_input_grad[2]:
             gb = ops.colsum(g)
-        return gx, gw, gb, None, None, None, gy if ctx.needs_input_grad[6] else None
+        return gx, gw, gb, None, None, None, gy if ctx.needs_input_grad[6] else None, None
 
 
 def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, relu: bool = False,
-           grad_masked: bool = False, relu_input: bool = False, residual: torch.Tensor = None) -> torch.Tensor:
-    return LinearFn.apply(x2d, weight, bias, relu, grad_masked, relu_input, residual)
+           grad_masked: bool = False, relu_input: bool = False, residual: torch.Tensor = None,
+           planes_out: bool = False) -> torch.Tensor:
+    return LinearFn.apply(x2d, weight, bias, relu, grad_masked, relu_input, residual, planes_out)
 
 
 class InstanceNormTokensFn(torch.autograd.Function):

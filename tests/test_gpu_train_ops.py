@@ -360,7 +360,7 @@ def test_linear_fn_split3_vs_fp64(monkeypatch, M, K, N, mode):
     of the fp32-MFMA GEMMs' error (TRAIN_SPLIT3 = False) on the same operands; ReLU, a fused residual,
     and the MLP pair with its ReLU adjoint folded into the
     second layer's input-gradient epilogue (relu = 2 on the SPLIT3 kernel), bit-identical to the
-    unfolded pair."""
+    unfolded pair and to the pair with the plane hand-off (LinearFn planes_out)."""
     from mhada_hip.engine import _split3_fills
     assert _split3_fills(M, min(N, K), torch.device(DEV))  # the shapes take the SPLIT3 path
     errs = {}
@@ -376,14 +376,21 @@ def test_linear_fn_split3_vs_fp64(monkeypatch, M, K, N, mode):
             b2 = rnd(K, seed=26, scale=0.1).requires_grad_(True)
             ps += [w2, b2]
             grads = []
-            for fold in (True, False):
+            for fold, hand in ((True, False), (False, False), (True, True)):
                 for t in ps:
                     t.grad = None
-                h = train_fns.linear(x, w, b, relu=True, grad_masked=fold)
+                used = train_fns.PLANES_HANDOFF["used"]
+                h = train_fns.linear(x, w, b, relu=True, grad_masked=fold, planes_out=hand)
                 y = train_fns.linear(h, w2, b2, relu_input=fold)
                 y.backward(gy)
                 grads.append([t.grad.clone() for t in ps])
-            for a, c in zip(*grads):
+                # the plane hand-offs on the SPLIT3 path: forward with planes_out (MLP1's epilogue writes h's
+                # planes for MLP2), backward with the folded ReLU adjoint (MLP2's input-gradient epilogue
+                # writes the planes of h's gradient for MLP1's input-gradient GEMM)
+                assert train_fns.PLANES_HANDOFF["used"] - used == s3 * (int(hand) + int(fold))
+            for a, c in zip(grads[0], grads[1]):
+                assert torch.equal(a, c)
+            for a, c in zip(grads[0], grads[2]):  # the hand-off planes are split3_rows' planes bit for bit
                 assert torch.equal(a, c)
         elif mode == "residual":
             r = rnd(M, N, seed=27).requires_grad_(True)
