@@ -363,6 +363,12 @@ int mhada_gemm_tn(const mhada_gemm_tn_args* args, float* work, long long work_fl
  * qkv [L][ntok][3C] (the forward input), dout [L][ntok][C] -> dqkv [L][ntok][3C]; L <= 8. */
 int mhada_vit_batch_attn_bwd(const float* qkv, const float* dout, float* dqkv, int L, int ntok, int heads,
                              int head_dim, mhada_stream_t stream);
+/* The same with dqkv's three bf16 planes written as well (ABI 16): plane p of element e of this call's
+ * dqkv at planes[p * pstride + e] (pstride >= L * ntok * 3C; a grouped call passes its slice of the full
+ * planes): the QKV input-gradient GEMM's SPLIT3 operand in training. */
+int mhada_vit_batch_attn_bwd_split3(const float* qkv, const float* dout, float* dqkv, void* planes,
+                                    long long pstride, int L, int ntok, int heads, int head_dim,
+                                    mhada_stream_t stream);
 
 /* Bias gradients: out[c] = sum_r x[r][c] (x [rows][C] fp32, C % 4 == 0); work >= C floats
  * (up to 1024*C used), fixed-order reduction. */
@@ -374,6 +380,10 @@ int mhada_colsum(const float* x, float* out, long long rows, int C, float* work,
  * cols 256 / 512 / 1024; 16-byte aligned x, y, gamma, beta. */
 int mhada_layernorm_fwd(const float* x, float* y, float* stats, const float* gamma, const float* beta,
                         int rows, int cols, float eps, mhada_stream_t stream);
+/* The same with y's three bf16 planes [3][rows][cols] written as well (ABI 16): the next SPLIT3 linear's
+ * A operand in training (replaces mhada_split3_rows of y). */
+int mhada_layernorm_fwd_split3(const float* x, float* y, void* planes, float* stats, const float* gamma,
+                               const float* beta, int rows, int cols, float eps, mhada_stream_t stream);
 
 /* LayerNorm backward: dx [rows][cols], dgamma / dbeta [cols] (fixed-order sums: per-128-row block
  * partials, then the slab reduction).  work: >= (ceil(rows/128) * 2 + 2) * cols floats. */

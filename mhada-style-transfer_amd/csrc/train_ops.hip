@@ -509,10 +509,13 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x
 //   dx = rstd (g' - mean_c(g') - xh mean_c(g' xh)),  dgamma = sum_rows dy xh,  dbeta = sum_rows dy
 // One wave per row (VPL = cols / 64 values per lane, 16-B column quads as layernorm_kernel).
 // ======================================================================================
+// planes (round 6, may be null): y's three bf16 planes [3][rows][cols] as well — the following SPLIT3
+// linear's operand (train_fns plane hand-off).
 template <int VPL>
 __global__ void __launch_bounds__(256) ln_fwd_train_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                            float* __restrict__ stats, const float* __restrict__ g,
-                                                           const float* __restrict__ b, int rows, float eps) {
+                                                           const float* __restrict__ b, int rows, float eps,
+                                                           bf16* __restrict__ planes) {
   constexpr int COLS = VPL * 64;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -545,6 +548,23 @@ __global__ void __launch_bounds__(256) ln_fwd_train_kernel(const float* __restri
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[4 * i + e] - mean) * rstd * gg[e] + bb[e];
     *reinterpret_cast<f32x4*>(yr + c) = o;
+    if (planes) {
+      const long long ps = (long long)rows * COLS;
+      bf16x4 p0, p1, p2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 a = (bf16)o[e];
+        const float r = o[e] - (float)a;
+        const bf16 q = (bf16)r;
+        p0[e] = a;
+        p1[e] = q;
+        p2[e] = (bf16)(r - (float)q);
+      }
+      bf16* pr = planes + (long long)row * COLS + c;
+      *reinterpret_cast<bf16x4*>(pr) = p0;
+      *reinterpret_cast<bf16x4*>(pr + ps) = p1;
+      *reinterpret_cast<bf16x4*>(pr + 2 * ps) = p2;
+    }
   }
   if (lane == 0) *reinterpret_cast<float2*>(stats + 2LL * row) = make_float2(mean, rstd);
 }
@@ -1003,10 +1023,22 @@ __global__ void __launch_bounds__(256) vgg_input_bwd_kernel(const float* __restr
 // lane = head dim (64); L <= 8 so the score / probability tiles are 8 x 8 (one lane each):
 //   S = (q/8) k^T, P = softmax_j(S), dP = dO v^T, dS = P (dP - rowsum(P dP)),
 //   dq = dS k / 8, dk = dS^T (q/8), dv = P^T dO.   fp32; writes dqkv [L][ntok][3C] (q|k|v).
+// planes (round 6, may be null): dqkv's three bf16 planes as well, plane stride pstride elements from
+// the dqkv base of this call — the QKV input-gradient GEMM's SPLIT3 operand (train_fns plane hand-off).
+MHADA_DEV void store_split3(bf16* p, long long ps, float x) {
+  const bf16 a = (bf16)x;
+  const float r = x - (float)a;
+  const bf16 b = (bf16)r;
+  p[0] = a;
+  p[ps] = b;
+  p[2 * ps] = (bf16)(r - (float)b);
+}
+
 __global__ void __launch_bounds__(256) vit_batch_attn_bwd_kernel(const float* __restrict__ qkv,
                                                                  const float* __restrict__ dout,
                                                                  float* __restrict__ dqkv, int L, int ntok,
-                                                                 int heads) {
+                                                                 int heads, bf16* __restrict__ planes,
+                                                                 long long pstride) {
   constexpr int D = 64;
   __shared__ float sq[4][8][D + 1];
   __shared__ float sk[4][8][D + 1];
@@ -1075,6 +1107,12 @@ __global__ void __launch_bounds__(256) vit_batch_attn_bwd_kernel(const float* __
     obase[r * row3] = dq * 0.125f;
     obase[r * row3 + C] = dk;
     obase[r * row3 + 2 * C] = dv;
+    if (planes) {
+      bf16* pb = planes + (obase - dqkv) + r * row3;
+      store_split3(pb, pstride, dq * 0.125f);
+      store_split3(pb + C, pstride, dk);
+      store_split3(pb + 2 * C, pstride, dv);
+    }
   }
 }
 
@@ -1227,20 +1265,31 @@ extern "C" int mhada_colsum(const float* x, float* out, long long rows, int C, f
   return check_launch("mhada_colsum(reduce)");
 }
 
-extern "C" int mhada_layernorm_fwd(const float* x, float* y, float* stats, const float* gamma, const float* beta,
-                                   int rows, int cols, float eps, mhada_stream_t s_) {
+static int layernorm_fwd_launch(const float* x, float* y, void* planes, float* stats, const float* gamma,
+                                const float* beta, int rows, int cols, float eps, hipStream_t s) {
   if (!x || !y || !stats || !gamma || !beta || rows <= 0) return fail("mhada_layernorm_fwd: bad args");
-  if (!al16(x) || !al16(y) || !al16(gamma) || !al16(beta) || ((uintptr_t)stats & 7))
-    return fail("mhada_layernorm_fwd: x, y, gamma, beta 16-byte aligned, stats 8-byte aligned");
+  if (!al16(x) || !al16(y) || !al16(gamma) || !al16(beta) || ((uintptr_t)stats & 7) || ((uintptr_t)planes & 7))
+    return fail("mhada_layernorm_fwd: x, y, gamma, beta 16-byte aligned, stats and planes 8-byte aligned");
   const dim3 grid((unsigned)((rows + 3) / 4));
-  hipStream_t s = (hipStream_t)s_;
+  bf16* pl = reinterpret_cast<bf16*>(planes);
   switch (cols) {
-    case 256: hipLaunchKernelGGL(ln_fwd_train_kernel<4>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
-    case 512: hipLaunchKernelGGL(ln_fwd_train_kernel<8>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
-    case 1024: hipLaunchKernelGGL(ln_fwd_train_kernel<16>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps); break;
+    case 256: hipLaunchKernelGGL(ln_fwd_train_kernel<4>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps, pl); break;
+    case 512: hipLaunchKernelGGL(ln_fwd_train_kernel<8>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps, pl); break;
+    case 1024: hipLaunchKernelGGL(ln_fwd_train_kernel<16>, grid, dim3(256), 0, s, x, y, stats, gamma, beta, rows, eps, pl); break;
     default: return fail("mhada_layernorm_fwd: cols must be 256, 512 or 1024");
   }
   return check_launch("mhada_layernorm_fwd");
+}
+
+extern "C" int mhada_layernorm_fwd(const float* x, float* y, float* stats, const float* gamma, const float* beta,
+                                   int rows, int cols, float eps, mhada_stream_t s_) {
+  return layernorm_fwd_launch(x, y, nullptr, stats, gamma, beta, rows, cols, eps, (hipStream_t)s_);
+}
+
+extern "C" int mhada_layernorm_fwd_split3(const float* x, float* y, void* planes, float* stats, const float* gamma,
+                                          const float* beta, int rows, int cols, float eps, mhada_stream_t s_) {
+  if (!planes) return fail("mhada_layernorm_fwd_split3: null planes");
+  return layernorm_fwd_launch(x, y, planes, stats, gamma, beta, rows, cols, eps, (hipStream_t)s_);
 }
 
 extern "C" int mhada_layernorm_bwd(const float* x, const float* dy, const float* stats, const float* gamma, float* dx,
@@ -1528,6 +1577,20 @@ extern "C" int mhada_vit_batch_attn_bwd(const float* qkv, const float* dout, flo
   if (head_dim != 64) return fail("mhada_vit_batch_attn_bwd: head_dim must be 64");
   const long long pairs = (long long)ntok * heads;
   hipLaunchKernelGGL(vit_batch_attn_bwd_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, (hipStream_t)s_, qkv,
-                     dout, dqkv, L, ntok, heads);
+                     dout, dqkv, L, ntok, heads, nullptr, 0LL);
   return check_launch("mhada_vit_batch_attn_bwd");
+}
+
+extern "C" int mhada_vit_batch_attn_bwd_split3(const float* qkv, const float* dout, float* dqkv, void* planes,
+                                               long long pstride, int L, int ntok, int heads, int head_dim,
+                                               mhada_stream_t s_) {
+  if (!qkv || !dout || !dqkv || !planes || L <= 0 || L > 8 || ntok <= 0 || heads <= 0)
+    return fail("mhada_vit_batch_attn_bwd_split3: bad args (1 <= L <= 8)");
+  if (head_dim != 64) return fail("mhada_vit_batch_attn_bwd_split3: head_dim must be 64");
+  if (pstride < (long long)L * ntok * 3 * heads * head_dim)
+    return fail("mhada_vit_batch_attn_bwd_split3: plane stride smaller than this call's dqkv");
+  const long long pairs = (long long)ntok * heads;
+  hipLaunchKernelGGL(vit_batch_attn_bwd_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, (hipStream_t)s_, qkv,
+                     dout, dqkv, L, ntok, heads, reinterpret_cast<bf16*>(planes), pstride);
+  return check_launch("mhada_vit_batch_attn_bwd_split3");
 }

@@ -98,11 +98,13 @@ SIGNATURES = {
     "mhada_gemm_tn": (_I, [ctypes.POINTER(GemmTnArgs), _vp, _c_ll, _vp]),
     "mhada_colsum": (_I, [_vp, _vp, _c_ll, _I, _vp, _c_ll, _vp]),
     "mhada_layernorm_fwd": (_I, [_vp, _vp, _vp, _vp, _vp, _I, _I, _F, _vp]),
+    "mhada_layernorm_fwd_split3": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _I, _I, _F, _vp]),
     "mhada_layernorm_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _I, _I, _vp]),
     "mhada_pos_embed_bwd": (_I, [_vp, _vp, _I, _I, _I, _I, _I, _vp]),
     "mhada_instnorm_bwd": (_I, [_vp, _vp, _vp, _vp, _vp, _I, _I, _I, _I, _vp]),
     "mhada_attn_train_bwd_prep": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "mhada_vit_batch_attn_bwd": (_I, [_vp, _vp, _vp, _I, _I, _I, _I, _vp]),
+    "mhada_vit_batch_attn_bwd_split3": (_I, [_vp, _vp, _vp, _vp, _c_ll, _I, _I, _I, _I, _vp]),
     "mhada_relu_bwd": (_I, [_vp, _vp, _vp, _c_ll, _vp]),
     "mhada_feat_stats_work": (_c_ll, [_I, _c_ll, _I]),
     "mhada_feat_stats": (_I, [_vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _I, _c_ll, _I, _vp]),

@@ -59,10 +59,10 @@ def _vit_forward_hip(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor
         att = blk.attention
         heads = att.num_heads
         d = C // heads
-        y = train_fns.layernorm(t.reshape(B * N, C), blk.ln1) if ln_hip else blk.ln1(t).reshape(B * N, C)
+        y = train_fns.layernorm(t.reshape(B * N, C), blk.ln1, 3 * C) if ln_hip else blk.ln1(t).reshape(B * N, C)
         qkv = train_fns.linear(y, att.in_proj_weight, att.in_proj_bias)
         if d == 64 and B // groups <= 8:  # the batch-axis attention core on HIP (L = B keys per token)
-            o = train_fns.BatchAxisAttnFn.apply(qkv.view(B, N, 3 * C), heads, groups).reshape(B * N, C)
+            o = train_fns.BatchAxisAttnFn.apply(qkv, heads, groups, B).reshape(B * N, C)
         else:
             Lg = B // groups
             q, k, v = (z.reshape(groups, Lg, N, heads, d).permute(0, 2, 3, 1, 4)  # (G, N, H, L, d)
@@ -71,7 +71,7 @@ def _vit_forward_hip(vit, x: torch.Tensor, groups: int = 1) -> List[torch.Tensor
             o = torch.matmul(a, v).permute(0, 3, 1, 2, 4).reshape(B * N, C)
         # the residual adds of vit.py:60-61 fused into the out-projection / MLP2 GEMM epilogues
         t = train_fns.linear(o, att.out_proj.weight, att.out_proj.bias, residual=t.reshape(B * N, C)).view(B, N, C)
-        y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2) if ln_hip else blk.ln2(t).reshape(B * N, C)
+        y2 = train_fns.layernorm(t.reshape(B * N, C), blk.ln2, 4 * C) if ln_hip else blk.ln2(t).reshape(B * N, C)
         # MLP1's ReLU adjoint is applied by MLP2's input-gradient GEMM (its only consumer)
         m = train_fns.linear(y2, blk.mlp[0].weight, blk.mlp[0].bias, relu=True, grad_masked=True, planes_out=True)
         t = train_fns.linear(m, blk.mlp[2].weight, blk.mlp[2].bias, relu_input=True,

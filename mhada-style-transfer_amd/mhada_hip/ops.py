@@ -462,8 +462,9 @@ def attn_train_bwd_prep(dout: torch.Tensor, x: torch.Tensor, mo: torch.Tensor):
     return dx, dmo, dd
 
 
-def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float):
-    """``mhada_layernorm_fwd``: fp32 rows [M][C] -> (y fp32, stats [M][2])."""
+def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, planes: bool = False):
+    """``mhada_layernorm_fwd``: fp32 rows [M][C] -> (y fp32, stats [M][2]); ``planes``: also y's three bf16
+    planes [3][M][C] (``mhada_layernorm_fwd_split3``) -> (y, stats, planes)."""
     _need_gpu(x, gamma, beta)
     for t in (x, gamma, beta):
         if t.dtype != torch.float32 or not t.is_contiguous():
@@ -471,6 +472,11 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
     M, C = x.shape
     y = torch.empty_like(x)
     st = torch.empty(M, 2, device=x.device, dtype=torch.float32)
+    if planes:
+        pl = torch.empty(3, M, C, device=x.device, dtype=torch.bfloat16)
+        _call("mhada_layernorm_fwd_split3", x, x.data_ptr(), y.data_ptr(), pl.data_ptr(), st.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), M, C, float(eps))
+        return y, st, pl
     _call("mhada_layernorm_fwd", x, x.data_ptr(), y.data_ptr(), st.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
           M, C, float(eps))
     return y, st
@@ -1130,17 +1136,23 @@ def loss_attn(qn: torch.Tensor, kn: torch.Tensor, v: torch.Tensor, x: torch.Tens
 
 
 def vit_batch_attn_bwd(qkv: torch.Tensor, dout: torch.Tensor, L: int, ntok: int, heads: int,
-                       groups: int = 1) -> torch.Tensor:
+                       groups: int = 1, planes: bool = False):
     """``mhada_vit_batch_attn_bwd``: fp32 qkv [L][ntok][3C], dout [L][ntok][C] -> dqkv (``groups``
-    as in vit_batch_attn)."""
+    as in vit_batch_attn); ``planes``: also dqkv's three bf16 planes [3][L * ntok][3C]
+    (``mhada_vit_batch_attn_bwd_split3``) -> (dqkv, planes)."""
     _need_gpu(qkv, dout)
     C = qkv.shape[-1] // 3
     if L % groups:
         raise ValueError("vit_batch_attn_bwd: L must be a multiple of groups")
     dqkv = torch.empty_like(qkv)
+    pl = torch.empty(3, L * ntok, 3 * C, device=qkv.device, dtype=torch.bfloat16) if planes else None
     Lg = L // groups
     for g in range(groups):
         o3, o1 = g * Lg * ntok * 3 * C * 4, g * Lg * ntok * C * 4
-        _call("mhada_vit_batch_attn_bwd", qkv, qkv.data_ptr() + o3, dout.data_ptr() + o1, dqkv.data_ptr() + o3, Lg,
-              ntok, heads, C // heads)
-    return dqkv
+        if planes:
+            _call("mhada_vit_batch_attn_bwd_split3", qkv, qkv.data_ptr() + o3, dout.data_ptr() + o1,
+                  dqkv.data_ptr() + o3, pl.data_ptr() + o3 // 2, L * ntok * 3 * C, Lg, ntok, heads, C // heads)
+        else:
+            _call("mhada_vit_batch_attn_bwd", qkv, qkv.data_ptr() + o3, dout.data_ptr() + o1, dqkv.data_ptr() + o3,
+                  Lg, ntok, heads, C // heads)
+    return (dqkv, pl) if planes else dqkv

@@ -322,9 +322,16 @@ class LayerNormFn(torch.autograd.Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, x, weight, bias, eps: float):
+    def forward(ctx, x, weight, bias, eps: float, planes_for_n: int = 0):
         x = x.contiguous()
-        y, st = ops.layernorm_fwd(x, weight.detach().contiguous(), bias.detach().contiguous(), eps)
+        # planes_for_n: y feeds a LinearFn with that many outputs — write its SPLIT3 planes here when
+        # that linear runs SPLIT3 (the plane hand-off)
+        M, C = x.shape
+        if planes_for_n and PLANES_HANDOFF_ON and _split3_ok(M, planes_for_n, C, x.device):
+            y, st, pl = ops.layernorm_fwd(x, weight.detach().contiguous(), bias.detach().contiguous(), eps, planes=True)
+            _attach_planes(y, pl)
+        else:
+            y, st = ops.layernorm_fwd(x, weight.detach().contiguous(), bias.detach().contiguous(), eps)
         ctx.save_for_backward(x, st, weight)
         return y
 
@@ -333,11 +340,11 @@ class LayerNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, st, weight = ctx.saved_tensors
         dx, dg, db = ops.layernorm_bwd(x, dy.contiguous(), st, weight.detach().contiguous())
-        return dx, dg, db, None
+        return dx, dg, db, None, None
 
 
-def layernorm(x2d: torch.Tensor, ln: torch.nn.LayerNorm) -> torch.Tensor:
-    return LayerNormFn.apply(x2d, ln.weight, ln.bias, ln.eps)
+def layernorm(x2d: torch.Tensor, ln: torch.nn.LayerNorm, planes_for_n: int = 0) -> torch.Tensor:
+    return LayerNormFn.apply(x2d, ln.weight, ln.bias, ln.eps, planes_for_n)
 
 
 class PosEmbedFn(torch.autograd.Function):
@@ -420,18 +427,29 @@ class BatchAxisAttnFn(torch.autograd.Function):
     mhada_vit_batch_attn_bwd backward."""
 
     @staticmethod
-    def forward(ctx, qkv, heads: int, groups: int = 1):
+    def forward(ctx, qkv, heads: int, groups: int = 1, L: int = 0):
+        """qkv [L][N][3C], or [L N][3C] rows with L given (the QKV LinearFn's own output tensor: its
+        gradient then reaches that LinearFn as the same tensor, carrying the SPLIT3 plane hand-off)."""
         qkv = qkv.contiguous()
-        L, N, _ = qkv.shape
-        ctx.save_for_backward(qkv)
-        ctx.heads, ctx.groups = heads, groups
-        return ops.vit_batch_attn(qkv, L, N, heads, groups)
+        rows2d = qkv.dim() == 2
+        q3 = qkv.view(L, qkv.shape[0] // L, qkv.shape[1]) if rows2d else qkv
+        Lq, N, _ = q3.shape
+        ctx.save_for_backward(q3)
+        ctx.heads, ctx.groups, ctx.rows2d = heads, groups, rows2d
+        return ops.vit_batch_attn(q3, Lq, N, heads, groups)
 
     @staticmethod
     def backward(ctx, gout):
         (qkv,) = ctx.saved_tensors
-        L, N, _ = qkv.shape
-        return ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads, ctx.groups), None, None
+        L, N, C3 = qkv.shape
+        # rows: the producing QKV LinearFn's input-gradient GEMM takes dqkv's planes when it is SPLIT3
+        if ctx.rows2d and PLANES_HANDOFF_ON and _split3_ok(L * N, C3 // 3, C3, qkv.device):
+            dqkv, pl = ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads, ctx.groups, planes=True)
+            dq2 = dqkv.view(L * N, C3)
+            _attach_planes(dq2, pl)
+            return dq2, None, None, None
+        dqkv = ops.vit_batch_attn_bwd(qkv, gout.contiguous(), L, N, ctx.heads, ctx.groups)
+        return (dqkv.view(L * N, C3) if ctx.rows2d else dqkv), None, None, None
 
 
 class PatchEmbedFn(torch.autograd.Function):

@@ -800,3 +800,55 @@ def test_vgg_stem_fn_vs_fp64(B, H, W):
     ref.backward(gy.double().permute(0, 3, 1, 2))
     assert rel(y, ref.permute(0, 2, 3, 1)) < 1e-5
     assert rel(ig.grad, i64.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,C", [(1000, 512), (32768, 512), (77, 256)])
+def test_layernorm_fwd_plane_output_is_split_of_y(M, C):
+    """mhada_layernorm_fwd_split3 (round 6): y bit-identical to mhada_layernorm_fwd and the planes exactly
+    split3_rows(y) — the QKV / MLP1 SPLIT3 operand handed over by LayerNormFn."""
+    x, g, b = rnd(M, C, seed=71), rnd(C, seed=72), rnd(C, seed=73)
+    y0, st0 = ops.layernorm_fwd(x, g, b, 1e-6)
+    y, st, pl = ops.layernorm_fwd(x, g, b, 1e-6, planes=True)
+    assert torch.equal(y, y0) and torch.equal(st, st0)
+    assert torch.equal(pl, ops.split3_rows(y))
+
+
+@pytest.mark.parametrize("L,N,groups", [(8, 300, 1), (16, 129, 2), (3, 64, 1)])
+def test_vit_batch_attn_bwd_plane_output_is_split_of_dqkv(L, N, groups):
+    """mhada_vit_batch_attn_bwd_split3 (round 6): dqkv bit-identical to mhada_vit_batch_attn_bwd and the
+    planes exactly split3_rows(dqkv), also when a grouped call writes its slice of the planes."""
+    heads, C = 8, 512
+    qkv, dout = rnd(L, N, 3 * C, seed=81), rnd(L, N, C, seed=82)
+    d0 = ops.vit_batch_attn_bwd(qkv, dout, L, N, heads, groups)
+    d, pl = ops.vit_batch_attn_bwd(qkv, dout, L, N, heads, groups, planes=True)
+    assert torch.equal(d, d0)
+    assert torch.equal(pl, ops.split3_rows(d.view(L * N, 3 * C)))
+
+
+def test_vit_training_plane_handoffs_are_bit_identical():
+    """The ViT training path at the 512^2 B8 batched-call size (32768 tokens: every linear SPLIT3) with the
+    SPLIT3 plane hand-offs (LayerNorm -> QKV / MLP1, MLP1 -> MLP2, and backward the batch-axis attention ->
+    QKV, MLP2 -> MLP1) against every linear splitting its own operand: outputs and every gradient bit for
+    bit, and the hand-offs actually taken."""
+    import network
+    from mhada_hip import autograd_path
+    from mhada_hip.recipe import load_recipe
+    vit = load_recipe(network.VisionTransformer(pos_embedding=True), "vit_c").to(DEV).train()
+    x = (rnd(8, 3, 512, 512, seed=91) * 40 + 128)
+    res = []
+    for on in (True, False):
+        train_fns.PLANES_HANDOFF_ON = on
+        try:
+            vit.zero_grad(set_to_none=True)
+            used = train_fns.PLANES_HANDOFF["used"]
+            outs = autograd_path.vit_forward(vit, x)
+            loss = sum((o * rnd(*o.shape, seed=92 + i)).sum() for i, o in enumerate(outs))
+            loss.backward()
+            res.append(([o.detach().clone() for o in outs], [p.grad.clone() for p in vit.parameters()],
+                        train_fns.PLANES_HANDOFF["used"] - used))
+        finally:
+            train_fns.PLANES_HANDOFF_ON = True
+    (o1, g1, u1), (o0, g0, u0) = res
+    assert u0 == 0 and u1 == 3 * 5  # per layer: LN1 -> QKV, LN2 -> MLP1, MLP1 -> MLP2, attn -> QKV, MLP2 -> MLP1
+    for a, b in zip(o1 + g1, o0 + g0):
+        assert torch.equal(a, b)
