@@ -32,12 +32,16 @@ def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item()
 
 
+@pytest.mark.parametrize("dq", ["s3", "f32"])
 @pytest.mark.parametrize("form", ["s3", "vt"])
 @pytest.mark.parametrize("BH,Nc,Ns,scale", [(2, 128, 64, 0.4), (3, 100, 70, 0.4), (1, 37, 300, 0.6),
-                                            (2, 256, 129, 1.5)])
-def test_attn_train_fwd_bwd_vs_fp64(monkeypatch, form, BH, Nc, Ns, scale):
+                                            (2, 256, 129, 1.5), (2, 200, 160, 1.0)])
+def test_attn_train_fwd_bwd_vs_fp64(monkeypatch, dq, form, BH, Nc, Ns, scale):
+    """Forward + backward through MHAdaAttnFn for both training forwards and both dQ GEMMs (the SPLIT3
+    one takes Ns % 32 == 0: Ns = 64, 160 here; the others fall back to the fp32 GEMM either way)."""
     monkeypatch.setattr(ops, "TRAIN_FWD_S3", form == "s3")
     monkeypatch.setattr(ops, "TRAIN_FWD_VT", True)
+    monkeypatch.setattr(ops, "TRAIN_DQ_S3", dq == "s3")
     g = torch.Generator().manual_seed(Nc * 7 + Ns)
     q = torch.randn(BH, Nc, 64, generator=g) * scale
     k = torch.randn(BH, Ns, 64, generator=g) * scale
