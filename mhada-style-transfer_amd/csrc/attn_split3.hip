@@ -406,7 +406,11 @@ MHADA_DEV void attn_train_epilogue_q(const AttnP& p, const f32x4 (&O)[2][8], con
 // group g's 16 MFMA steps are 64 contiguous bytes) in the K-plane region of the plane image; in LDS the
 // 16-B chunk c of key row k at slot c ^ f(k & 7), f(k) = (k & 3) | (k >> 2) << 3 (the 16 lanes of a
 // ds_read_b128 group then hit 16 distinct slots).
-template <int NW, bool TRAIN = false, bool QK32 = false, int ACC = 0>
+// IL 1 (the inference kernel, ACC 0): key group 1's exp / split interleaved with key group 0's P V
+// MFMAs — bit-identical, 1.6-3.4 % faster at the bench shapes than the two groups in sequence
+// (tools/attn_s3_variants_interleaved.py, profiles/r06_attn_s3_interleave_ab.log; a full-tile
+// interleave with the Q K^T of group 1 beside the split of group 0 measured no better).
+template <int NW, bool TRAIN = false, bool QK32 = false, int ACC = 0, int IL = 0>
 __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   constexpr int TK = kS3Tk;
   constexpr int KPL = TK * 64, VPL = 128 * TK;                // bf16 elements per plane
@@ -532,8 +536,48 @@ __global__ void __launch_bounds__(64 * NW, 1) attn_s3_kernel(const AttnP p) {
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  // ACC 0 building blocks of the interleaved forms (IL): P V' / P V'^2 of one key group and row block,
+  // and one key group's row sums
+  auto pv = [&](int sl, int kg, int dvb, const bf16x8 (&pf)[3][2]) {
+    const int off = 8 * ((4 * kg + g) ^ ((r16 >> 1) & 7));
+    const bf16* vr = smem + sl * SLOT + KREG + (16 * dvb + r16) * TK + off;
+    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vr);
+    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vr + VPL);
+    const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vr + 2 * VPL);
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) O[qg][dvb] = mfma6(v0, v1, v2, pf[0][qg], pf[1][qg], pf[2][qg], O[qg][dvb]);
+  };
+  auto rowsum = [&](const bf16x8 (&pf)[3][2]) {
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[2][qg], L[qg], 0, 0, 0);
+      L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[1][qg], L[qg], 0, 0, 0);
+      L[qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[0][qg], L[qg], 0, 0, 0);
+    }
+  };
   auto finish = [&](int sl, const f32x4 (&S)[2][2][2]) {
     const bf16* cv = smem + sl * SLOT + KREG;
+    if constexpr (IL != 0 && ACC == 0) {
+      // the exp / split of key group 1 interleaved with key group 0's P V MFMAs (two scores per row
+      // block), so this wave's VALU burst no longer runs beside an idle matrix pipe
+      bf16x8 pa[3][2], pb[3][2];
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3_into(fast_exp2(S[qg][0][j >> 2][j & 3]), pa[0][qg], pa[1][qg], pa[2][qg], j);
+      rowsum(pa);
+#pragma unroll
+      for (int dvb = 0; dvb < 8; ++dvb) {
+        pv(sl, 0, dvb, pa);
+        const int qg = dvb >> 2, j = 2 * (dvb & 3);
+        split3_into(fast_exp2(S[qg][1][j >> 2][j & 3]), pb[0][qg], pb[1][qg], pb[2][qg], j);
+        split3_into(fast_exp2(S[qg][1][(j + 1) >> 2][(j + 1) & 3]), pb[0][qg], pb[1][qg], pb[2][qg], j + 1);
+      }
+      rowsum(pb);
+#pragma unroll
+      for (int dvb = 0; dvb < 8; ++dvb) pv(sl, 1, dvb, pb);
+      return;
+    }
 #pragma unroll
     for (int kg = 0; kg < 2; ++kg) {
       bf16x8 pf[3][2];
@@ -697,8 +741,8 @@ extern "C" int mhada_attn_split3(const float* q, const void* img, const float* f
   if (nblk > (1LL << 31) - 1) return fail("mhada_attn_split3: grid too large");
   p.nblk = (int)nblk;
   const hipStream_t s = (hipStream_t)s_;
-  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8>), dim3(p.nblk), dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((attn_s3_kernel<4>), dim3(p.nblk), dim3(256), 0, s, p);
+  if (nw == 8) hipLaunchKernelGGL((attn_s3_kernel<8, false, false, 0, 1>), dim3(p.nblk), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((attn_s3_kernel<4, false, false, 0, 1>), dim3(p.nblk), dim3(256), 0, s, p);
   return check_launch("mhada_attn_split3");
 }
 
